@@ -1,0 +1,570 @@
+// Dense 2-D convolutions of the StyleGAN2 G/D on MFMA (gfx950), NHWC activations.
+//
+// Replaces the cuDNN convolutions the reference reaches through
+// SG3/torch_utils/ops/conv2d_resample.py:29-41 -> conv2d_gradfix.py:37-45 (F.conv2d,
+// F.conv_transpose2d) and their autograd weight gradients.
+//
+// Forward / data-gradient: implicit GEMM.  M = output pixels of one output phase, N = Cout,
+// K = taps x Cin.  A transposed stride-S convolution is split into S*S output phases; inside a phase
+// every output pixel uses the same taps, so the GEMM has no zero-inserted work
+// (2*N*Cout*Cin*KH*KW*H*W FLOPs in total, the SURVEY 8(d) count).
+//   A[m][k] = x[n, q*is + tap.dy, q*is + tap.dx, c]     (gathered, zero outside the image)
+//   B[k][o] = w[o][tap][c]                               (packed weight, K-contiguous per o)
+// Block tile BM x BN, 4 waves in 2 x 2, each wave (BM/2) x (BN/2) of 16x16 MFMA tiles:
+//   f16/bf16: v_mfma_f32_16x16x32_{f16,bf16}, K-stage 32 elements
+//   f32     : v_mfma_f32_16x16x4_f32 (exact f32), K-stage 16 elements
+// Both operand tiles are register-staged global->LDS with two LDS buffers: the next stage's 16-byte
+// global loads are issued before the current stage's MFMAs, and written to the other buffer after.
+// Small-M layers (low resolutions) split K over blocks and reduce with f32 atomics.
+//
+// Weight gradient: dw[a][tap][b] = sum_m g[m][a] * x[in(m,tap)][b]; GEMM over K = pixels with both
+// operands pixel-major in LDS; the 16-bit fragments are read with ds_read_b64_tr_b16 (hardware
+// transpose), f32 fragments with plain ds_read_b32.  Split over pixels, f32 atomic reduction.
+#include "sg2_common.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace sg2 {
+namespace {
+
+constexpr int kMaxTaps = 16;
+
+struct TapTable {
+    int n;
+    int dy[kMaxTaps], dx[kMaxTaps], w[kMaxTaps];
+};
+
+struct ConvArgs {
+    const void* x;
+    const void* w;
+    void* y;       // T output (non-split)
+    float* acc;    // f32 output for split-K (zeroed)
+    int N, H, W, Cin, Cout, OH, OW;
+    int QH, QW, M;           // phase grid, M = N*QH*QW
+    int osy, osx, oy0, ox0;  // output coordinate = q*os + o0
+    int isy, isx;            // input coordinate  = q*is + tap.d
+    int wtaps;               // taps per output channel in the packed weight (KH*KW)
+    int nck;                 // ceil(Cin / BK)
+    int nk;                  // taps.n * nck
+    int kper;                // K-chunks per split
+    TapTable taps;
+};
+
+template <typename T> struct Traits;
+template <> struct Traits<float> {
+    static constexpr int BK = 16, V = 4;
+};
+template <> struct Traits<f16_t> {
+    static constexpr int BK = 32, V = 8;
+};
+template <> struct Traits<bf16_t> {
+    static constexpr int BK = 32, V = 8;
+};
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+template <typename T>
+using v8_t = typename std::conditional<std::is_same<T, bf16_t>::value, bf16x8, f16x8>::type;
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16v(v8_t<T> a, v8_t<T> b, f32x4 c) {
+    if constexpr (std::is_same<T, bf16_t>::value)
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16(const T* pa, const T* pb, f32x4 c) {
+    if constexpr (std::is_same<T, bf16_t>::value) {
+        bf16x8 a = *(const bf16x8*)pa, b = *(const bf16x8*)pb;
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    } else {
+        f16x8 a = *(const f16x8*)pa, b = *(const f16x8*)pb;
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+}
+
+template <typename T, bool VEC>
+struct Loader {
+    // A 16-byte (or masked scalar) chunk of one tile row.
+    typedef T vecT __attribute__((ext_vector_type(Traits<T>::V)));
+    static __device__ __forceinline__ vecT load(const T* row, int c, int Cin, bool valid) {
+        constexpr int V = Traits<T>::V;
+        vecT v;
+        if (VEC) {
+            if (valid && c < Cin) return *(const vecT*)(row + c);
+#pragma unroll
+            for (int j = 0; j < V; ++j) v[j] = (T)0.f;
+            return v;
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[j] = (valid && c + j < Cin) ? row[c + j] : (T)0.f;
+        return v;
+    }
+};
+
+template <typename T, int BM, int BN, bool VEC, bool SPLIT>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
+    constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
+    constexpr int LPR = BK / V;          // lanes per tile row
+    constexpr int RPP = 256 / LPR;       // rows per load pass
+    constexpr int PA = BM / RPP, PB = BN / RPP;
+    constexpr int LDK = BK + V;          // padded LDS row (16 B pad)
+    constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+    typedef typename Loader<T, VEC>::vecT vecT;
+
+    __shared__ __attribute__((aligned(16))) T lds[2][(BM + BN) * LDK];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const T* __restrict__ x = (const T*)a.x;
+    const T* __restrict__ w = (const T*)a.w;
+
+    // --- per-thread load geometry (fixed across K) ---
+    const int lrow = tid / LPR, lcol = (tid % LPR) * V;
+    int a_n[PA], a_qy[PA], a_qx[PA];
+    bool a_ok[PA];
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+        const int m = m0 + lrow + i * RPP;
+        a_ok[i] = m < a.M;
+        const int mm = a_ok[i] ? m : 0;
+        const int per = a.QH * a.QW;
+        a_n[i] = mm / per;
+        const int r = mm - a_n[i] * per;
+        a_qy[i] = (r / a.QW) * a.isy;
+        a_qx[i] = (r % a.QW) * a.isx;
+    }
+    const int64_t wrow = (int64_t)a.wtaps * a.Cin;
+
+    const int k_begin = blockIdx.z * a.kper;
+    const int k_end = min(a.nk, k_begin + a.kper);
+
+    vecT ra[PA], rb[PB];
+    auto gload = [&](int kc) {
+        const int t = kc / a.nck;
+        const int c = (kc - t * a.nck) * BK + lcol;
+        const int dy = a.taps.dy[t], dx = a.taps.dx[t], wt = a.taps.w[t];
+#pragma unroll
+        for (int i = 0; i < PA; ++i) {
+            const int iy = a_qy[i] + dy, ix = a_qx[i] + dx;
+            const bool ok = a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            const T* row = x + (((int64_t)a_n[i] * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.Cin;
+            ra[i] = Loader<T, VEC>::load(row, c, a.Cin, ok);
+        }
+#pragma unroll
+        for (int i = 0; i < PB; ++i) {
+            const int o = n0 + lrow + i * RPP;
+            const bool ok = o < a.Cout;
+            const T* row = w + (ok ? o : 0) * wrow + (int64_t)wt * a.Cin;
+            rb[i] = Loader<T, VEC>::load(row, c, a.Cin, ok);
+        }
+    };
+    auto sstore = [&](int buf) {
+        T* As = lds[buf];
+        T* Bs = lds[buf] + BM * LDK;
+#pragma unroll
+        for (int i = 0; i < PA; ++i) *(vecT*)(As + (lrow + i * RPP) * LDK + lcol) = ra[i];
+#pragma unroll
+        for (int i = 0; i < PB; ++i) *(vecT*)(Bs + (lrow + i * RPP) * LDK + lcol) = rb[i];
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (k_begin < k_end) {
+        gload(k_begin);
+        sstore(0);
+        __syncthreads();
+        for (int kc = k_begin; kc < k_end; ++kc) {
+            const int cur = (kc - k_begin) & 1;
+            const bool more = kc + 1 < k_end;
+            if (more) gload(kc + 1);
+            const T* As = lds[cur] + (wm * WM) * LDK;
+            const T* Bs = lds[cur] + BM * LDK + (wn * WN) * LDK;
+            if constexpr (std::is_same<T, float>::value) {
+#pragma unroll
+                for (int kk = 0; kk < BK; kk += 4) {
+                    float af[TM], bfr[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) af[i] = As[(i * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) bfr[j] = Bs[(j * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                }
+            } else {
+                const int ko = 8 * (lane >> 4);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = mfma16<T>(As + (i * 16 + (lane & 15)) * LDK + ko,
+                                              Bs + (j * 16 + (lane & 15)) * LDK + ko, acc[i][j]);
+            }
+            if (more) sstore(cur ^ 1);
+            __syncthreads();
+        }
+    }
+
+    // --- epilogue ---
+    const int per = a.QH * a.QW;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + r;
+            if (m >= a.M) continue;
+            const int n = m / per;
+            const int rr = m - n * per;
+            const int oy = (rr / a.QW) * a.osy + a.oy0, ox = (rr % a.QW) * a.osx + a.ox0;
+            const int64_t obase = (((int64_t)n * a.OH + oy) * a.OW + ox) * a.Cout;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int o = n0 + wn * WN + j * 16 + (lane & 15);
+                if (o >= a.Cout) continue;
+                if (SPLIT)
+                    atomicAdd(a.acc + obase + o, acc[i][j][r]);
+                else
+                    ((T*)a.y)[obase + o] = (T)acc[i][j][r];
+            }
+        }
+    }
+}
+
+template <typename T>
+__global__ void f32_to_t_kernel(T* y, const float* src, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = (T)src[i];
+}
+
+template <typename T, int BM, int BN>
+int launch_fwd(ConvArgs& a, bool vec, int splits, hipStream_t s) {
+    dim3 grid((unsigned)cdiv(a.M, BM), (unsigned)cdiv(a.Cout, BN), (unsigned)splits);
+    a.kper = (int)cdiv(a.nk, splits);
+    if (splits > 1) {
+        if (vec) conv_fwd_kernel<T, BM, BN, true, true><<<grid, 256, 0, s>>>(a);
+        else conv_fwd_kernel<T, BM, BN, false, true><<<grid, 256, 0, s>>>(a);
+    } else {
+        if (vec) conv_fwd_kernel<T, BM, BN, true, false><<<grid, 256, 0, s>>>(a);
+        else conv_fwd_kernel<T, BM, BN, false, false><<<grid, 256, 0, s>>>(a);
+    }
+    return launch_status("sg2_conv2d");
+}
+
+// ------------------------------------------------------------------------------------ wgrad
+
+struct WgradArgs {
+    const void* g;   // [N, OH, OW, A]
+    const void* x;   // [N, H, W, B]
+    float* dw;       // [A][KK][B]
+    int N, A, OH, OW, B, H, W, KH, KW, stride, pady, padx;
+    int M;           // N*OH*OW
+    int kper;        // pixels per split (multiple of BK)
+    int splits;
+};
+
+template <typename T>
+__device__ __forceinline__ v8_t<T> frag_tr(const T* base, int ld, int k0, int c0, int lane) {
+    // element j = base[(k0 + 8*(lane>>4) + j) * ld + c0 + (lane & 15)],  j = 0..7  (ds_read_b64_tr_b16)
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const T* p0 = base + (k0 + 8 * g + q) * ld + c0 + 4 * p;
+    const T* p1 = p0 + 4 * ld;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p1);
+    s16x8 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(v8_t<T>, r);
+}
+
+template <typename T, int BM, int BN, bool VEC>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+    constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
+    constexpr int LDA = BM + V, LDB = BN + V;   // padded pixel-major rows
+    constexpr int LPA = BM / V, LPB = BN / V;   // lanes per row
+    constexpr int RPA = 256 / LPA, RPB = 256 / LPB;
+    constexpr int PA = (BK + RPA - 1) / RPA, PB = (BK + RPB - 1) / RPB;
+    constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+    typedef typename Loader<T, VEC>::vecT vecT;
+
+    __shared__ __attribute__((aligned(16))) T lds[2][BK * (LDA + LDB)];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int a0 = blockIdx.x * BM, b0 = blockIdx.y * BN;
+    const int tap = blockIdx.z / a.splits, split = blockIdx.z % a.splits;
+    const int ky = tap / a.KW, kx = tap % a.KW;
+    const T* __restrict__ g = (const T*)a.g;
+    const T* __restrict__ x = (const T*)a.x;
+
+    const int ga_row = tid / LPA, ga_col = (tid % LPA) * V;
+    const int xb_row = tid / LPB, xb_col = (tid % LPB) * V;
+    const int p_begin = split * a.kper;
+    const int p_end = min(a.M, p_begin + a.kper);
+
+    vecT ra[PA], rb[PB];
+    auto gload = [&](int p0) {
+#pragma unroll
+        for (int i = 0; i < PA; ++i) {
+            const int r = ga_row + i * RPA;
+            const int m = p0 + r;
+            const bool ok = r < BK && m < p_end;
+            const T* row = g + (int64_t)(ok ? m : 0) * a.A;
+            ra[i] = Loader<T, VEC>::load(row, a0 + ga_col, a.A, ok);
+        }
+#pragma unroll
+        for (int i = 0; i < PB; ++i) {
+            const int r = xb_row + i * RPB;
+            const int m = p0 + r;
+            bool ok = r < BK && m < p_end;
+            int n = 0, iy = 0, ix = 0;
+            if (ok) {
+                const int per = a.OH * a.OW;
+                n = m / per;
+                const int rr = m - n * per;
+                iy = (rr / a.OW) * a.stride + ky - a.pady;
+                ix = (rr % a.OW) * a.stride + kx - a.padx;
+                ok = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            }
+            const T* row = x + (((int64_t)n * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.B;
+            rb[i] = Loader<T, VEC>::load(row, b0 + xb_col, a.B, ok);
+        }
+    };
+    auto sstore = [&](int buf) {
+        T* As = lds[buf];
+        T* Bs = lds[buf] + BK * LDA;
+#pragma unroll
+        for (int i = 0; i < PA; ++i) {
+            const int r = ga_row + i * RPA;
+            if (r < BK) *(vecT*)(As + r * LDA + ga_col) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < PB; ++i) {
+            const int r = xb_row + i * RPB;
+            if (r < BK) *(vecT*)(Bs + r * LDB + xb_col) = rb[i];
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (p_begin < p_end) {
+        gload(p_begin);
+        sstore(0);
+        __syncthreads();
+        int it = 0;
+        for (int p0 = p_begin; p0 < p_end; p0 += BK, ++it) {
+            const int cur = it & 1;
+            const bool more = p0 + BK < p_end;
+            if (more) gload(p0 + BK);
+            const T* As = lds[cur];
+            const T* Bs = lds[cur] + BK * LDA;
+            if constexpr (std::is_same<T, float>::value) {
+#pragma unroll
+                for (int kk = 0; kk < BK; kk += 4) {
+                    float af[TM], bfr[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) af[i] = As[(kk + (lane >> 4)) * LDA + wm * WM + i * 16 + (lane & 15)];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) bfr[j] = Bs[(kk + (lane >> 4)) * LDB + wn * WN + j * 16 + (lane & 15)];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                }
+            } else {
+                v8_t<T> af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) af[i] = frag_tr<T>(As, LDA, 0, wm * WM + i * 16, lane);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bfr[j] = frag_tr<T>(Bs, LDB, 0, wn * WN + j * 16, lane);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma16v<T>(af[i], bfr[j], acc[i][j]);
+            }
+            if (more) sstore(cur ^ 1);
+            __syncthreads();
+        }
+    }
+
+    const int KK = a.KH * a.KW;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int ar = a0 + wm * WM + i * 16 + 4 * (lane >> 4) + r;
+            if (ar >= a.A) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int bc = b0 + wn * WN + j * 16 + (lane & 15);
+                if (bc < a.B) atomicAdd(a.dw + ((int64_t)ar * KK + tap) * a.B + bc, acc[i][j][r]);
+            }
+        }
+}
+
+template <typename T, int BM, int BN>
+int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
+    constexpr int BK = Traits<T>::BK;
+    const int mt = (int)cdiv(a.A, BM), nt = (int)cdiv(a.B, BN);
+    const int KK = a.KH * a.KW;
+    const int chunks = (int)cdiv(a.M, BK);
+    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(chunks / 8, cdiv(2048, (int64_t)mt * nt * KK)));
+    a.kper = (int)cdiv(chunks, splits) * BK;
+    a.splits = (int)cdiv(a.M, a.kper);
+    dim3 grid(mt, nt, KK * a.splits);
+    if (vec) conv_wgrad_kernel<T, BM, BN, true><<<grid, 256, 0, s>>>(a);
+    else conv_wgrad_kernel<T, BM, BN, false><<<grid, 256, 0, s>>>(a);
+    return launch_status("sg2_conv2d_wgrad");
+}
+
+int floordiv_h(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+}  // namespace
+}  // namespace sg2
+
+extern "C" int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W, int Cout,
+                          int OH, int OW, int KH, int KW, int stride, int pad_y, int pad_x, int transpose,
+                          float* workspace, int64_t workspace_elems, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(y && x && w, "sg2_conv2d: null pointer");
+    SG2_CHECK(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0 && OH > 0 && OW > 0, "sg2_conv2d: empty shape");
+    SG2_CHECK(KH >= 1 && KW >= 1 && KH * KW <= kMaxTaps, "sg2_conv2d: kernel too large");
+    SG2_CHECK(stride >= 1 && stride <= 4, "sg2_conv2d: unsupported stride");
+    SG2_CHECK((int64_t)N * OH * OW * Cout < INT32_MAX && (int64_t)N * H * W * Cin < ((int64_t)1 << 40),
+              "sg2_conv2d: tensor too large");
+    hipStream_t s = as_stream(stream);
+
+    // Output phases.
+    struct Phase { ConvArgs a; };
+    Phase ph[16];
+    int nph = 0;
+    ConvArgs base{};
+    base.x = x; base.w = w; base.y = y; base.acc = nullptr;
+    base.N = N; base.H = H; base.W = W; base.Cin = Cin; base.Cout = Cout; base.OH = OH; base.OW = OW;
+    base.wtaps = KH * KW;
+    if (!transpose) {
+        ConvArgs a = base;
+        a.QH = OH; a.QW = OW; a.osy = a.osx = 1; a.oy0 = a.ox0 = 0; a.isy = a.isx = stride;
+        SG2_CHECK((int64_t)(OH - 1) * stride - pad_y + KH - 1 >= 0, "sg2_conv2d: bad geometry");
+        a.taps.n = 0;
+        for (int ky = 0; ky < KH; ++ky)
+            for (int kx = 0; kx < KW; ++kx) {
+                a.taps.dy[a.taps.n] = ky - pad_y;
+                a.taps.dx[a.taps.n] = kx - pad_x;
+                a.taps.w[a.taps.n] = ky * KW + kx;
+                a.taps.n++;
+            }
+        ph[nph++].a = a;
+    } else {
+        // y[oy] = sum_{iy,ky: oy = iy*S + ky - P} x[iy] w[ky]  ->  phase py = oy mod S
+        for (int py = 0; py < stride; ++py)
+            for (int px = 0; px < stride; ++px) {
+                ConvArgs a = base;
+                a.QH = (OH - py + stride - 1) / stride;
+                a.QW = (OW - px + stride - 1) / stride;
+                if (a.QH <= 0 || a.QW <= 0) continue;
+                a.osy = a.osx = stride; a.oy0 = py; a.ox0 = px; a.isy = a.isx = 1;
+                a.taps.n = 0;
+                for (int ky = 0; ky < KH; ++ky) {
+                    const int ny = py + pad_y - ky;
+                    if (((ny % stride) + stride) % stride) continue;
+                    for (int kx = 0; kx < KW; ++kx) {
+                        const int nx = px + pad_x - kx;
+                        if (((nx % stride) + stride) % stride) continue;
+                        a.taps.dy[a.taps.n] = floordiv_h(ny, stride);
+                        a.taps.dx[a.taps.n] = floordiv_h(nx, stride);
+                        a.taps.w[a.taps.n] = ky * KW + kx;
+                        a.taps.n++;
+                    }
+                }
+                ph[nph++].a = a;
+            }
+    }
+
+    int rc = 0;
+    SG2_DISPATCH(dtype, T, {
+        constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
+        const bool vec = (Cin % V == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)w % 16 == 0);
+        const bool wide = Cout > 64;
+        // split-K when the grid is too small to fill 256 CUs
+        int64_t blocks = 0;
+        int64_t minnk = INT32_MAX;
+        for (int i = 0; i < nph; ++i) {
+            ConvArgs& a = ph[i].a;
+            a.M = N * a.QH * a.QW;
+            a.nck = (Cin + BK - 1) / BK;
+            a.nk = a.taps.n * a.nck;
+            blocks += cdiv(a.M, wide ? 128 : 128) * cdiv(Cout, wide ? 128 : 64);
+            minnk = std::min<int64_t>(minnk, std::max(1, a.nk));
+        }
+        int splits = 1;
+        const int64_t total_out = (int64_t)N * OH * OW * Cout;
+        if (blocks < 512 && workspace != nullptr && workspace_elems >= total_out)
+            splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(1024, blocks), minnk / 4));
+        const bool split = splits > 1;
+        if (split) {
+            hipError_t e = hipMemsetAsync(workspace, 0, total_out * sizeof(float), s);
+            if (e != hipSuccess) { set_error("sg2_conv2d: memset failed"); return (int)e; }
+        } else if (transpose) {
+            // phases with no taps produce zeros
+            for (int i = 0; i < nph; ++i)
+                if (ph[i].a.taps.n == 0) {
+                    hipError_t e = hipMemsetAsync(y, 0, total_out * sizeof(T), s);
+                    if (e != hipSuccess) { set_error("sg2_conv2d: memset failed"); return (int)e; }
+                    break;
+                }
+        }
+        for (int i = 0; i < nph && rc == 0; ++i) {
+            ConvArgs& a = ph[i].a;
+            a.acc = split ? workspace : nullptr;
+            if (a.taps.n == 0) continue;
+            if (wide) rc = launch_fwd<T, 128, 128>(a, vec, split ? splits : 1, s);
+            else rc = launch_fwd<T, 128, 64>(a, vec, split ? splits : 1, s);
+        }
+        if (rc == 0 && split) {
+            const int g = (int)std::min<int64_t>(cdiv(total_out, 256), 4096);
+            f32_to_t_kernel<T><<<g, 256, 0, s>>>((T*)y, workspace, total_out);
+            rc = launch_status("sg2_conv2d finalize");
+        }
+    });
+    return rc;
+}
+
+extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
+                                int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(dw && g && x, "sg2_conv2d_wgrad: null pointer");
+    SG2_CHECK(N > 0 && A > 0 && B > 0 && OH > 0 && OW > 0 && H > 0 && W > 0, "sg2_conv2d_wgrad: empty shape");
+    SG2_CHECK(KH >= 1 && KW >= 1 && KH * KW <= 64, "sg2_conv2d_wgrad: kernel too large");
+    hipStream_t s = as_stream(stream);
+    hipError_t e = hipMemsetAsync(dw, 0, (int64_t)A * KH * KW * B * sizeof(float), s);
+    if (e != hipSuccess) { set_error("sg2_conv2d_wgrad: memset failed"); return (int)e; }
+    WgradArgs a{};
+    a.g = g; a.x = x; a.dw = dw;
+    a.N = N; a.A = A; a.OH = OH; a.OW = OW; a.B = B; a.H = H; a.W = W; a.KH = KH; a.KW = KW;
+    a.stride = stride; a.pady = pad_y; a.padx = pad_x;
+    a.M = N * OH * OW;
+    int rc = 0;
+    SG2_DISPATCH(dtype, T, {
+        constexpr int V = Traits<T>::V;
+        const bool vec = (A % V == 0) && (B % V == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)g % 16 == 0);
+        if (A > 64 && B > 64) rc = launch_wgrad<T, 128, 128>(a, vec, s);
+        else if (A > 64) rc = launch_wgrad<T, 128, 64>(a, vec, s);
+        else if (B > 64) rc = launch_wgrad<T, 64, 128>(a, vec, s);
+        else rc = launch_wgrad<T, 64, 64>(a, vec, s);
+    });
+    return rc;
+}

@@ -1,0 +1,143 @@
+// Bilinear grid sampling (zeros padding, align_corners = False) and its input gradient.
+// Replaces aten::grid_sampler_2d / grid_sampler_2d_backward as used by
+// SG3/torch_utils/ops/grid_sample_gradfix.py:28-83 inside the ADA pipe (augment_mi.py:317-318).
+// The gradient w.r.t. the grid is never needed on the training path (the grid is built from
+// random augmentation parameters), and the backward-of-backward is the forward itself.
+//
+// One lane per output pixel; the four corner weights are computed once and reused across channels.
+// Backward scatters with float atomics into a float32 buffer (images are 1-3 channels, so the
+// atomic traffic is ~4 x 4 B per output pixel per channel).
+#include "sg2_common.h"
+
+namespace sg2 {
+namespace {
+
+struct GSParams {
+    const void* in;
+    void* out;
+    const float* grid;
+    int N, C, Hi, Wi, Ho, Wo;
+    int64_t is_n, is_c, is_h, is_w;
+    int64_t os_n, os_c, os_h, os_w;
+};
+
+struct Corners {
+    int x0, y0;
+    float w00, w01, w10, w11;  // w[yy][xx]
+};
+
+__device__ __forceinline__ Corners corners(const GSParams& p, int n, int oy, int ox) {
+    const float* g = p.grid + (((int64_t)n * p.Ho + oy) * p.Wo + ox) * 2;
+    const float ix = ((g[0] + 1.f) * p.Wi - 1.f) * 0.5f;
+    const float iy = ((g[1] + 1.f) * p.Hi - 1.f) * 0.5f;
+    Corners c;
+    const float fx = floorf(ix), fy = floorf(iy);
+    c.x0 = (int)fx;
+    c.y0 = (int)fy;
+    const float ax = ix - fx, ay = iy - fy;
+    const float bx = (fx + 1.f) - ix, by = (fy + 1.f) - iy;
+    c.w00 = bx * by;
+    c.w01 = ax * by;
+    c.w10 = bx * ay;
+    c.w11 = ax * ay;
+    return c;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void grid_sample_fwd_kernel(GSParams p) {
+    const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
+    const T* in = (const T*)p.in;
+    T* out = (T*)p.out;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int ox = (int)(idx % p.Wo);
+        const int oy = (int)((idx / p.Wo) % p.Ho);
+        const int n = (int)(idx / ((int64_t)p.Wo * p.Ho));
+        const Corners k = corners(p, n, oy, ox);
+        const bool vx0 = k.x0 >= 0 && k.x0 < p.Wi, vx1 = k.x0 + 1 >= 0 && k.x0 + 1 < p.Wi;
+        const bool vy0 = k.y0 >= 0 && k.y0 < p.Hi, vy1 = k.y0 + 1 >= 0 && k.y0 + 1 < p.Hi;
+        for (int c = 0; c < p.C; ++c) {
+            const T* b = in + n * p.is_n + c * p.is_c;
+            float acc = 0.f;
+            if (vy0 && vx0) acc += (float)b[k.y0 * p.is_h + k.x0 * p.is_w] * k.w00;
+            if (vy0 && vx1) acc += (float)b[k.y0 * p.is_h + (k.x0 + 1) * p.is_w] * k.w01;
+            if (vy1 && vx0) acc += (float)b[(k.y0 + 1) * p.is_h + k.x0 * p.is_w] * k.w10;
+            if (vy1 && vx1) acc += (float)b[(k.y0 + 1) * p.is_h + (k.x0 + 1) * p.is_w] * k.w11;
+            out[n * p.os_n + c * p.os_c + (int64_t)oy * p.os_h + (int64_t)ox * p.os_w] = (T)acc;
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void grid_sample_bwd_kernel(GSParams p) {
+    const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
+    const T* gout = (const T*)p.in;   // gradient w.r.t. output (layout os_*)
+    float* gin = (float*)p.out;       // gradient w.r.t. input  (layout is_*)
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int ox = (int)(idx % p.Wo);
+        const int oy = (int)((idx / p.Wo) % p.Ho);
+        const int n = (int)(idx / ((int64_t)p.Wo * p.Ho));
+        const Corners k = corners(p, n, oy, ox);
+        const bool vx0 = k.x0 >= 0 && k.x0 < p.Wi, vx1 = k.x0 + 1 >= 0 && k.x0 + 1 < p.Wi;
+        const bool vy0 = k.y0 >= 0 && k.y0 < p.Hi, vy1 = k.y0 + 1 >= 0 && k.y0 + 1 < p.Hi;
+        for (int c = 0; c < p.C; ++c) {
+            const float g = (float)gout[n * p.os_n + c * p.os_c + (int64_t)oy * p.os_h + (int64_t)ox * p.os_w];
+            float* b = gin + n * p.is_n + c * p.is_c;
+            if (vy0 && vx0) atomicAdd(b + k.y0 * p.is_h + k.x0 * p.is_w, g * k.w00);
+            if (vy0 && vx1) atomicAdd(b + k.y0 * p.is_h + (k.x0 + 1) * p.is_w, g * k.w01);
+            if (vy1 && vx0) atomicAdd(b + (k.y0 + 1) * p.is_h + k.x0 * p.is_w, g * k.w10);
+            if (vy1 && vx1) atomicAdd(b + (k.y0 + 1) * p.is_h + (k.x0 + 1) * p.is_w, g * k.w11);
+        }
+    }
+}
+
+int fill(GSParams& p, const int64_t* in_size, const int64_t* in_stride, const int64_t* out_size,
+         const int64_t* out_stride) {
+    SG2_CHECK(in_size && in_stride && out_size && out_stride, "sg2_grid_sample: null size/stride");
+    p.N = (int)in_size[0]; p.C = (int)in_size[1]; p.Hi = (int)in_size[2]; p.Wi = (int)in_size[3];
+    SG2_CHECK(out_size[0] == p.N && out_size[1] == p.C, "sg2_grid_sample: batch/channel mismatch");
+    p.Ho = (int)out_size[2]; p.Wo = (int)out_size[3];
+    p.is_n = in_stride[0]; p.is_c = in_stride[1]; p.is_h = in_stride[2]; p.is_w = in_stride[3];
+    p.os_n = out_stride[0]; p.os_c = out_stride[1]; p.os_h = out_stride[2]; p.os_w = out_stride[3];
+    return 0;
+}
+
+}  // namespace
+}  // namespace sg2
+
+extern "C" int sg2_grid_sample_fwd(void* out, const void* in, const float* grid, int dtype, const int64_t* in_size,
+                                   const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
+                                   void* stream) {
+    using namespace sg2;
+    SG2_CHECK(out && in && grid, "sg2_grid_sample_fwd: null pointer");
+    GSParams p;
+    p.in = in; p.out = out; p.grid = grid;
+    if (fill(p, in_size, in_stride, out_size, out_stride)) return -1;
+    const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
+    if (total == 0 || p.C == 0) return 0;
+    const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 32);
+    SG2_DISPATCH(dtype, T, { grid_sample_fwd_kernel<T><<<g, 256, 0, as_stream(stream)>>>(p); });
+    return launch_status("sg2_grid_sample_fwd");
+}
+
+extern "C" int sg2_grid_sample_bwd(float* gin, const void* gout, const float* grid, int dtype, const int64_t* in_size,
+                                   const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
+                                   void* stream) {
+    using namespace sg2;
+    SG2_CHECK(gin && gout && grid, "sg2_grid_sample_bwd: null pointer");
+    GSParams p;
+    p.in = gout; p.out = gin; p.grid = grid;
+    if (fill(p, in_size, in_stride, out_size, out_stride)) return -1;
+    SG2_CHECK(p.is_w == 1 || p.C == 1 || true, "");
+    // zero the float32 input-gradient buffer (dense over the strided extent)
+    const int64_t extent = (p.N - 1) * p.is_n + (p.C - 1) * p.is_c + (p.Hi - 1) * p.is_h + (p.Wi - 1) * p.is_w + 1;
+    hipStream_t s = as_stream(stream);
+    hipError_t e = hipMemsetAsync(gin, 0, extent * sizeof(float), s);
+    if (e != hipSuccess) { set_error("sg2_grid_sample_bwd: memset failed"); return (int)e; }
+    const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
+    if (total == 0 || p.C == 0) return 0;
+    const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 32);
+    SG2_DISPATCH(dtype, T, { grid_sample_bwd_kernel<T><<<g, 256, 0, s>>>(p); });
+    return launch_status("sg2_grid_sample_bwd");
+}

@@ -1,0 +1,94 @@
+// Small kernels of the training step: demodulation coefficients, fused gradient sanitation + Adam,
+// and the G_ema lerp.  All HBM-bound, grid-stride, 16-byte vectorised where the data allow.
+#include "sg2_common.h"
+
+namespace sg2 {
+namespace {
+
+// d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps);  wsq[o,i] = sum_k w[o,i,k]^2.
+// One workgroup per (o, block of samples): the 256 lanes reduce over i.
+__global__ __launch_bounds__(256) void demod_kernel(float* d, const float* s, const float* w, int N, int O, int I,
+                                                    int KK, float eps) {
+    __shared__ float wsq[1024];
+    __shared__ float red[4];
+    const int o = blockIdx.x;
+    for (int i = threadIdx.x; i < I; i += 256) {
+        const float* wr = w + ((int64_t)o * I + i) * KK;
+        float acc = 0.f;
+        for (int k = 0; k < KK; ++k) acc += wr[k] * wr[k];
+        wsq[i] = acc;
+    }
+    __syncthreads();
+    for (int n = blockIdx.y; n < N; n += gridDim.y) {
+        float acc = 0.f;
+        for (int i = threadIdx.x; i < I; i += 256) {
+            const float v = s[(int64_t)n * I + i];
+            acc += v * v * wsq[i];
+        }
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) d[(int64_t)n * O + o] = rsqrtf(red[0] + red[1] + red[2] + red[3] + eps);
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                                                   const float* __restrict__ g, int64_t n, float lr, float b1, float b2,
+                                                   float eps, float gscale, float bc1, float bc2_sqrt) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float gi = g[i] * gscale;
+        if (gi != gi) gi = 0.f;
+        gi = fminf(fmaxf(gi, -1e5f), 1e5f);
+        const float mi = m[i] * b1 + (1.f - b1) * gi;
+        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        p[i] -= (lr / bc1) * mi / denom;
+    }
+}
+
+__global__ __launch_bounds__(256) void lerp_kernel(float* __restrict__ dst, const float* __restrict__ src, int64_t n,
+                                                   float beta) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float a = src[i];
+        dst[i] = a + beta * (dst[i] - a);
+    }
+}
+
+}  // namespace
+}  // namespace sg2
+
+extern "C" int sg2_demod_coefs(float* d, const float* s, const float* w, int N, int O, int I, int KK, float eps,
+                               void* stream) {
+    using namespace sg2;
+    SG2_CHECK(d && s && w, "sg2_demod_coefs: null pointer");
+    SG2_CHECK(I <= 1024 && I > 0 && O > 0 && N > 0 && KK > 0, "sg2_demod_coefs: unsupported shape");
+    dim3 grid(O, std::min(N, 64));
+    demod_kernel<<<grid, 256, 0, as_stream(stream)>>>(d, s, w, N, O, I, KK, eps);
+    return launch_status("sg2_demod_coefs");
+}
+
+extern "C" int sg2_adam_step(float* param, float* exp_avg, float* exp_avg_sq, const float* grad, int64_t n, float lr,
+                             float beta1, float beta2, float eps, float grad_scale, int64_t step, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(param && exp_avg && exp_avg_sq && grad, "sg2_adam_step: null pointer");
+    SG2_CHECK(step >= 1, "sg2_adam_step: step must be >= 1");
+    if (n == 0) return 0;
+    const float bc1 = 1.f - powf(beta1, (float)step);
+    const float bc2 = 1.f - powf(beta2, (float)step);
+    const int g = (int)std::min<int64_t>(cdiv(n, 256), 8192);
+    adam_kernel<<<g, 256, 0, as_stream(stream)>>>(param, exp_avg, exp_avg_sq, grad, n, lr, beta1, beta2, eps,
+                                                 grad_scale, bc1, sqrtf(bc2));
+    return launch_status("sg2_adam_step");
+}
+
+extern "C" int sg2_lerp(float* dst, const float* src, int64_t n, float beta, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(dst && src, "sg2_lerp: null pointer");
+    if (n == 0) return 0;
+    const int g = (int)std::min<int64_t>(cdiv(n, 256), 8192);
+    lerp_kernel<<<g, 256, 0, as_stream(stream)>>>(dst, src, n, beta);
+    return launch_status("sg2_lerp");
+}

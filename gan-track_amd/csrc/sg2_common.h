@@ -1,0 +1,55 @@
+// Shared helpers for the sg2hip kernels (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/sg2hip.h"
+
+typedef _Float16 f16_t;
+typedef __bf16 bf16_t;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef bf16_t bf16x8 __attribute__((ext_vector_type(8)));
+typedef f16_t f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+namespace sg2 {
+
+// Per-host-thread error message (sg2_last_error).
+void set_error(const std::string& msg);
+
+#define SG2_CHECK(cond, msg)                     \
+    do {                                         \
+        if (!(cond)) {                           \
+            ::sg2::set_error(std::string(msg));  \
+            return -1;                           \
+        }                                        \
+    } while (0)
+
+inline int launch_status(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error(std::string(what) + ": " + hipGetErrorString(e));
+        return (int)e;
+    }
+    return 0;
+}
+
+template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T)v; }
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace sg2
+
+// Dispatch on the runtime dtype code.
+#define SG2_DISPATCH(dtype, T, ...)                                  \
+    switch (dtype) {                                                 \
+        case SG2_F32: { typedef float T; __VA_ARGS__; break; }       \
+        case SG2_F16: { typedef f16_t T; __VA_ARGS__; break; }       \
+        case SG2_BF16: { typedef bf16_t T; __VA_ARGS__; break; }     \
+        default: ::sg2::set_error("unsupported dtype"); return -1;   \
+    }

@@ -1,0 +1,182 @@
+// upfirdn2d: zero-insertion upsample -> pad/crop -> 2-D FIR -> decimate.
+// Semantics: SG3/torch_utils/ops/upfirdn2d.py:118-211 (plugin contract upfirdn2d.cpp:16-98).
+//
+// Output sample o (per axis) reads upsampled-padded positions u = o*down - pad0 + t, t in [0, f);
+// only u divisible by `up` carry input samples x[u/up], so per output row the valid taps are
+// t = t0 + k*up with t0 = (-(o*down - pad0)) mod up.  Filter taps are staged once per workgroup in
+// LDS; the weight of tap t is f[f-1-t] (convolution) or f[t] (flip = correlation).
+//
+// Two kernels:
+//  * upfirdn_nhwc_vec: channels-last activations with C % V == 0 (the network's feature maps);
+//    each lane owns one 16-byte channel vector of one output pixel, so every tap read is a
+//    coalesced 16-byte load and neighbouring taps hit L1/L2.
+//  * upfirdn_generic : any 4-D strides (images, NCHW tensors, odd channel counts).
+#include "sg2_common.h"
+
+namespace sg2 {
+namespace {
+
+constexpr int kMaxTaps = 1024;
+
+struct UpfParams {
+    const void* x;
+    void* y;
+    const float* f;
+    int N, C, H, W;           // input
+    int OH, OW;               // output
+    int64_t xs_n, xs_c, xs_h, xs_w;
+    int64_t ys_n, ys_c, ys_h, ys_w;
+    int fw, fh;
+    int upx, upy, downx, downy, padx0, pady0;
+    int flip;
+    float gain;
+};
+
+__device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+// Tap geometry along one axis for output coordinate o.
+__device__ __forceinline__ void axis_taps(int o, int down, int pad0, int up, int& t0, int& i0) {
+    const int z = o * down - pad0;
+    int r = (-z) % up;
+    if (r < 0) r += up;
+    t0 = r;
+    i0 = floordiv(z + r, up);
+}
+
+__device__ __forceinline__ void stage_filter(float* sf, const UpfParams& p) {
+    const int n = p.fw * p.fh;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        // store in "tap order": sf[ty*fw+tx] = weight applied to tap (ty, tx)
+        const int ty = i / p.fw, tx = i % p.fw;
+        const int sy = p.flip ? ty : p.fh - 1 - ty;
+        const int sx = p.flip ? tx : p.fw - 1 - tx;
+        sf[i] = p.f[sy * p.fw + sx] * p.gain;
+    }
+    __syncthreads();
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void upfirdn_generic(UpfParams p) {
+    __shared__ float sf[kMaxTaps];
+    stage_filter(sf, p);
+    const T* x = (const T*)p.x;
+    T* y = (T*)p.y;
+    const int64_t total = (int64_t)p.N * p.C * p.OH * p.OW;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        int64_t r = idx;
+        const int ox = (int)(r % p.OW); r /= p.OW;
+        const int oy = (int)(r % p.OH); r /= p.OH;
+        const int c = (int)(r % p.C); r /= p.C;
+        const int n = (int)r;
+        int ty0, iy0, tx0, ix0;
+        axis_taps(oy, p.downy, p.pady0, p.upy, ty0, iy0);
+        axis_taps(ox, p.downx, p.padx0, p.upx, tx0, ix0);
+        const T* xb = x + n * p.xs_n + c * p.xs_c;
+        float acc = 0.f;
+        for (int ty = ty0, iy = iy0; ty < p.fh; ty += p.upy, ++iy) {
+            if (iy < 0 || iy >= p.H) continue;
+            const T* xr = xb + iy * p.xs_h;
+            for (int tx = tx0, ix = ix0; tx < p.fw; tx += p.upx, ++ix) {
+                if (ix < 0 || ix >= p.W) continue;
+                acc += (float)xr[ix * p.xs_w] * sf[ty * p.fw + tx];
+            }
+        }
+        y[n * p.ys_n + c * p.ys_c + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w] = (T)acc;
+    }
+}
+
+template <typename T> struct VecN { static constexpr int N = 8; };
+template <> struct VecN<float> { static constexpr int N = 4; };
+
+// channels-last, C % V == 0, xs_c == ys_c == 1.
+template <typename T>
+__global__ __launch_bounds__(256) void upfirdn_nhwc_vec(UpfParams p) {
+    constexpr int V = VecN<T>::N;
+    typedef T vecT __attribute__((ext_vector_type(V)));
+    __shared__ float sf[kMaxTaps];
+    stage_filter(sf, p);
+    const T* x = (const T*)p.x;
+    T* y = (T*)p.y;
+    const int CV = p.C / V;
+    const int64_t total = (int64_t)p.N * p.OH * p.OW * CV;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        int64_t r = idx;
+        const int cv = (int)(r % CV); r /= CV;
+        const int ox = (int)(r % p.OW); r /= p.OW;
+        const int oy = (int)(r % p.OH); r /= p.OH;
+        const int n = (int)r;
+        int ty0, iy0, tx0, ix0;
+        axis_taps(oy, p.downy, p.pady0, p.upy, ty0, iy0);
+        axis_taps(ox, p.downx, p.padx0, p.upx, tx0, ix0);
+        const T* xb = x + n * p.xs_n + cv * V;
+        float acc[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] = 0.f;
+        for (int ty = ty0, iy = iy0; ty < p.fh; ty += p.upy, ++iy) {
+            if (iy < 0 || iy >= p.H) continue;
+            const T* xr = xb + iy * p.xs_h;
+            for (int tx = tx0, ix = ix0; tx < p.fw; tx += p.upx, ++ix) {
+                if (ix < 0 || ix >= p.W) continue;
+                const float wt = sf[ty * p.fw + tx];
+                const vecT v = *(const vecT*)(xr + ix * p.xs_w);
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[j] += (float)v[j] * wt;
+            }
+        }
+        vecT o;
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = (T)acc[j];
+        *(vecT*)(y + n * p.ys_n + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w + cv * V) = o;
+    }
+}
+
+template <typename T>
+int launch(const UpfParams& p, bool vec, hipStream_t s) {
+    const int64_t work = vec ? (int64_t)p.N * p.OH * p.OW * (p.C / VecN<T>::N) : (int64_t)p.N * p.C * p.OH * p.OW;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 256 * 32));
+    if (vec)
+        upfirdn_nhwc_vec<T><<<grid, 256, 0, s>>>(p);
+    else
+        upfirdn_generic<T><<<grid, 256, 0, s>>>(p);
+    return launch_status("sg2_upfirdn2d");
+}
+
+}  // namespace
+}  // namespace sg2
+
+extern "C" int sg2_upfirdn2d(void* y, const void* x, const float* f, int dtype, const int64_t* in_size,
+                             const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride, int fw,
+                             int fh, int upx, int upy, int downx, int downy, int padx0, int padx1, int pady0,
+                             int pady1, int flip, float gain, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(x && y && f && in_size && in_stride && out_size && out_stride, "sg2_upfirdn2d: null argument");
+    SG2_CHECK(upx >= 1 && upy >= 1 && downx >= 1 && downy >= 1, "sg2_upfirdn2d: up/down must be >= 1");
+    SG2_CHECK(fw >= 1 && fh >= 1 && fw * fh <= kMaxTaps, "sg2_upfirdn2d: filter too large");
+    UpfParams p;
+    p.x = x; p.y = y; p.f = f;
+    p.N = (int)in_size[0]; p.C = (int)in_size[1]; p.H = (int)in_size[2]; p.W = (int)in_size[3];
+    p.OH = (int)out_size[2]; p.OW = (int)out_size[3];
+    SG2_CHECK(out_size[0] == p.N && out_size[1] == p.C, "sg2_upfirdn2d: batch/channel mismatch");
+    const int64_t eh = ((int64_t)p.H * upy + pady0 + pady1 - fh + downy) / downy;
+    const int64_t ew = ((int64_t)p.W * upx + padx0 + padx1 - fw + downx) / downx;
+    SG2_CHECK(p.H * upy + pady0 + pady1 >= fh && p.W * upx + padx0 + padx1 >= fw,
+              "sg2_upfirdn2d: upsampled buffer must be at least the size of the filter");
+    SG2_CHECK(eh == p.OH && ew == p.OW, "sg2_upfirdn2d: output size mismatch");
+    p.xs_n = in_stride[0]; p.xs_c = in_stride[1]; p.xs_h = in_stride[2]; p.xs_w = in_stride[3];
+    p.ys_n = out_stride[0]; p.ys_c = out_stride[1]; p.ys_h = out_stride[2]; p.ys_w = out_stride[3];
+    p.fw = fw; p.fh = fh; p.upx = upx; p.upy = upy; p.downx = downx; p.downy = downy;
+    p.padx0 = padx0; p.pady0 = pady0; p.flip = flip; p.gain = gain;
+    if ((int64_t)p.N * p.C * p.OH * p.OW == 0) return 0;
+    hipStream_t s = as_stream(stream);
+    SG2_DISPATCH(dtype, T, {
+        constexpr int V = VecN<T>::N;
+        const bool vec = p.xs_c == 1 && p.ys_c == 1 && p.C % V == 0 && p.C >= V &&
+                         ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
+                         p.xs_w % V == 0 && p.xs_h % V == 0 && p.xs_n % V == 0 &&
+                         p.ys_w % V == 0 && p.ys_h % V == 0 && p.ys_n % V == 0;
+        return launch<T>(p, vec, s);
+    });
+    return 0;
+}

@@ -1,0 +1,92 @@
+"""ctypes binding of libsg2hip.so -- the C-ABI declared in include/sg2hip.h.
+
+The product path has no fallback: if the library is missing, or a tensor is not on a ROCm
+device, every op raises.  (The reference's ops silently fall back to slow `_ref` paths on CPU,
+SG3/torch_utils/ops/upfirdn2d.py:160-162; here that would hide a broken build, so it is an error.)
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('SG2HIP_LIB', os.path.join(_HERE, 'libsg2hip.so'))
+
+F32, F16, BF16 = 0, 1, 2
+_DTYPES = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16}
+
+_c_i64p = ctypes.POINTER(ctypes.c_int64)
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+
+# name -> argtypes (restype is int for all entry points except sg2_last_error)
+SIGNATURES = {
+    'sg2_abi_version': [],
+    'sg2_bias_act': [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i64, _i64, _i64, _i, _i, _f, _f, _f, _vp],
+    'sg2_upfirdn2d': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i,
+                      _i, _f, _vp],
+    'sg2_conv2d': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i64, _vp],
+    'sg2_conv2d_wgrad': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp],
+    'sg2_grid_sample_fwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp],
+    'sg2_grid_sample_bwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp],
+    'sg2_demod_coefs': [_vp, _vp, _vp, _i, _i, _i, _i, _f, _vp],
+    'sg2_adam_step': [_vp, _vp, _vp, _vp, _i64, _f, _f, _f, _f, _f, _i64, _vp],
+    'sg2_lerp': [_vp, _vp, _i64, _f, _vp],
+}
+ABI_VERSION = 1
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if the HIP build is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f'sg2hip: {LIB_PATH} not found -- build it with `python -c "import __graft_entry__ as '
+                               f'g; g.build()"` (hipcc --offload-arch=gfx950); there is no CPU fallback')
+        L = ctypes.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        L.sg2_last_error.argtypes = []
+        L.sg2_last_error.restype = ctypes.c_char_p
+        if L.sg2_abi_version() != ABI_VERSION:
+            raise RuntimeError(f'sg2hip: ABI version mismatch ({L.sg2_abi_version()} != {ABI_VERSION})')
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().sg2_last_error().decode(errors='replace')
+        raise RuntimeError(f'{what} failed ({rc}): {msg}')
+
+
+def dtype_code(t):
+    try:
+        return _DTYPES[t.dtype]
+    except KeyError:
+        raise RuntimeError(f'sg2hip: unsupported dtype {t.dtype}') from None
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and (not isinstance(t, torch.Tensor) or t.device.type != 'cuda'):
+            raise RuntimeError('sg2hip ops run only on ROCm device tensors (no CPU fallback); got '
+                               f'{type(t).__name__} on {getattr(t, "device", None)}')
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def i64arr(vals):
+    return (ctypes.c_int64 * len(vals))(*[int(v) for v in vals])

@@ -1,0 +1,201 @@
+"""2-D convolution / transposed convolution on MI355X MFMA (HIP kernels sg2_conv2d, sg2_conv2d_wgrad)
+with gradients of arbitrary order.
+
+Drop-in for SG3/torch_utils/ops/conv2d_gradfix.py (:37-45 `conv2d`, `conv_transpose2d`,
+`no_weight_gradients`, module flags `enabled` / `weight_gradients_disabled`).  The reference
+routes to cuDNN (its custom op is disabled on torch >= 1.11, :53-55); here every call runs the HIP
+implicit-GEMM kernels, and the three ops {conv, transposed conv, weight gradient} are closed under
+differentiation, so the path-length (G) and R1 (D) double-backward passes stay on MFMA:
+
+    conv2d(x, w)        : dx = conv_transpose2d(dy, w)   dw = wgrad(dy, x)
+    conv_transpose2d(x,w): dx = conv2d(dy, w)            dw = wgrad(x, dy)   (roles swapped)
+    wgrad(g, x) -> dw   : dg = conv2d(x, ddw)            dx = conv_transpose2d(g, ddw)
+
+Activations are NHWC in memory (torch channels_last); weights are packed K-contiguous per output
+channel before each launch (a few MB at most).
+"""
+import contextlib
+
+import torch
+
+import sg2hip as _hip
+
+enabled = True                      # accepted for API compatibility; the HIP path is always used
+weight_gradients_disabled = False   # skip dw (reference :21-33); values are unaffected
+
+
+@contextlib.contextmanager
+def no_weight_gradients(disable=True):
+    global weight_gradients_disabled
+    old = weight_gradients_disabled
+    if disable:
+        weight_gradients_disabled = True
+    yield
+    weight_gradients_disabled = old
+
+
+def _pair(v):
+    if isinstance(v, (list, tuple)):
+        assert len(v) == 2
+        return int(v[0]), int(v[1])
+    return int(v), int(v)
+
+
+_CL = torch.channels_last
+
+
+def _nhwc(t):
+    t = t.contiguous(memory_format=_CL)
+    if t.data_ptr() % 16:
+        t = t.clone(memory_format=_CL)
+    return t
+
+
+_WS_LIMIT = 1 << 23  # split-K f32 workspace only for small outputs (low-resolution layers)
+
+
+def _conv_raw(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose):
+    """x [N,Cin,H,W] (NHWC memory), wp packed [Cout][kh][kw][Cin] -> y [N,Cout,oh,ow] (NHWC memory)."""
+    n, cin, h, w = x.shape
+    y = torch.empty([n, cout, oh, ow], dtype=x.dtype, device=x.device, memory_format=_CL)
+    total = n * cout * oh * ow
+    ws = torch.empty([total], dtype=torch.float32, device=x.device) if total <= _WS_LIMIT else None
+    _hip.check(_hip.lib().sg2_conv2d(
+        _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
+        stride, pad[0], pad[1], int(transpose), _hip.ptr(ws), ws.numel() if ws is not None else 0,
+        _hip.stream_ptr(x.device)), 'sg2_conv2d')
+    return y
+
+
+def _wgrad_raw(g, x, kh, kw, stride, pad):
+    """dw[a, b, ky, kx] = sum g[n,a,oy,ox] x[n,b,oy*s+ky-p,ox*s+kx-p]; returns f32 [A,B,kh,kw] (NHWC-packed)."""
+    n, a, oh, ow = g.shape
+    _, b, h, w = x.shape
+    dw = torch.empty([a, kh, kw, b], dtype=torch.float32, device=g.device)
+    _hip.check(_hip.lib().sg2_conv2d_wgrad(
+        _hip.ptr(dw), _hip.ptr(g), _hip.ptr(x), _hip.dtype_code(g), n, a, oh, ow, b, h, w, kh, kw, stride,
+        pad[0], pad[1], _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad')
+    return dw.permute(0, 3, 1, 2)
+
+
+def _pack_conv(w):          # [O, I, kh, kw] -> [O][kh][kw][I]
+    return w.permute(0, 2, 3, 1).contiguous()
+
+
+def _pack_convT(w):         # [I, O, kh, kw] -> [O][kh][kw][I]
+    return w.permute(1, 2, 3, 0).contiguous()
+
+
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, out_hw):
+        x = _nhwc(x)
+        o, i, kh, kw = w.shape
+        assert x.shape[1] == i and x.dtype == w.dtype
+        oh, ow = out_hw
+        y = _conv_raw(x, _pack_conv(w), o, oh, ow, kh, kw, stride, pad, False)
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.pad = stride, pad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = _ConvT2d.apply(dy, w, ctx.stride, ctx.pad, tuple(x.shape[2:]))
+        if ctx.needs_input_grad[1] and not weight_gradients_disabled:
+            dw = _WGrad.apply(dy, x, tuple(w.shape[2:]), ctx.stride, ctx.pad).to(w.dtype)
+        return dx, dw, None, None, None
+
+
+class _ConvT2d(torch.autograd.Function):
+    """y = conv_transpose2d(x, w[I, O, kh, kw], stride, padding) with explicit output size."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, out_hw):
+        x = _nhwc(x)
+        i, o, kh, kw = w.shape
+        assert x.shape[1] == i and x.dtype == w.dtype
+        oh, ow = out_hw
+        y = _conv_raw(x, _pack_convT(w), o, oh, ow, kh, kw, stride, pad, True)
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.pad = stride, pad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = _Conv2d.apply(dy, w, ctx.stride, ctx.pad, tuple(x.shape[2:]))
+        if ctx.needs_input_grad[1] and not weight_gradients_disabled:
+            dw = _WGrad.apply(x, dy, tuple(w.shape[2:]), ctx.stride, ctx.pad).to(w.dtype)
+        return dx, dw, None, None, None
+
+
+class _WGrad(torch.autograd.Function):
+    """dw[a, b, ky, kx] = sum_{n,p} g[n, a, p] * x[n, b, p*s + k - pad]  (f32 result)."""
+
+    @staticmethod
+    def forward(ctx, g, x, ksize, stride, pad):
+        g, x = _nhwc(g), _nhwc(x)
+        ctx.save_for_backward(g, x)
+        ctx.stride, ctx.pad = stride, pad
+        return _wgrad_raw(g, x, ksize[0], ksize[1], stride, pad)
+
+    @staticmethod
+    def backward(ctx, ddw):
+        g, x = ctx.saved_tensors
+        ddw = ddw.to(g.dtype)
+        dg = dx = None
+        if ctx.needs_input_grad[0]:
+            dg = _Conv2d.apply(x, ddw, ctx.stride, ctx.pad, tuple(g.shape[2:]))
+        if ctx.needs_input_grad[1]:
+            dx = _ConvT2d.apply(g, ddw, ctx.stride, ctx.pad, tuple(x.shape[2:]))
+        return dg, dx, None, None, None
+
+
+def conv2d(input, weight, bias=None, stride=1, padding=0, dilation=1, groups=1):
+    """torch.nn.functional.conv2d semantics (correlation)."""
+    _hip.require_device(input, weight)
+    assert _pair(dilation) == (1, 1), 'dilation is not supported'
+    sy, sx = _pair(stride)
+    assert sy == sx, 'anisotropic stride is not supported'
+    py, px = _pair(padding)
+    if groups != 1:
+        xs = input.chunk(groups, dim=1)
+        ws = weight.chunk(groups, dim=0)
+        y = torch.cat([conv2d(a, b_, None, stride, padding) for a, b_ in zip(xs, ws)], dim=1)
+    else:
+        n, c, h, w = input.shape
+        o, i, kh, kw = weight.shape
+        oh = (h + 2 * py - kh) // sy + 1
+        ow = (w + 2 * px - kw) // sx + 1
+        y = _Conv2d.apply(input, weight, sy, (py, px), (oh, ow))
+    if bias is not None:
+        y = y + bias.reshape(1, -1, 1, 1)
+    return y
+
+
+def conv_transpose2d(input, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1):
+    """torch.nn.functional.conv_transpose2d semantics."""
+    _hip.require_device(input, weight)
+    assert _pair(dilation) == (1, 1), 'dilation is not supported'
+    sy, sx = _pair(stride)
+    assert sy == sx, 'anisotropic stride is not supported'
+    py, px = _pair(padding)
+    opy, opx = _pair(output_padding)
+    if groups != 1:
+        xs = input.chunk(groups, dim=1)
+        ws = weight.chunk(groups, dim=0)
+        y = torch.cat([conv_transpose2d(a, b_, None, stride, padding, output_padding) for a, b_ in zip(xs, ws)], dim=1)
+    else:
+        n, c, h, w = input.shape
+        i, o, kh, kw = weight.shape
+        oh = (h - 1) * sy - 2 * py + kh + opy
+        ow = (w - 1) * sx - 2 * px + kw + opx
+        y = _ConvT2d.apply(input, weight, sy, (py, px), (oh, ow))
+    if bias is not None:
+        y = y + bias.reshape(1, -1, 1, 1)
+    return y

@@ -1,0 +1,161 @@
+"""upfirdn2d on MI355X (HIP kernel sg2_upfirdn2d, filter taps staged in LDS).
+
+Drop-in for SG3/torch_utils/ops/upfirdn2d.py: `setup_filter`, `upfirdn2d`, `filter2d`,
+`upsample2d`, `downsample2d` with identical arguments and padding algebra (:70-389).  Gradients
+of any order w.r.t. x (the op is linear; its adjoint is again an upfirdn2d with up/down swapped
+and the filter flipped, reference :250-269).  Separable (1-D) filters run as a horizontal then a
+vertical pass, like the reference plugin (:243-245).
+"""
+import numpy as np
+import torch
+
+import sg2hip as _hip
+
+
+def _parse_scaling(scaling):
+    if isinstance(scaling, int):
+        scaling = [scaling, scaling]
+    assert isinstance(scaling, (list, tuple)) and all(isinstance(v, int) for v in scaling)
+    sx, sy = scaling
+    assert sx >= 1 and sy >= 1
+    return sx, sy
+
+
+def _parse_padding(padding):
+    if isinstance(padding, int):
+        padding = [padding, padding]
+    assert isinstance(padding, (list, tuple)) and all(isinstance(v, int) for v in padding)
+    if len(padding) == 2:
+        px, py = padding
+        padding = [px, px, py, py]
+    px0, px1, py0, py1 = padding
+    return px0, px1, py0, py1
+
+
+def _get_filter_size(f):
+    if f is None:
+        return 1, 1
+    assert isinstance(f, torch.Tensor) and f.ndim in [1, 2]
+    fw = int(f.shape[-1])
+    fh = int(f.shape[0])
+    assert fw >= 1 and fh >= 1
+    return fw, fh
+
+
+def setup_filter(f, device=torch.device('cpu'), normalize=True, flip_filter=False, gain=1, separable=None):
+    """Prepare a float32 FIR filter (reference :70-114)."""
+    if f is None:
+        f = 1
+    f = torch.as_tensor(f, dtype=torch.float32)
+    assert f.ndim in [0, 1, 2] and f.numel() > 0
+    if f.ndim == 0:
+        f = f[np.newaxis]
+    if separable is None:
+        separable = (f.ndim == 1 and f.numel() >= 8)
+    if f.ndim == 1 and not separable:
+        f = f.ger(f)
+    assert f.ndim == (1 if separable else 2)
+    if normalize:
+        f /= f.sum()
+    if flip_filter:
+        f = f.flip(list(range(f.ndim)))
+    f = f * (gain ** (f.ndim / 2))
+    return f.to(device=device)
+
+
+def _raw(x, f2, upx, upy, downx, downy, px0, px1, py0, py1, flip, gain):
+    """One sg2_upfirdn2d launch with a 2-D float32 filter f2 [fh, fw]."""
+    n, c, h, w = x.shape
+    fh, fw = f2.shape
+    oh = (h * upy + py0 + py1 - fh + downy) // downy
+    ow = (w * upx + px0 + px1 - fw + downx) // downx
+    assert oh >= 1 and ow >= 1, 'upfirdn2d: output would be empty'
+    fmt = torch.channels_last if (x.stride(1) == 1 and c > 1) else torch.contiguous_format
+    y = torch.empty([n, c, oh, ow], dtype=x.dtype, device=x.device, memory_format=fmt)
+    _hip.check(_hip.lib().sg2_upfirdn2d(
+        _hip.ptr(y), _hip.ptr(x), _hip.ptr(f2), _hip.dtype_code(x), _hip.i64arr(x.shape), _hip.i64arr(x.stride()),
+        _hip.i64arr(y.shape), _hip.i64arr(y.stride()), fw, fh, upx, upy, downx, downy, px0, px1, py0, py1,
+        int(bool(flip)), float(gain), _hip.stream_ptr(x.device)), 'sg2_upfirdn2d')
+    return y
+
+
+_cache = {}
+
+
+def _upfirdn2d_fn(up=1, down=1, padding=0, flip_filter=False, gain=1):
+    upx, upy = _parse_scaling(up)
+    downx, downy = _parse_scaling(down)
+    px0, px1, py0, py1 = _parse_padding(padding)
+    key = (upx, upy, downx, downy, px0, px1, py0, py1, flip_filter, gain)
+    if key in _cache:
+        return _cache[key]
+
+    class Upfirdn2d(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, f):
+            assert x.ndim == 4
+            if f is None:
+                f = torch.ones([1, 1], dtype=torch.float32, device=x.device)
+            if f.ndim == 1 and f.shape[0] == 1:
+                f = f.square().unsqueeze(0)
+            f = f.to(device=x.device, dtype=torch.float32).contiguous()
+            if f.ndim == 2:
+                y = _raw(x, f, upx, upy, downx, downy, px0, px1, py0, py1, flip_filter, gain)
+            else:
+                y = _raw(x, f.unsqueeze(0), upx, 1, downx, 1, px0, px1, 0, 0, flip_filter, 1.0)
+                y = _raw(y, f.unsqueeze(1), 1, upy, 1, downy, 0, 0, py0, py1, flip_filter, gain)
+            ctx.save_for_backward(f)
+            ctx.x_shape = x.shape
+            return y
+
+        @staticmethod
+        def backward(ctx, dy):
+            f, = ctx.saved_tensors
+            _, _, ih, iw = ctx.x_shape
+            _, _, oh, ow = dy.shape
+            fw, fh = _get_filter_size(f)
+            # adjoint: upsample by `down`, filter with the flipped taps, decimate by `up`
+            p = [fw - px0 - 1, iw * upx - ow * downx + px0 - upx + 1,
+                 fh - py0 - 1, ih * upy - oh * downy + py0 - upy + 1]
+            dx = None
+            if ctx.needs_input_grad[0]:
+                dx = _upfirdn2d_fn(up=[downx, downy], down=[upx, upy], padding=p, flip_filter=(not flip_filter),
+                                   gain=gain).apply(dy, f)
+            assert not ctx.needs_input_grad[1]
+            return dx, None
+
+    _cache[key] = Upfirdn2d
+    return Upfirdn2d
+
+
+def upfirdn2d(x, f, up=1, down=1, padding=0, flip_filter=False, gain=1, impl='cuda'):
+    """Pad, upsample, filter and downsample a batch of 2-D images (reference :118-162)."""
+    assert isinstance(x, torch.Tensor)
+    _hip.require_device(x)
+    return _upfirdn2d_fn(up=up, down=down, padding=padding, flip_filter=flip_filter, gain=gain).apply(x, f)
+
+
+def filter2d(x, f, padding=0, flip_filter=False, gain=1, impl='cuda'):
+    """Filter keeping the input size (reference :277-309)."""
+    px0, px1, py0, py1 = _parse_padding(padding)
+    fw, fh = _get_filter_size(f)
+    p = [px0 + fw // 2, px1 + (fw - 1) // 2, py0 + fh // 2, py1 + (fh - 1) // 2]
+    return upfirdn2d(x, f, padding=p, flip_filter=flip_filter, gain=gain, impl=impl)
+
+
+def upsample2d(x, f, up=2, padding=0, flip_filter=False, gain=1, impl='cuda'):
+    """Upsample by `up` (reference :313-348)."""
+    upx, upy = _parse_scaling(up)
+    px0, px1, py0, py1 = _parse_padding(padding)
+    fw, fh = _get_filter_size(f)
+    p = [px0 + (fw + upx - 1) // 2, px1 + (fw - upx) // 2, py0 + (fh + upy - 1) // 2, py1 + (fh - upy) // 2]
+    return upfirdn2d(x, f, up=up, padding=p, flip_filter=flip_filter, gain=gain * upx * upy, impl=impl)
+
+
+def downsample2d(x, f, down=2, padding=0, flip_filter=False, gain=1, impl='cuda'):
+    """Downsample by `down` (reference :352-387)."""
+    downx, downy = _parse_scaling(down)
+    px0, px1, py0, py1 = _parse_padding(padding)
+    fw, fh = _get_filter_size(f)
+    p = [px0 + (fw - downx + 1) // 2, px1 + (fw - downx) // 2, py0 + (fh - downy + 1) // 2, py1 + (fh - downy) // 2]
+    return upfirdn2d(x, f, down=down, padding=p, flip_filter=flip_filter, gain=gain, impl=impl)

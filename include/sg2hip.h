@@ -1,0 +1,124 @@
+/*
+ * sg2hip -- C-ABI of the MI355X (gfx950) kernels of the StyleGAN2-ADA training hot path.
+ *
+ * The library (libsg2hip.so, built from gan-track_amd/csrc) replaces the reference's two
+ * pybind11 CUDA plugins and the cuDNN convolutions reached through conv2d_gradfix:
+ *
+ *   reference (ltronchin/Gan-track, src/models/stylegan3 = SG3/)          replaced by
+ *   SG3/torch_utils/ops/bias_act.cpp:32   bias_act(x,b,xref,yref,dy,grad,dim,act,alpha,gain,clamp)
+ *                                                                          -> sg2_bias_act
+ *   SG3/torch_utils/ops/upfirdn2d.cpp:16  upfirdn2d(x,f,upx,upy,downx,downy,padx0,padx1,pady0,pady1,flip,gain)
+ *                                                                          -> sg2_upfirdn2d
+ *   SG3/torch_utils/ops/conv2d_gradfix.py:37-45 (F.conv2d / F.conv_transpose2d, cuDNN)
+ *                                                                          -> sg2_conv2d (fwd + dgrad)
+ *   autograd weight gradient of those convolutions (cuDNN wgrad)          -> sg2_conv2d_wgrad
+ *   SG3/torch_utils/ops/grid_sample_gradfix.py:28-65 (aten grid_sampler_2d fwd/bwd)
+ *                                                                          -> sg2_grid_sample_fwd / _bwd
+ *   SG3/training/networks_stylegan2.py:59-63 demodulation coefficients    -> sg2_demod_coefs
+ *   SG3/training/training_loop_mi_multimodal.py:343-351,363-364 (nan_to_num + Adam, EMA lerp)
+ *                                                                          -> sg2_adam_step, sg2_lerp
+ *
+ * Conventions
+ *  - Every pointer is a device pointer; the library never allocates or frees device memory and keeps
+ *    no mutable global state (re-entrant; safe to capture into a hipGraph).
+ *  - `stream` is a hipStream_t (pass the caller's current stream; NULL = default stream).
+ *  - dtype codes: SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2 (arithmetic is always f32 internally).
+ *  - 4-D activations are NHWC in memory (torch channels_last); sizes are given as [N, C, H, W]
+ *    like the reference, strides (in elements) as [sN, sC, sH, sW] where a function accepts strides.
+ *  - Return value: 0 = success, < 0 = invalid argument (see sg2_last_error()), > 0 = hipError_t of
+ *    the launch.  The Python wrapper raises RuntimeError with sg2_last_error() -- the same behaviour
+ *    as the reference's TORCH_CHECK / AT_CUDA_CHECK.
+ */
+#ifndef SG2HIP_H
+#define SG2HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG2_ABI_VERSION 1
+
+enum sg2_dtype { SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2 };
+
+/* ABI version of the loaded library (SG2_ABI_VERSION). */
+int sg2_abi_version(void);
+
+/* Message of the last failing call on this host thread ("" if none). */
+const char* sg2_last_error(void);
+
+/* Fused bias + activation + gain + clamp, and its 1st/2nd order gradients.
+ * Replaces SG3/torch_utils/ops/bias_act.cpp:32 (kernel semantics bias_act.cu:23-147).
+ *   y[i] = f(x[i], b[(i / step_b) % size_b], ...) for i < numel.
+ *   grad = 0: y = clamp(act(x + b) * gain)
+ *   grad = 1: y = x * act'(...) * gain masked by |yref| < clamp     (x holds dL/dy)
+ *   grad = 2: second-order term (needs dy, the first-order incoming gradient)
+ * b / xref / yref / dy may be NULL (absent, like the reference's empty tensor).
+ * act: 1 linear, 2 relu, 3 lrelu, 4 tanh, 5 sigmoid, 6 elu, 7 selu, 8 softplus, 9 swish
+ * (the reference's cuda_idx, bias_act.py:21-31).  clamp < 0 disables clamping. */
+int sg2_bias_act(void* y, const void* x, const void* b, const void* xref, const void* yref, const void* dy,
+                 int dtype, int64_t numel, int64_t size_b, int64_t step_b, int grad, int act, float alpha,
+                 float gain, float clamp, void* stream);
+
+/* Upsample (zero insertion), pad/crop, 2-D FIR, downsample.
+ * Replaces SG3/torch_utils/ops/upfirdn2d.cpp:16 (semantics upfirdn2d.py:118-211).
+ *   in/out sizes [N, C, H, W], strides in elements (any layout); f is a float32 [fh, fw] filter
+ *   (row-major, device).  flip = 0: true convolution (filter flipped), 1: correlation.
+ *   Output size must equal ((in*up + pad0 + pad1 - f) / down) + 1 per axis. */
+int sg2_upfirdn2d(void* y, const void* x, const float* f, int dtype, const int64_t* in_size,
+                  const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride, int fw, int fh,
+                  int upx, int upy, int downx, int downy, int padx0, int padx1, int pady0, int pady1, int flip,
+                  float gain, void* stream);
+
+/* Dense 2-D convolution on NHWC activations (implicit GEMM on MFMA).
+ *   transpose = 0: y = conv2d(x, w, stride, padding)            (torch.nn.functional.conv2d)
+ *                  w packed [Cout][KH][KW][Cin]  (= OIHW weight in channels_last memory)
+ *   transpose = 1: y = conv_transpose2d(x, w, stride, padding)  (torch.nn.functional.conv_transpose2d)
+ *                  w packed [Cout][KH][KW][Cin]  (= the [Cin, Cout, KH, KW] torch weight permuted (1,2,3,0))
+ *   x [N, H, W, Cin], y [N, OH, OW, Cout] (OH/OW explicit: output_padding is implied).
+ *   workspace: float32 scratch of >= N*OH*OW*Cout elements, or NULL (then no split-K is used). */
+int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W, int Cout,
+               int OH, int OW, int KH, int KW, int stride, int pad_y, int pad_x, int transpose,
+               float* workspace, int64_t workspace_elems, void* stream);
+
+/* Weight gradient of sg2_conv2d (transpose = 0 form):
+ *   dw[a][ky][kx][b] = sum_{n,oy,ox} g[n,oy,ox,a] * x[n, oy*stride+ky-pad_y, ox*stride+kx-pad_x, b]
+ *   g [N, OH, OW, A] NHWC, x [N, H, W, B] NHWC; dw is float32 [A][KH][KW][B], overwritten.
+ *   The conv_transpose2d weight gradient is the same call with (g, x) = (x_of_convT, dy). */
+int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
+                     int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, void* stream);
+
+/* Bilinear grid sample, zeros padding, align_corners = False (the only mode the reference uses,
+ * grid_sample_gradfix.py:9-12).  in [N,C,Hi,Wi] any strides; grid float32 [N,Ho,Wo,2] contiguous;
+ * out [N,C,Ho,Wo] any strides. */
+int sg2_grid_sample_fwd(void* out, const void* in, const float* grid, int dtype, const int64_t* in_size,
+                        const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
+                        void* stream);
+
+/* Gradient of sg2_grid_sample_fwd w.r.t. its input: gin (float32, [N,C,Hi,Wi] with in_stride) is
+ * zero-filled then accumulated. */
+int sg2_grid_sample_bwd(float* gin, const void* gout, const float* grid, int dtype, const int64_t* in_size,
+                        const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
+                        void* stream);
+
+/* Demodulation coefficients d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps), wsq[o,i] = sum_k w[o,i,k]^2
+ * (SG3/training/networks_stylegan2.py:59-63, summation regrouped).  s [N,I] f32, w [O,I*KK] f32. */
+int sg2_demod_coefs(float* d, const float* s, const float* w, int N, int O, int I, int KK, float eps,
+                    void* stream);
+
+/* Adam step on a flat float32 parameter vector (torch.optim.Adam semantics, no weight decay,
+ * amsgrad off) with the reference's gradient sanitation fused in front:
+ *   g = nan_to_num(g * grad_scale, nan=0, posinf=1e5, neginf=-1e5)  (training_loop_mi_multimodal.py:346-347)
+ * step is the 1-based step count after increment. */
+int sg2_adam_step(float* param, float* exp_avg, float* exp_avg_sq, const float* grad, int64_t n, float lr,
+                  float beta1, float beta2, float eps, float grad_scale, int64_t step, void* stream);
+
+/* dst = src + (dst - src) * beta  == src.lerp(dst, beta)   (G_ema update, training_loop:363-364). */
+int sg2_lerp(float* dst, const float* src, int64_t n, float beta, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SG2HIP_H */

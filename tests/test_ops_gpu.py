@@ -1,0 +1,296 @@
+"""Parity of the HIP ops (called through the C-ABI via the product wrappers) against the CPU oracle,
+the reference's golden vectors, and torch-fp32 references for the convolution kernels.
+
+Tolerances (relative L2 error):
+  fp32 elementwise / FIR / grid_sample: 1e-5     fp32 MFMA convolutions: 1e-5
+  fp16/bf16 (fp32 accumulate) vs the fp32 reference: 1e-2 (fp16), 2e-2 (bf16)
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from golden_util import load, lit, rel_err
+from rngtape import Tape
+from oracle import sg2_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda', 0)
+
+
+def T(a, dev=DEV, rg=False):
+    return torch.from_numpy(np.array(a, dtype=np.float32)).to(dev).requires_grad_(rg)
+
+
+# ------------------------------------------------------------------ bias_act
+BA = load('bias_act.npz')
+
+
+@pytest.mark.parametrize('name', [str(n) for n in BA['names']])
+def test_bias_act_golden(name):
+    from torch_utils.ops import bias_act
+    z = BA
+    act, g, c = name.split('_g')[0], name.split('_g')[1].split('_c')[0], name.split('_c')[1]
+    gain = None if g == 'None' else float(g)
+    clamp = None if c == 'None' else float(c)
+    for fmt in [torch.contiguous_format, torch.channels_last]:
+        x = T(z['x']).contiguous(memory_format=fmt).requires_grad_(True)
+        b = T(z['b'], rg=True)
+        y = bias_act.bias_act(x, b, act=act, gain=gain, clamp=clamp)
+        assert rel_err(y, z[f'{name}_y']) < 1e-5
+        gx, gb = torch.autograd.grad((y * T(z['dy'])).sum(), [x, b], create_graph=True)
+        assert rel_err(gx, z[f'{name}_dx']) < 1e-5
+        assert rel_err(gb, z[f'{name}_db']) < 1e-5
+        if f'{name}_ddx' in z.files:
+            hx, = torch.autograd.grad((gx * T(z['v'])).sum(), [x])
+            assert rel_err(hx, z[f'{name}_ddx']) < 1e-4
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_bias_act_lowp(dtype):
+    from torch_utils.ops import bias_act
+    x = torch.randn(4, 64, 9, 11, device=DEV).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(64, device=DEV)
+    y = bias_act.bias_act(x.to(dtype), b.to(dtype), act='lrelu', gain=np.sqrt(2), clamp=256)
+    r = O.bias_act(x.cpu(), b.cpu(), act='lrelu', gain=np.sqrt(2), clamp=256)
+    assert rel_err(y.float(), r) < (1e-2 if dtype == torch.float16 else 2e-2)
+
+
+def test_bias_act_odd_sizes():
+    from torch_utils.ops import bias_act
+    for shape in [(3, 5), (1, 7, 3, 3), (2, 3, 1, 13)]:
+        x = torch.randn(*shape, device=DEV)
+        b = torch.randn(shape[1], device=DEV)
+        y = bias_act.bias_act(x, b, act='swish', clamp=0.5)
+        assert rel_err(y, O.bias_act(x.cpu(), b.cpu(), act='swish', clamp=0.5)) < 1e-5
+
+
+def test_rejects_cpu():
+    from torch_utils.ops import bias_act, upfirdn2d
+    with pytest.raises(RuntimeError):
+        bias_act.bias_act(torch.zeros(2, 3))
+    with pytest.raises(RuntimeError):
+        upfirdn2d.upfirdn2d(torch.zeros(1, 1, 4, 4), None)
+
+
+# ------------------------------------------------------------------ upfirdn2d
+UPF = load('upfirdn2d.npz')
+
+
+@pytest.mark.parametrize('name', [str(n) for n in UPF['names']])
+@pytest.mark.parametrize('fmt', ['nchw', 'nhwc'])
+def test_upfirdn2d_golden(name, fmt):
+    from torch_utils.ops import upfirdn2d
+    z = UPF
+    kw = lit(z, f'{name}_kw')
+    f = z[f'{name}_f']
+    f = None if f.size == 0 else torch.from_numpy(f).to(DEV)
+    x = T(z[f'{name}_x'])
+    if fmt == 'nhwc':
+        x = x.contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = upfirdn2d.upfirdn2d(x, f, **kw)
+    assert rel_err(y, z[f'{name}_y']) < 1e-5
+    dx, = torch.autograd.grad((y * T(z[f'{name}_dy'])).sum(), [x])
+    assert rel_err(dx, z[f'{name}_dx']) < 1e-5
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
+def test_upfirdn2d_vec_path(dtype):
+    """Channel-vectorised NHWC kernel on network-shaped tensors, vs the oracle in fp32."""
+    from torch_utils.ops import upfirdn2d
+    f = upfirdn2d.setup_filter([1, 3, 3, 1])
+    x = torch.randn(2, 64, 17, 17)
+    cases = [dict(padding=[1, 1, 1, 1], gain=4), dict(padding=[2, 2, 2, 2]), dict(down=2, padding=[1, 1, 1, 1]),
+             dict(up=2, padding=[2, 1, 2, 1], gain=4)]
+    tol = {torch.float32: 1e-5, torch.float16: 2e-3, torch.bfloat16: 1e-2}[dtype]
+    for kw in cases:
+        xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+        y = upfirdn2d.upfirdn2d(xd, f.to(DEV), **kw)
+        r = O.upfirdn2d(x.to(dtype).float(), f, **kw)
+        assert rel_err(y.float(), r) < tol, kw
+
+
+# ------------------------------------------------------------------ convolutions (torch fp32 reference)
+CONV_CASES = [
+    # N, Cin, H, W, Cout, k, stride, pad
+    (2, 64, 16, 16, 64, 3, 1, 1),
+    (2, 32, 9, 9, 48, 3, 2, 0),
+    (3, 16, 8, 8, 24, 1, 1, 0),
+    (2, 1, 8, 8, 16, 1, 1, 0),
+    (2, 3, 10, 10, 8, 3, 1, 1),
+    (2, 13, 7, 7, 130, 3, 1, 1),
+    (2, 513, 4, 4, 64, 3, 1, 1),
+    (1, 128, 4, 4, 256, 3, 1, 1),
+    (32, 512, 4, 4, 512, 3, 1, 1),
+]
+
+
+def _ref_conv(x, w, stride, pad, transpose=False, out_hw=None):
+    x, w = x.double().cpu(), w.double().cpu()
+    if transpose:
+        y = F.conv_transpose2d(x, w, stride=stride, padding=pad)
+        if out_hw is not None and tuple(y.shape[2:]) != tuple(out_hw):
+            op = (out_hw[0] - y.shape[2], out_hw[1] - y.shape[3])
+            y = F.conv_transpose2d(x, w, stride=stride, padding=pad, output_padding=op)
+        return y
+    return F.conv2d(x, w, stride=stride, padding=pad)
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
+def test_conv2d_fwd_bwd(case, dtype):
+    from torch_utils.ops import conv2d_gradfix as cg
+    N, Cin, H, W, Cout, k, s, p = case
+    torch.manual_seed(0)
+    x = torch.randn(N, Cin, H, W)
+    w = torch.randn(Cout, Cin, k, k) / np.sqrt(Cin * k * k)
+    tol = {torch.float32: 1e-5, torch.float16: 4e-3, torch.bfloat16: 2e-2}[dtype]
+    xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    wd = w.to(DEV, dtype).requires_grad_(True)
+    y = cg.conv2d(xd, wd, stride=s, padding=p)
+    xr, wr = x.to(dtype).double(), w.to(dtype).double()
+    yr = _ref_conv(xr, wr, s, p)
+    assert y.shape == yr.shape
+    assert rel_err(y.float(), yr) < tol
+    dy = torch.randn(y.shape)
+    gx, gw = torch.autograd.grad(y, [xd, wd], dy.to(DEV, dtype))
+    xr.requires_grad_(True)
+    wr.requires_grad_(True)
+    gxr, gwr = torch.autograd.grad(F.conv2d(xr, wr, stride=s, padding=p), [xr, wr], dy.to(dtype).double())
+    assert rel_err(gx.float(), gxr) < tol
+    assert rel_err(gw.float(), gwr) < tol * 2
+
+
+@pytest.mark.parametrize('case', [(2, 64, 8, 8, 64, 3, 2, 0), (2, 16, 5, 5, 8, 3, 2, 1), (2, 32, 4, 4, 32, 1, 1, 0),
+                                  (4, 512, 4, 4, 512, 3, 2, 0), (2, 24, 6, 6, 40, 3, 1, 1)])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16])
+def test_conv_transpose2d(case, dtype):
+    from torch_utils.ops import conv2d_gradfix as cg
+    N, Cin, H, W, Cout, k, s, p = case
+    torch.manual_seed(1)
+    x = torch.randn(N, Cin, H, W)
+    w = torch.randn(Cin, Cout, k, k) / np.sqrt(Cin * k * k)
+    tol = {torch.float32: 1e-5, torch.float16: 4e-3}[dtype]
+    xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    wd = w.to(DEV, dtype).requires_grad_(True)
+    y = cg.conv_transpose2d(xd, wd, stride=s, padding=p)
+    xr, wr = x.to(dtype).double().requires_grad_(True), w.to(dtype).double().requires_grad_(True)
+    yr = F.conv_transpose2d(xr, wr, stride=s, padding=p)
+    assert y.shape == yr.shape
+    assert rel_err(y.float(), yr.detach()) < tol
+    dy = torch.randn(y.shape)
+    gx, gw = torch.autograd.grad(y, [xd, wd], dy.to(DEV, dtype))
+    gxr, gwr = torch.autograd.grad(yr, [xr, wr], dy.to(dtype).double())
+    assert rel_err(gx.float(), gxr) < tol
+    assert rel_err(gw.float(), gwr) < tol * 2
+
+
+def test_conv_double_backward():
+    """Second order through conv (the PL / R1 path): d/dw <dL/dx, v> vs torch fp64 on CPU."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(2)
+    x = torch.randn(2, 16, 8, 8)
+    w = torch.randn(24, 16, 3, 3) / 12
+    v = torch.randn(2, 16, 8, 8)
+    res = []
+    for dev, dt in [(DEV, torch.float32), (torch.device('cpu'), torch.float64)]:
+        xd = x.to(dev, dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        wd = w.to(dev, dt).requires_grad_(True)
+        fn = cg.conv2d if dev.type == 'cuda' else F.conv2d
+        y = fn(xd, wd, stride=1, padding=1)
+        l1 = (y.square()).sum()
+        gx, = torch.autograd.grad(l1, [xd], create_graph=True)
+        gw2, gx2 = torch.autograd.grad((gx * v.to(dev, dt)).sum(), [wd, xd])
+        res.append((gw2.double().cpu(), gx2.double().cpu()))
+    assert rel_err(res[0][0], res[1][0]) < 1e-5
+    assert rel_err(res[0][1], res[1][1]) < 1e-5
+
+
+# ------------------------------------------------------------------ grid_sample
+def test_grid_sample():
+    from torch_utils.ops import grid_sample_gradfix as gs
+    torch.manual_seed(3)
+    x = torch.randn(2, 3, 20, 24)
+    theta = torch.tensor([[[1.05, 0.1, 0.03], [-0.08, 0.95, -0.02]], [[0.9, -0.2, 0.1], [0.15, 1.1, 0.05]]])
+    grid = F.affine_grid(theta, [2, 3, 30, 26], align_corners=False)
+    xd = x.to(DEV).requires_grad_(True)
+    y = gs.grid_sample(xd, grid.to(DEV))
+    yr = F.grid_sample(x.double(), grid.double(), mode='bilinear', padding_mode='zeros', align_corners=False)
+    assert rel_err(y, yr) < 1e-5
+    dy = torch.randn(y.shape)
+    dyd = dy.to(DEV).requires_grad_(True)
+    gx, = torch.autograd.grad(y, [xd], dyd, create_graph=True)
+    xr = x.double().requires_grad_(True)
+    gxr, = torch.autograd.grad(F.grid_sample(xr, grid.double(), align_corners=False), [xr], dy.double())
+    assert rel_err(gx, gxr) < 1e-5
+    # backward-of-backward w.r.t. the incoming gradient = forward sampling of v
+    v = torch.randn(gx.shape)
+    ggo, = torch.autograd.grad((gx * v.to(DEV)).sum(), [dyd])
+    assert rel_err(ggo, F.grid_sample(v.double(), grid.double(), align_corners=False)) < 1e-5
+
+
+# ------------------------------------------------------------------ modulated conv + conv layers (golden)
+CV = load('conv.npz')
+
+
+@pytest.mark.parametrize('name', [str(n) for n in CV['names'] if str(n).startswith('modconv')])
+def test_modconv_golden(name):
+    from training import networks_stylegan2 as net
+    from torch_utils.ops import upfirdn2d
+    z = CV
+    up = int(name.split('_up')[1][0])
+    demod = bool(int(name.split('_d')[1][0]))
+    fused = bool(int(name.split('_f')[1][0]))
+    x, w, s, nz = (T(z[f'{name}_{k}'], rg=True) for k in ['x', 'w', 's', 'noise'])
+    y = net.modulated_conv2d(x, w, s, noise=nz, up=up, padding=1,
+                             resample_filter=upfirdn2d.setup_filter([1, 3, 3, 1]).to(DEV), demodulate=demod,
+                             flip_weight=(up == 1), fused_modconv=fused)
+    assert rel_err(y, z[f'{name}_y']) < 1e-5
+    grads = torch.autograd.grad((y * T(z[f'{name}_dy'])).sum(), [x, w, s, nz])
+    for k, g in zip(['dx', 'dw', 'ds', 'dnoise'], grads):
+        assert rel_err(g, z[f'{name}_{k}']) < 1e-5, k
+
+
+@pytest.mark.parametrize('name', [str(n) for n in CV['names'] if not str(n).startswith('modconv')])
+def test_conv_layer_golden(name):
+    from training import networks_stylegan2 as net
+    z = CV
+    layer = net.Conv2dLayer(**lit(z, f'{name}_kw')).to(DEV)
+    with torch.no_grad():
+        layer.weight.copy_(T(z[f'{name}_w']))
+        if layer.bias is not None:
+            layer.bias.copy_(T(z[f'{name}_b']))
+    x = T(z[f'{name}_x'], rg=True)
+    y = layer(x, gain=float(z[f'{name}_gain']))
+    assert rel_err(y, z[f'{name}_y']) < 1e-5
+    params = [x, layer.weight] + ([layer.bias] if layer.bias is not None else [])
+    grads = torch.autograd.grad((y * T(z[f'{name}_dy'])).sum(), params)
+    assert rel_err(grads[0], z[f'{name}_dx']) < 1e-5
+    assert rel_err(grads[1], z[f'{name}_dw']) < 1e-5
+    if layer.bias is not None:
+        assert rel_err(grads[2], z[f'{name}_db']) < 1e-5
+
+
+# ------------------------------------------------------------------ augment pipe (golden)
+AU = load('augment.npz')
+
+
+@pytest.mark.parametrize('name', [str(n) for n in AU['names']])
+def test_augment_golden(name):
+    from training import augment_mi
+    z = AU
+    cfg = lit(z, f'{name.split("_")[0]}_cfg')
+    pipe = augment_mi.AugmentPipe(run_dir=None, batch_size=2, **cfg).to(DEV)
+    x = T(z[f'{name}_x'], rg=True)
+    if name.endswith('_rand'):
+        pipe.p.fill_(float(z[f'{name}_p']))
+        tape = Tape.from_npz(z, prefix=f'{name}_tape')
+        with tape.replay():
+            y = pipe(x, False)
+        assert tape.pos == len(tape.entries)
+    else:
+        y = pipe(x, False, debug_percentile=float(name.split('_p')[1]))
+    assert rel_err(y, z[f'{name}_y']) < 2e-5
+    dx, = torch.autograd.grad((y * T(z[f'{name}_dy'])).sum(), [x])
+    assert rel_err(dx, z[f'{name}_dx']) < 2e-5
