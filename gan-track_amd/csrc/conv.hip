@@ -28,7 +28,7 @@
 namespace sg2 {
 namespace {
 
-constexpr int kMaxTaps = 16;
+constexpr int kMaxTaps = 64;
 
 struct TapTable {
     int n;
@@ -449,7 +449,7 @@ extern "C" int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int 
 
     // Output phases.
     struct Phase { ConvArgs a; };
-    Phase ph[16];
+    Phase ph[16];  // stride <= 4
     int nph = 0;
     ConvArgs base{};
     base.x = x; base.w = w; base.y = y; base.acc = nullptr;

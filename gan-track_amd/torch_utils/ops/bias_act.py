@@ -92,7 +92,10 @@ def _bias_act_fn(dim, act, alpha, gain, clamp):
             ctx.fmt = fmt
             y = x if (trivial and b is None) else _launch(x, b, None, None, None, 0, dim, spec, alpha, gain, clamp)
             keep_x = 'x' in spec.ref or spec.has_2nd_grad
-            ctx.save_for_backward(x if keep_x else None, b if keep_x else None, y if 'y' in spec.ref else None)
+            # y is also needed for the clamp mask when clamping is on (the reference's plugin drops it
+            # for 'linear', so its GPU gradient ignores the clamp there; its CPU path and this build mask)
+            keep_y = 'y' in spec.ref or clamp >= 0
+            ctx.save_for_backward(x if keep_x else None, b if keep_x else None, y if keep_y else None)
             return y
 
         @staticmethod
