@@ -69,7 +69,7 @@ class GradReducer:
 
         def hook(p):
             bi = self._bucket_of.get(p)
-            if bi is None:
+            if bi is None or p.grad is None:   # the hook also fires for structurally-zero (undefined) grads
                 return
             self._ready[bi] += 1
             if self._ready[bi] == expected * len(self._bucket_list[bi]) and not self._launched[bi]:
