@@ -114,31 +114,43 @@ def one_step(tr, args, device, real, real_c):
 
 
 def roofline(device, res, cbase, dtype):
-    """Average duration of the dominant kernel (forward MFMA conv of the top-resolution 3x3 layer,
-    [32, C, res, res] -> [32, C, res, res]) measured with HIP events on its launch stream."""
+    """Average duration of the dominant kernel -- the LDS-halo MFMA 3x3 conv (sg2_conv3x3) of the
+    top-resolution layer, [32, C, res, res] -> [32, C, res, res] with the fused modulation/demod/noise/
+    bias/lrelu/clamp epilogue -- measured with HIP events on its launch stream."""
     from torch_utils.ops import conv2d_gradfix as cg
     C = min(cbase // res, 512)
     N = 32
     x = torch.randn([N, C, res, res], device=device, dtype=dtype).contiguous(memory_format=torch.channels_last)
     w = (torch.randn([C, C, 3, 3], device=device) / np.sqrt(C * 9)).to(dtype)
     wp = cg._pack_conv(w)
+    s = torch.rand([N, C], device=device) + 0.5
+    d = torch.rand([N, C], device=device) + 0.5
+    noise = torch.randn([N, res, res], device=device, dtype=dtype)
+    b = torch.zeros([C], device=device)
+
+    def launch():
+        cg.conv3x3_fused(x, wp, C, in_scale=s, out_scale=d, noise=noise, noise_gain=0.1, bias=b, act=1,
+                         gain=float(np.sqrt(2)), clamp=256.0)
     for _ in range(3):
-        cg._conv_raw(x, wp, C, res, res, 3, 3, 1, (1, 1), False)
+        launch()
     reps = 20
     stream = torch.cuda.current_stream(device)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(reps):
-        cg._conv_raw(x, wp, C, res, res, 3, 3, 1, (1, 1), False)
+        launch()
     e1.record(stream)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / reps
     flops = 2.0 * N * C * C * 9 * res * res
     ach = flops / (ms * 1e-3) / 1e12
-    return {'kernel': f'conv_fwd_kernel<{str(dtype).split(".")[-1]},128,64> (G/D {res}^2 3x3, C={C}, N={N})',
+    byts = (2 * N * C * res * res + N * res * res) * x.element_size() + C * C * 9 * x.element_size()
+    return {'kernel': f'conv3x3_halo_kernel<{str(dtype).split(".")[-1]},TW=32,scale,epilogue> '
+                      f'(G {res}^2 modulated 3x3 conv, C={C}, N={N})',
             'bound': 'mfma', 'achieved': round(ach, 2), 'peak': MFMA_PEAK_FP16, 'unit': 'TFLOP/s',
             'frac': round(ach / MFMA_PEAK_FP16, 4), 'traffic': None, 'ms_per_launch': round(ms, 4),
-            'algorithmic_flops_per_launch': flops}
+            'algorithmic_flops_per_launch': flops, 'algorithmic_hbm_bytes_per_launch': byts,
+            'achieved_hbm_GBps': round(byts / (ms * 1e-3) / 1e9, 1)}
 
 
 def cpu_baseline(args):

@@ -88,19 +88,22 @@ __device__ __forceinline__ f32x4 mfma16(const T* pa, const T* pb, f32x4 c) {
 
 template <typename T, bool VEC>
 struct Loader {
-    // A 16-byte (or masked scalar) chunk of one tile row.
+    // A 16-byte chunk of one tile row.  The load itself is unconditional (callers pass a clamped,
+    // always-valid row pointer); masking is a select applied when the registers are written to LDS,
+    // so no branch sits between the prefetch and the MFMAs (see conv3x3.hip).
     typedef T vecT __attribute__((ext_vector_type(Traits<T>::V)));
-    static __device__ __forceinline__ vecT load(const T* row, int c, int Cin, bool valid) {
+    static __device__ __forceinline__ vecT load(const T* row, int c, int Cin) {
         constexpr int V = Traits<T>::V;
+        if (VEC) return *(const vecT*)(row + (c < Cin ? c : 0));
         vecT v;
-        if (VEC) {
-            if (valid && c < Cin) return *(const vecT*)(row + c);
 #pragma unroll
-            for (int j = 0; j < V; ++j) v[j] = (T)0.f;
-            return v;
-        }
+        for (int j = 0; j < V; ++j) v[j] = row[(c + j < Cin) ? c + j : 0];
+        return v;
+    }
+    static __device__ __forceinline__ vecT mask(vecT v, int c, int Cin, bool valid) {
+        constexpr int V = Traits<T>::V;
 #pragma unroll
-        for (int j = 0; j < V; ++j) v[j] = (valid && c + j < Cin) ? row[c + j] : (T)0.f;
+        for (int j = 0; j < V; ++j) v[j] = (valid && c + j < Cin) ? v[j] : (T)0.f;
         return v;
     }
 };
@@ -144,32 +147,39 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     const int k_end = min(a.nk, k_begin + a.kper);
 
     vecT ra[PA], rb[PB];
+    bool ra_ok[PA], rb_ok[PB];
+    int cur_c = 0;
     auto gload = [&](int kc) {
         const int t = kc / a.nck;
         const int c = (kc - t * a.nck) * BK + lcol;
+        cur_c = c;
         const int dy = a.taps.dy[t], dx = a.taps.dx[t], wt = a.taps.w[t];
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             const int iy = a_qy[i] + dy, ix = a_qx[i] + dx;
             const bool ok = a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            ra_ok[i] = ok;
             const T* row = x + (((int64_t)a_n[i] * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.Cin;
-            ra[i] = Loader<T, VEC>::load(row, c, a.Cin, ok);
+            ra[i] = Loader<T, VEC>::load(row, c, a.Cin);
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
             const int o = n0 + lrow + i * RPP;
             const bool ok = o < a.Cout;
+            rb_ok[i] = ok;
             const T* row = w + (ok ? o : 0) * wrow + (int64_t)wt * a.Cin;
-            rb[i] = Loader<T, VEC>::load(row, c, a.Cin, ok);
+            rb[i] = Loader<T, VEC>::load(row, c, a.Cin);
         }
     };
     auto sstore = [&](int buf) {
         T* As = lds[buf];
         T* Bs = lds[buf] + BM * LDK;
 #pragma unroll
-        for (int i = 0; i < PA; ++i) *(vecT*)(As + (lrow + i * RPP) * LDK + lcol) = ra[i];
+        for (int i = 0; i < PA; ++i)
+            *(vecT*)(As + (lrow + i * RPP) * LDK + lcol) = Loader<T, VEC>::mask(ra[i], cur_c, a.Cin, ra_ok[i]);
 #pragma unroll
-        for (int i = 0; i < PB; ++i) *(vecT*)(Bs + (lrow + i * RPP) * LDK + lcol) = rb[i];
+        for (int i = 0; i < PB; ++i)
+            *(vecT*)(Bs + (lrow + i * RPP) * LDK + lcol) = Loader<T, VEC>::mask(rb[i], cur_c, a.Cin, rb_ok[i]);
     };
 
     f32x4 acc[TM][TN];
@@ -311,14 +321,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
     const int p_end = min(a.M, p_begin + a.kper);
 
     vecT ra[PA], rb[PB];
+    bool ra_ok[PA], rb_ok[PB];
     auto gload = [&](int p0) {
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             const int r = ga_row + i * RPA;
             const int m = p0 + r;
             const bool ok = r < BK && m < p_end;
+            ra_ok[i] = ok;
             const T* row = g + (int64_t)(ok ? m : 0) * a.A;
-            ra[i] = Loader<T, VEC>::load(row, a0 + ga_col, a.A, ok);
+            ra[i] = Loader<T, VEC>::load(row, a0 + ga_col, a.A);
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
@@ -326,16 +338,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
             const int m = p0 + r;
             bool ok = r < BK && m < p_end;
             int n = 0, iy = 0, ix = 0;
-            if (ok) {
+            {
+                const int mm = ok ? m : 0;
                 const int per = a.OH * a.OW;
-                n = m / per;
-                const int rr = m - n * per;
+                n = mm / per;
+                const int rr = mm - n * per;
                 iy = (rr / a.OW) * a.stride + ky - a.pady;
                 ix = (rr % a.OW) * a.stride + kx - a.padx;
-                ok = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+                ok = ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
             }
+            rb_ok[i] = ok;
             const T* row = x + (((int64_t)n * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.B;
-            rb[i] = Loader<T, VEC>::load(row, b0 + xb_col, a.B, ok);
+            rb[i] = Loader<T, VEC>::load(row, b0 + xb_col, a.B);
         }
     };
     auto sstore = [&](int buf) {
@@ -344,12 +358,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             const int r = ga_row + i * RPA;
-            if (r < BK) *(vecT*)(As + r * LDA + ga_col) = ra[i];
+            if (r < BK) *(vecT*)(As + r * LDA + ga_col) = Loader<T, VEC>::mask(ra[i], a0 + ga_col, a.A, ra_ok[i]);
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
             const int r = xb_row + i * RPB;
-            if (r < BK) *(vecT*)(Bs + r * LDB + xb_col) = rb[i];
+            if (r < BK) *(vecT*)(Bs + r * LDB + xb_col) = Loader<T, VEC>::mask(rb[i], b0 + xb_col, a.B, rb_ok[i]);
         }
     };
 

@@ -1,0 +1,328 @@
+// 3x3 / stride 1 / pad 1 convolution with an LDS halo tile, for the 16-bit layers (f16 / bf16,
+// the 32^2 .. 256^2 blocks of G and D) -- the bulk of the training FLOPs.
+//
+// Why a second kernel next to the generic implicit GEMM (conv.hip): the generic kernel gathers the
+// A operand per tap from global memory, so every input pixel is fetched 9 times.  Here a workgroup
+// owns a TH x TW tile of output pixels of one sample and BN = 64 output channels; per 32-channel
+// chunk of the input it stages the (TH+2) x (TW+2) halo ONCE in LDS plus the chunk's 9 x 64 x 32
+// weights, then runs all 9 taps as MFMAs reading shifted windows of the halo:
+//   per chunk and wave (64 pixels x 64 channels): 9 taps x 16 v_mfma_f32_16x16x32 = 144 MFMAs
+//   against 9 x 8 ds_read_b128 fragment reads; halo pixel rows padded to 80 B so the 16 rows of a
+//   fragment read hit 16 distinct 16-byte bank slots (conflict free).
+// The two LDS buffers are filled through registers: the next chunk's global loads are issued
+// before the current chunk's MFMAs and written after them (one barrier per chunk).
+//
+// Fused prologue / epilogue (the StyleGAN2 modulated-conv layer, networks_stylegan2.py:309-328):
+//   A operand : x[n,y,x,c] * in_scale[n,c]                       (modulation, optional)
+//   raw out   : c = conv(.)                                      (optional second output, for backward)
+//   epilogue  : z = c * out_scale[n,o] + noise[n,y,x] * noise_gain + bias[o]  (demod + noise + bias)
+//               y = clamp(act(z) * gain, +-clamp), act in {linear, lrelu(alpha)}
+#include "sg2_common.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace sg2 {
+namespace {
+
+constexpr int CK = 32;              // input channels per chunk (= MFMA K)
+constexpr int BN = 64;              // output channels per workgroup
+constexpr int PX = CK + 8;          // LDS pixel / weight-row stride in elements (80 B)
+
+struct Conv3Args {
+    const void* x;
+    const void* w;          // packed [Cout][9][Cin]
+    void* y;
+    void* y_raw;            // optional: conv result before the epilogue
+    const float* in_scale;  // [N, Cin] or null
+    const float* out_scale; // [N, Cout] or null
+    const void* noise;      // [N, H, W] (dtype T) or null
+    const float* bias;      // [Cout] or null
+    float noise_gain, alpha, gain, clamp;
+    int act;                // 0 linear, 1 lrelu
+    int N, H, W, Cin, Cout;
+    int tiles_x, tiles_y;
+};
+
+template <typename T>
+using v8 = typename std::conditional<std::is_same<T, bf16_t>::value, bf16x8, f16x8>::type;
+
+template <typename T>
+__device__ __forceinline__ f32x4 mma(v8<T> a, v8<T> b, f32x4 c) {
+    if constexpr (std::is_same<T, bf16_t>::value)
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// TW: tile width (pixels); TH = 256 / TW.  4 waves, each owns 64 consecutive tile pixels x 64 channels.
+// NBUF = 2: double-buffered chunks (1 workgroup / CU); NBUF = 1: single buffer, 2 workgroups / CU
+// overlap each other's staging (better when Cin spans only a couple of chunks).
+template <typename T, int TW, bool SCALE_IN, bool EPI, int NBUF>
+__global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
+    constexpr int TH = 256 / TW;
+    constexpr int HW_ = TW + 2, HH = TH + 2, HP = HW_ * HH;          // halo pixels
+    constexpr int HALO = HP * PX;                                      // elements per halo buffer
+    constexpr int WTS = 9 * BN * PX;                                   // elements per weight buffer
+    constexpr int NH = (HP * 4 + 255) / 256;                          // halo 16-B loads per thread
+    constexpr int NW = (9 * BN * 4) / 256;                            // weight 16-B loads per thread (= 9)
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    T* smem = (T*)smem_raw;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tile = blockIdx.x;
+    const int n = tile / (a.tiles_x * a.tiles_y);
+    const int tr = tile - n * a.tiles_x * a.tiles_y;
+    const int ty0 = (tr / a.tiles_x) * TH, tx0 = (tr % a.tiles_x) * TW;
+    const int o0 = blockIdx.y * BN;
+    const T* __restrict__ x = (const T*)a.x;
+    const T* __restrict__ w = (const T*)a.w;
+    const int nchunks = (a.Cin + CK - 1) / CK;
+
+    // ---- staging geometry ----
+    int h_src[NH], h_dst[NH];
+    bool h_ok[NH];
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+        const int idx = tid + i * 256;             // (pixel, 16-byte quarter)
+        const int p = idx >> 2, q = idx & 3;
+        const int hy = p / HW_, hx = p - hy * HW_;
+        const int iy = ty0 - 1 + hy, ix = tx0 - 1 + hx;
+        h_ok[i] = p < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+        h_src[i] = h_ok[i] ? ((n * a.H + iy) * a.W + ix) : 0;     // pixel index
+        h_dst[i] = (p < HP ? p : 0) * PX + q * 8;
+        if (p >= HP) h_dst[i] = -1;
+    }
+    const int hq = (tid & 3) * 8;
+    int w_src[NW], w_dst[NW];
+    bool w_ok[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const int idx = tid + i * 256;             // (tap, o, quarter)
+        const int r = idx >> 2;                    // 0 .. 9*BN-1
+        const int tap = r / BN, o = r - tap * BN;
+        w_ok[i] = o0 + o < a.Cout;
+        w_src[i] = (w_ok[i] ? (o0 + o) : 0) * 9 + tap;              // row index in [Cout*9]
+        w_dst[i] = (tap * BN + o) * PX + (idx & 3) * 8;
+    }
+
+    // Loads are unconditional (out-of-image / out-of-range lanes read a valid dummy address) and the
+    // zero-fill + modulation happen at the LDS write, after the MFMAs: a branch around a load would
+    // make hipcc drain vmcnt per load and serialise the prefetch against the math.
+    vec8 rh[NH], rw[NW];
+    float4 sc0, sc1;
+    bool cok = true;
+    auto gload = [&](int chunk) {
+        const int c = chunk * CK + hq;
+        cok = c < a.Cin;
+        const int cc = cok ? c : 0;
+#pragma unroll
+        for (int i = 0; i < NH; ++i) rh[i] = *(const vec8*)(x + (int64_t)h_src[i] * a.Cin + cc);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) rw[i] = *(const vec8*)(w + (int64_t)w_src[i] * a.Cin + cc);
+        if (SCALE_IN) {
+            const float* sc = a.in_scale + (int64_t)n * a.Cin + cc;
+            sc0 = *(const float4*)sc;
+            sc1 = *(const float4*)(sc + 4);
+        }
+    };
+    auto sstore = [&](int buf) {
+        T* hb = smem + buf * (HALO + WTS);
+        T* wb = hb + HALO;
+        const float scl[8] = {sc0.x, sc0.y, sc0.z, sc0.w, sc1.x, sc1.y, sc1.z, sc1.w};
+#pragma unroll
+        for (int i = 0; i < NH; ++i) {
+            if (h_dst[i] < 0) continue;
+            const bool ok = h_ok[i] && cok;
+            vec8 v;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float f = (float)rh[i][j];
+                if (SCALE_IN) f *= scl[j];
+                v[j] = (T)(ok ? f : 0.f);
+            }
+            *(vec8*)(hb + h_dst[i]) = v;
+        }
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const bool ok = w_ok[i] && cok;
+            vec8 v;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = ok ? rw[i][j] : (T)0.f;
+            *(vec8*)(wb + w_dst[i]) = v;
+        }
+    };
+
+    // ---- per-lane fragment bases ----
+    const int ko = 8 * (lane >> 4);
+    int a_base[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = wave * 64 + i * 16 + (lane & 15);
+        const int py = m / TW, px = m - py * TW;
+        a_base[i] = (py * HW_ + px) * PX + ko;     // halo position of tap (0,0)
+    }
+    const int b_base = (lane & 15) * PX + ko;
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int cur = NBUF == 2 ? (ch & 1) : 0;
+        const bool more = ch + 1 < nchunks;
+        if (more) gload(ch + 1);
+        const T* hb = smem + cur * (HALO + WTS);
+        const T* wb = hb + HALO;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const int toff = (ky * HW_ + kx) * PX;
+                const int tap = ky * 3 + kx;
+                v8<T> af[4], bfr[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) af[i] = *(const v8<T>*)(hb + a_base[i] + toff);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bfr[j] = *(const v8<T>*)(wb + tap * BN * PX + j * 16 * PX + b_base);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[i][j] = mma<T>(af[i], bfr[j], acc[i][j]);
+            }
+        }
+        if (NBUF == 1 && more) __syncthreads();   // everyone done reading before the overwrite
+        if (more) sstore(NBUF == 2 ? (cur ^ 1) : 0);
+        __syncthreads();
+    }
+
+    // ---- epilogue: fused math in registers, transpose through LDS, 16-byte row stores ----
+    // per-lane channel parameters (n is fixed per workgroup)
+    float dsc[4], bsc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int o = o0 + j * 16 + (lane & 15);
+        const int oc = o < a.Cout ? o : 0;
+        dsc[j] = (EPI && a.out_scale) ? a.out_scale[(int64_t)n * a.Cout + oc] : 1.f;
+        bsc[j] = (EPI && a.bias) ? a.bias[oc] : 0.f;
+    }
+    constexpr int OS = BN + 8;                 // LDS row stride (elements) of the output tile
+    T* ot = smem;                              // y tile  [256][OS]
+    T* rt = smem + 256 * OS;                   // raw tile [256][OS] (only if y_raw)
+    const T* nz = (const T*)a.noise;
+    const bool want_raw = a.y_raw != nullptr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = wave * 64 + i * 16 + 4 * (lane >> 4) + r;
+            float nv = 0.f;
+            if (EPI && nz) {
+                const int py = m / TW, px = m - py * TW;
+                const int oy = min(ty0 + py, a.H - 1), ox = min(tx0 + px, a.W - 1);
+                nv = (float)nz[((int64_t)n * a.H + oy) * a.W + ox] * a.noise_gain;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float v = acc[i][j][r];
+                if (want_raw) rt[m * OS + j * 16 + (lane & 15)] = (T)v;
+                if (EPI) {
+                    v = v * dsc[j] + nv + bsc[j];
+                    if (a.act == 1) v = v > 0.f ? v : v * a.alpha;
+                    v *= a.gain;
+                    if (a.clamp >= 0.f) v = fminf(fmaxf(v, -a.clamp), a.clamp);
+                }
+                ot[m * OS + j * 16 + (lane & 15)] = (T)v;
+            }
+        }
+    }
+    __syncthreads();
+    typedef T vec8o __attribute__((ext_vector_type(8)));
+    T* y = (T*)a.y;
+    T* yr = (T*)a.y_raw;
+    const bool cvec = (a.Cout % 8) == 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {               // 256 pixels x 8 chunks of 8 channels / 256 threads
+        const int idx = tid + k * 256;
+        const int m = idx >> 3, c8 = (idx & 7) * 8;
+        const int py = m / TW, px = m - py * TW;
+        const int oy = ty0 + py, ox = tx0 + px;
+        const int o = o0 + c8;
+        if (oy >= a.H || ox >= a.W || o >= a.Cout) continue;
+        const int64_t dst = (((int64_t)n * a.H + oy) * a.W + ox) * a.Cout + o;
+        if (cvec) {
+            *(vec8o*)(y + dst) = *(const vec8o*)(ot + m * OS + c8);
+            if (want_raw) *(vec8o*)(yr + dst) = *(const vec8o*)(rt + m * OS + c8);
+        } else {
+            for (int e = 0; e < 8 && o + e < a.Cout; ++e) {
+                y[dst + e] = ot[m * OS + c8 + e];
+                if (want_raw) yr[dst + e] = rt[m * OS + c8 + e];
+            }
+        }
+    }
+}
+
+template <typename T, int TW, bool SI, bool EPI, int NBUF>
+int launch3(const Conv3Args& a, hipStream_t s) {
+    constexpr int TH = 256 / TW;
+    size_t lds = NBUF * (size_t)((TW + 2) * (TH + 2) * PX + 9 * BN * PX) * sizeof(T);
+    lds = std::max(lds, (size_t)2 * 256 * (BN + 8) * sizeof(T));   // epilogue tiles
+    auto kern = conv3x3_halo_kernel<T, TW, SI, EPI, NBUF>;
+    static bool attr_set = false;   // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
+    }
+    dim3 grid(a.N * a.tiles_x * a.tiles_y, (a.Cout + BN - 1) / BN);
+    kern<<<grid, 256, lds, s>>>(a);
+    return launch_status("sg2_conv3x3");
+}
+
+template <typename T>
+int dispatch(Conv3Args& a, hipStream_t s) {
+    const bool si = a.in_scale != nullptr;
+    const bool epi = a.out_scale || a.noise || a.bias || a.act != 0 || a.gain != 1.f || a.clamp >= 0.f;
+    const int TW = a.W >= 32 ? 32 : 16;
+    a.tiles_x = (a.W + TW - 1) / TW;
+    a.tiles_y = (a.H + (256 / TW) - 1) / (256 / TW);
+    const int nbuf = (a.Cin <= 2 * CK) ? 1 : 2;
+#define L3(TWV, SIV, EPIV) return nbuf == 1 ? launch3<T, TWV, SIV, EPIV, 1>(a, s) : launch3<T, TWV, SIV, EPIV, 2>(a, s)
+    if (TW == 32) {
+        if (si) { if (epi) L3(32, true, true); else L3(32, true, false); }
+        else { if (epi) L3(32, false, true); else L3(32, false, false); }
+    } else {
+        if (si) { if (epi) L3(16, true, true); else L3(16, true, false); }
+        else { if (epi) L3(16, false, true); else L3(16, false, false); }
+    }
+#undef L3
+}
+
+}  // namespace
+}  // namespace sg2
+
+extern "C" int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
+                           int Cout, const float* in_scale, const float* out_scale, const void* noise, float noise_gain,
+                           const float* bias, int act, float alpha, float gain, float clamp, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(y && x && w, "sg2_conv3x3: null pointer");
+    SG2_CHECK(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "sg2_conv3x3: empty shape");
+    SG2_CHECK(dtype == SG2_F16 || dtype == SG2_BF16, "sg2_conv3x3: f16/bf16 only");
+    SG2_CHECK(Cin % 8 == 0, "sg2_conv3x3: Cin must be a multiple of 8");
+    SG2_CHECK(((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0, "sg2_conv3x3: 16-byte alignment required");
+    SG2_CHECK(act == 0 || act == 1, "sg2_conv3x3: act must be 0 (linear) or 1 (lrelu)");
+    SG2_CHECK((int64_t)N * H * W < INT32_MAX / 2, "sg2_conv3x3: tensor too large");
+    Conv3Args a{};
+    a.x = x; a.w = w; a.y = y; a.y_raw = y_raw; a.in_scale = in_scale; a.out_scale = out_scale; a.noise = noise;
+    a.bias = bias; a.noise_gain = noise_gain; a.alpha = alpha; a.gain = gain; a.clamp = clamp; a.act = act;
+    a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
+    hipStream_t s = as_stream(stream);
+    if (dtype == SG2_F16) return dispatch<f16_t>(a, s);
+    return dispatch<bf16_t>(a, s);
+}

@@ -63,8 +63,11 @@ def _bias_act_fn(dim, act, alpha, gain, clamp):
 
         @staticmethod
         def forward(ctx, dy, x, b, y):
-            fmt = _layout(dy)
+            ref = y if y is not None else x
+            fmt = _layout(ref) if ref is not None else _layout(dy)
             dy = _dense(dy, fmt)
+            x = _dense(x, fmt)
+            y = _dense(y, fmt)
             ctx.fmt = fmt
             dx = _launch(dy, b, x, y, None, 1, dim, spec, alpha, gain, clamp)
             ctx.save_for_backward(dy if spec.has_2nd_grad else None, x, b, y)
@@ -109,8 +112,21 @@ def _bias_act_fn(dim, act, alpha, gain, clamp):
                 db = dx.sum([i for i in range(dx.ndim) if i != dim])
             return dx, db
 
+    BiasAct.Grad = BiasActGrad
     _cache[key] = BiasAct
     return BiasAct
+
+
+def bias_act_grad(dy, y, act='linear', alpha=None, gain=None, clamp=None, dim=1):
+    """Differentiable dL/dx of y = bias_act(x, ...) given dL/dy and the saved output y (for activations
+    whose derivative is expressed through y, reference `ref='y'`).  Used by fused layer backwards."""
+    spec = activation_funcs[act]
+    assert 'x' not in spec.ref
+    alpha = float(alpha if alpha is not None else spec.def_alpha)
+    gain = float(gain if gain is not None else spec.def_gain)
+    clamp = float(clamp if clamp is not None else -1)
+    dy = _dense(dy, _layout(y))     # the kernel indexes dy and y with one flat index
+    return _bias_act_fn(dim, act, alpha, gain, clamp).Grad.apply(dy, None, None, y)
 
 
 def bias_act(x, b=None, dim=1, act='linear', alpha=None, gain=None, clamp=None, impl='cuda'):

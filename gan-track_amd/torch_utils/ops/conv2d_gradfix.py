@@ -86,6 +86,26 @@ def _pack_convT(w):         # [I, O, kh, kw] -> [O][kh][kw][I]
     return w.permute(1, 2, 3, 0).contiguous()
 
 
+def _halo_ok(x, kh, kw, stride, pad, out_hw):
+    """The LDS-halo 3x3 kernel (sg2_conv3x3) serves 16-bit 3x3/s1/p1 layers of the 16^2+ blocks."""
+    n, c, h, w = x.shape
+    return (kh == 3 and kw == 3 and stride == 1 and tuple(pad) == (1, 1) and tuple(out_hw) == (h, w) and
+            x.dtype in (torch.float16, torch.bfloat16) and c % 8 == 0 and h >= 16 and w >= 16)
+
+
+def conv3x3_fused(x, wp, cout, in_scale=None, out_scale=None, noise=None, noise_gain=0.0, bias=None, act=0,
+                  alpha=0.2, gain=1.0, clamp=-1.0, want_raw=False):
+    """sg2_conv3x3 launch.  x NHWC 16-bit, wp packed [Cout][3][3][Cin]; returns (y, raw or None)."""
+    n, cin, h, w = x.shape
+    y = torch.empty([n, cout, h, w], dtype=x.dtype, device=x.device, memory_format=_CL)
+    raw = torch.empty_like(y) if want_raw else None
+    _hip.check(_hip.lib().sg2_conv3x3(
+        _hip.ptr(y), _hip.ptr(raw), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout,
+        _hip.ptr(in_scale), _hip.ptr(out_scale), _hip.ptr(noise), float(noise_gain), _hip.ptr(bias), int(act),
+        float(alpha), float(gain), float(clamp), _hip.stream_ptr(x.device)), 'sg2_conv3x3')
+    return y, raw
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pad, out_hw):
@@ -93,7 +113,10 @@ class _Conv2d(torch.autograd.Function):
         o, i, kh, kw = w.shape
         assert x.shape[1] == i and x.dtype == w.dtype
         oh, ow = out_hw
-        y = _conv_raw(x, _pack_conv(w), o, oh, ow, kh, kw, stride, pad, False)
+        if _halo_ok(x, kh, kw, stride, pad, out_hw):
+            y, _ = conv3x3_fused(x, _pack_conv(w), o)
+        else:
+            y = _conv_raw(x, _pack_conv(w), o, oh, ow, kh, kw, stride, pad, False)
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad = stride, pad
         return y
@@ -118,7 +141,11 @@ class _ConvT2d(torch.autograd.Function):
         i, o, kh, kw = w.shape
         assert x.shape[1] == i and x.dtype == w.dtype
         oh, ow = out_hw
-        y = _conv_raw(x, _pack_convT(w), o, oh, ow, kh, kw, stride, pad, True)
+        if _halo_ok(x, kh, kw, stride, pad, out_hw):
+            # stride-1 transposed conv == correlation with the spatially flipped, transposed kernel
+            y, _ = conv3x3_fused(x, _pack_convT(w.flip([2, 3])), o)
+        else:
+            y = _conv_raw(x, _pack_convT(w), o, oh, ow, kh, kw, stride, pad, True)
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.pad = stride, pad
         return y

@@ -22,6 +22,7 @@ from torch_utils import persistence
 from torch_utils.ops import bias_act
 from torch_utils.ops import conv2d_resample
 from torch_utils.ops import fma
+from torch_utils.ops import modconv
 from torch_utils.ops import upfirdn2d
 
 _CL = torch.channels_last
@@ -207,6 +208,19 @@ class SynthesisLayer(torch.nn.Module):
             noise = torch.randn([x.shape[0], 1, self.resolution, self.resolution], device=x.device) * self.noise_strength
         if self.use_noise and noise_mode == 'const':
             noise = self.noise_const * self.noise_strength
+        if self.activation == 'lrelu' and modconv.supported(x, self.weight, self.up):
+            # one-kernel modulated conv + demod + noise + bias + lrelu + clamp (sg2_conv3x3)
+            weight = self.weight
+            if x.dtype == torch.float16:   # fp16 range pre-normalisation (:52-54)
+                weight = weight * (1 / np.sqrt(self.in_channels * 9) / weight.norm(float('inf'), dim=[1, 2, 3],
+                                                                                   keepdim=True))
+                styles = styles / styles.norm(float('inf'), dim=1, keepdim=True)
+            if noise is not None and noise.ndim == 2:
+                noise = noise.reshape(1, 1, *noise.shape).expand(x.shape[0], 1, -1, -1)
+            clamp = self.conv_clamp * gain if self.conv_clamp is not None else None
+            return modconv.modconv_layer(x, styles, weight, _demod(weight, styles), noise, self.bias,
+                                         alpha=bias_act.activation_funcs[self.activation].def_alpha,
+                                         gain=self.act_gain * gain, clamp=clamp)
         x = modulated_conv2d(x=x, weight=self.weight, styles=styles, noise=noise, up=self.up, padding=self.padding,
                              resample_filter=self.resample_filter, flip_weight=(self.up == 1),
                              fused_modconv=fused_modconv)

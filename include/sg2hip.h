@@ -82,6 +82,17 @@ int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int N, int Cin,
                int OH, int OW, int KH, int KW, int stride, int pad_y, int pad_x, int transpose,
                float* workspace, int64_t workspace_elems, void* stream);
 
+/* 3x3 / stride 1 / pad 1 convolution of 16-bit NHWC activations with an LDS halo tile, optional
+ * modulation of the input and the fused StyleGAN2 layer epilogue (networks_stylegan2.py:309-328):
+ *   c      = conv(x[n,:,:,ci] * in_scale[n,ci], w)          w packed [Cout][3][3][Cin], Cin % 8 == 0
+ *   y_raw  = c                                              (optional second output, may be NULL)
+ *   y      = clamp(act(c * out_scale[n,o] + noise[n,y,x] * noise_gain + bias[o]) * gain, +-clamp)
+ * in_scale / out_scale / bias are float32 (NULL = off); noise has the activation dtype, [N,H,W]
+ * (NULL = off); act 0 = linear, 1 = lrelu(alpha); clamp < 0 = off.  dtype: SG2_F16 or SG2_BF16. */
+int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
+                int Cout, const float* in_scale, const float* out_scale, const void* noise, float noise_gain,
+                const float* bias, int act, float alpha, float gain, float clamp, void* stream);
+
 /* Weight gradient of sg2_conv2d (transpose = 0 form):
  *   dw[a][ky][kx][b] = sum_{n,oy,ox} g[n,oy,ox,a] * x[n, oy*stride+ky-pad_y, ox*stride+kx-pad_x, b]
  *   g [N, OH, OW, A] NHWC, x [N, H, W, B] NHWC; dw is float32 [A][KH][KW][B], overwritten.

@@ -294,3 +294,78 @@ def test_augment_golden(name):
     assert rel_err(y, z[f'{name}_y']) < 2e-5
     dx, = torch.autograd.grad((y * T(z[f'{name}_dy'])).sum(), [x])
     assert rel_err(dx, z[f'{name}_dx']) < 2e-5
+
+
+# ------------------------------------------------------------------ LDS-halo 3x3 conv with fused epilogue
+@pytest.mark.parametrize('shape', [(2, 64, 32, 32, 64), (2, 64, 20, 37, 96), (1, 512, 32, 32, 512), (2, 128, 16, 16, 128),
+                                   (2, 40, 16, 24, 8)])
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_conv3x3_fused(shape, dtype):
+    from torch_utils.ops import conv2d_gradfix as cg
+    N, Cin, H, W, Cout = shape
+    torch.manual_seed(5)
+    x = torch.randn(N, Cin, H, W)
+    w = torch.randn(Cout, Cin, 3, 3) / np.sqrt(Cin * 9)
+    s = torch.rand(N, Cin) + 0.5
+    d = torch.rand(N, Cout) + 0.5
+    noise = torch.randn(N, 1, H, W)
+    b = torch.randn(Cout) * 0.1
+    xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    wp = cg._pack_conv(w.to(DEV, dtype))
+    y, raw = cg.conv3x3_fused(xd, wp, Cout, in_scale=s.to(DEV), out_scale=d.to(DEV),
+                              noise=noise.to(DEV, dtype).reshape(N, H, W).contiguous(), noise_gain=0.3,
+                              bias=b.to(DEV), act=1, alpha=0.2, gain=np.sqrt(2), clamp=1.5, want_raw=True)
+    xs = (x.to(dtype).float() * s[:, :, None, None]).to(dtype).double()
+    c = F.conv2d(xs, w.to(dtype).double(), padding=1)
+    z = c * d[:, :, None, None] + noise.to(dtype).double() * 0.3 + b[None, :, None, None]
+    yr = (F.leaky_relu(z, 0.2) * np.sqrt(2)).clamp(-1.5, 1.5)
+    tol = 5e-3 if dtype == torch.float16 else 2e-2
+    assert rel_err(raw.float(), c) < tol
+    assert rel_err(y.float(), yr) < tol
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_fused_synthesis_layer_matches_composed(dtype):
+    """SynthesisLayer through the one-kernel path (sg2_conv3x3 + ModConvLayer backward) vs the composed
+    path (x*s, conv, fma, bias_act kernels): outputs, first-order grads and the PL-style second-order
+    grads w.r.t. the parameters."""
+    from training import networks_stylegan2 as net
+    from torch_utils.ops import modconv
+    torch.manual_seed(9)
+    layer = net.SynthesisLayer(32, 48, w_dim=16, resolution=16, conv_clamp=256).to(DEV)
+    with torch.no_grad():
+        layer.noise_strength.fill_(0.3)
+        layer.bias.copy_(torch.randn(48) * 0.2)
+    x0 = torch.randn(4, 32, 16, 16, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    w0 = torch.randn(4, 16, device=DEV)
+    noise = torch.randn(4, 1, 16, 16, device=DEV)
+    pl = torch.randn(4, 48, 16, 16, device=DEV)
+    res = []
+    for fused in [True, False]:
+        modconv.enabled = fused
+        x = x0.clone().requires_grad_(True)
+        wv = w0.clone().requires_grad_(True)
+        orig = torch.randn
+        torch.randn = lambda *a, **k: noise.clone()
+        try:
+            y = layer(x, wv)
+        finally:
+            torch.randn = orig
+        params = [layer.weight, layer.bias, layer.noise_strength, layer.affine.weight, layer.affine.bias]
+        for p_ in params:
+            p_.requires_grad_(True)
+        g_w, = torch.autograd.grad((y.float() * pl).sum(), [wv], create_graph=True)
+        gx, = torch.autograd.grad((y.float() * pl).sum(), [x], retain_graph=True)
+        g2 = torch.autograd.grad(g_w.square().sum(), params, allow_unused=True)
+        res.append((y.float(), gx.float(), g_w.float(), [g if g is None else g.float() for g in g2]))
+    modconv.enabled = True
+    tol = 2e-2 if dtype == torch.float16 else 5e-2
+    (y1, gx1, gw1, g21), (y2, gx2, gw2, g22) = res
+    assert rel_err(y1, y2) < tol
+    assert rel_err(gx1, gx2) < tol
+    assert rel_err(gw1, gw2) < tol
+    for a_, b_ in zip(g21, g22):
+        if b_ is None:
+            continue
+        assert a_ is not None
+        assert rel_err(a_, b_) < 4 * tol
