@@ -277,6 +277,7 @@ struct WgradArgs {
     const void* g;   // [N, OH, OW, A]
     const void* x;   // [N, H, W, B]
     float* dw;       // [A][KK][B]
+    const float* b_scale;   // optional [N, B]: x operand multiplied by b_scale[n, b]
     int N, A, OH, OW, B, H, W, KH, KW, stride, pady, padx;
     int M;           // N*OH*OW
     int kper;        // pixels per split (multiple of BK)
@@ -322,6 +323,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 
     vecT ra[PA], rb[PB];
     bool ra_ok[PA], rb_ok[PB];
+    float rsc[PB][V];
     auto gload = [&](int p0) {
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
@@ -350,6 +352,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
             rb_ok[i] = ok;
             const T* row = x + (((int64_t)n * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.B;
             rb[i] = Loader<T, VEC>::load(row, b0 + xb_col, a.B);
+            if (a.b_scale) {
+                const float* sp = a.b_scale + (int64_t)n * a.B;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const int b = b0 + xb_col + j;
+                    rsc[i][j] = sp[b < a.B ? b : 0];
+                }
+            }
         }
     };
     auto sstore = [&](int buf) {
@@ -363,7 +373,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
             const int r = xb_row + i * RPB;
-            if (r < BK) *(vecT*)(Bs + r * LDB + xb_col) = Loader<T, VEC>::mask(rb[i], b0 + xb_col, a.B, rb_ok[i]);
+            vecT v = Loader<T, VEC>::mask(rb[i], b0 + xb_col, a.B, rb_ok[i]);
+            if (a.b_scale) {
+#pragma unroll
+                for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * rsc[i][j]);
+            }
+            if (r < BK) *(vecT*)(Bs + r * LDB + xb_col) = v;
         }
     };
 
@@ -558,7 +573,8 @@ extern "C" int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int 
 }
 
 extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
-                                int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, void* stream) {
+                                int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* x_scale,
+                                void* stream) {
     using namespace sg2;
     SG2_CHECK(dw && g && x, "sg2_conv2d_wgrad: null pointer");
     SG2_CHECK(N > 0 && A > 0 && B > 0 && OH > 0 && OW > 0 && H > 0 && W > 0, "sg2_conv2d_wgrad: empty shape");
@@ -567,7 +583,7 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     hipError_t e = hipMemsetAsync(dw, 0, (int64_t)A * KH * KW * B * sizeof(float), s);
     if (e != hipSuccess) { set_error("sg2_conv2d_wgrad: memset failed"); return (int)e; }
     WgradArgs a{};
-    a.g = g; a.x = x; a.dw = dw;
+    a.g = g; a.x = x; a.dw = dw; a.b_scale = x_scale;
     a.N = N; a.A = A; a.OH = OH; a.OW = OW; a.B = B; a.H = H; a.W = W; a.KH = KH; a.KW = KW;
     a.stride = stride; a.pady = pad_y; a.padx = pad_x;
     a.M = N * OH * OW;

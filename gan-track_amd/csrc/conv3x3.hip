@@ -38,6 +38,8 @@ struct Conv3Args {
     const float* out_scale; // [N, Cout] or null
     const void* noise;      // [N, H, W] (dtype T) or null
     const float* bias;      // [Cout] or null
+    const void* dot_src;    // optional [N,H,W,Cout] (dtype T): dot_out[n,o] += sum_p c * dot_src
+    float* dot_out;         // [N, Cout] float accum
     float noise_gain, alpha, gain, clamp;
     int act;                // 0 linear, 1 lrelu
     int N, H, W, Cin, Cout;
@@ -215,9 +217,13 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
     }
     constexpr int OS = BN + 8;                 // LDS row stride (elements) of the output tile
     T* ot = smem;                              // y tile  [256][OS]
-    T* rt = smem + 256 * OS;                   // raw tile [256][OS] (only if y_raw)
+    T* rt = smem + 256 * OS;                   // raw tile [256][OS] (y_raw and/or dot)
+    float* red = (float*)(smem + 2 * 256 * OS);   // [BN] dot partial sums
     const T* nz = (const T*)a.noise;
     const bool want_raw = a.y_raw != nullptr;
+    const bool want_dot = a.dot_out != nullptr;
+    const bool keep_raw = want_raw || want_dot;
+    if (want_dot && tid < BN) red[tid] = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -232,7 +238,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 float v = acc[i][j][r];
-                if (want_raw) rt[m * OS + j * 16 + (lane & 15)] = (T)v;
+                if (keep_raw) rt[m * OS + j * 16 + (lane & 15)] = (T)v;
                 if (EPI) {
                     v = v * dsc[j] + nv + bsc[j];
                     if (a.act == 1) v = v > 0.f ? v : v * a.alpha;
@@ -247,11 +253,16 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
     typedef T vec8o __attribute__((ext_vector_type(8)));
     T* y = (T*)a.y;
     T* yr = (T*)a.y_raw;
+    const T* dsrc = (const T*)a.dot_src;
     const bool cvec = (a.Cout % 8) == 0;
+    float dacc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dacc[e] = 0.f;
+    const int c8 = (tid & 7) * 8;              // fixed per thread (256 % 8 == 0)
 #pragma unroll
     for (int k = 0; k < 8; ++k) {               // 256 pixels x 8 chunks of 8 channels / 256 threads
         const int idx = tid + k * 256;
-        const int m = idx >> 3, c8 = (idx & 7) * 8;
+        const int m = idx >> 3;
         const int py = m / TW, px = m - py * TW;
         const int oy = ty0 + py, ox = tx0 + px;
         const int o = o0 + c8;
@@ -260,12 +271,25 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
         if (cvec) {
             *(vec8o*)(y + dst) = *(const vec8o*)(ot + m * OS + c8);
             if (want_raw) *(vec8o*)(yr + dst) = *(const vec8o*)(rt + m * OS + c8);
+            if (want_dot) {
+                const vec8o sv = *(const vec8o*)(dsrc + dst);
+                const vec8o rv = *(const vec8o*)(rt + m * OS + c8);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) dacc[e] += (float)rv[e] * (float)sv[e];
+            }
         } else {
             for (int e = 0; e < 8 && o + e < a.Cout; ++e) {
                 y[dst + e] = ot[m * OS + c8 + e];
                 if (want_raw) yr[dst + e] = rt[m * OS + c8 + e];
+                if (want_dot) dacc[e] += (float)rt[m * OS + c8 + e] * (float)dsrc[dst + e];
             }
         }
+    }
+    if (want_dot) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) atomicAdd(&red[c8 + e], dacc[e]);
+        __syncthreads();
+        if (tid < BN && o0 + tid < a.Cout) atomicAdd(&a.dot_out[(int64_t)n * a.Cout + o0 + tid], red[tid]);
     }
 }
 
@@ -273,7 +297,7 @@ template <typename T, int TW, bool SI, bool EPI, int NBUF>
 int launch3(const Conv3Args& a, hipStream_t s) {
     constexpr int TH = 256 / TW;
     size_t lds = NBUF * (size_t)((TW + 2) * (TH + 2) * PX + 9 * BN * PX) * sizeof(T);
-    lds = std::max(lds, (size_t)2 * 256 * (BN + 8) * sizeof(T));   // epilogue tiles
+    lds = std::max(lds, (size_t)2 * 256 * (BN + 8) * sizeof(T) + BN * sizeof(float));   // epilogue tiles
     auto kern = conv3x3_halo_kernel<T, TW, SI, EPI, NBUF>;
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
@@ -289,6 +313,10 @@ template <typename T>
 int dispatch(Conv3Args& a, hipStream_t s) {
     const bool si = a.in_scale != nullptr;
     const bool epi = a.out_scale || a.noise || a.bias || a.act != 0 || a.gain != 1.f || a.clamp >= 0.f;
+    if (a.dot_out) {
+        hipError_t e = hipMemsetAsync(a.dot_out, 0, (size_t)a.N * a.Cout * sizeof(float), s);
+        if (e != hipSuccess) { set_error("sg2_conv3x3: memset failed"); return (int)e; }
+    }
     const int TW = a.W >= 32 ? 32 : 16;
     a.tiles_x = (a.W + TW - 1) / TW;
     a.tiles_y = (a.H + (256 / TW) - 1) / (256 / TW);
@@ -309,7 +337,8 @@ int dispatch(Conv3Args& a, hipStream_t s) {
 
 extern "C" int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
                            int Cout, const float* in_scale, const float* out_scale, const void* noise, float noise_gain,
-                           const float* bias, int act, float alpha, float gain, float clamp, void* stream) {
+                           const float* bias, int act, float alpha, float gain, float clamp, const void* dot_src,
+                           float* dot_out, void* stream) {
     using namespace sg2;
     SG2_CHECK(y && x && w, "sg2_conv3x3: null pointer");
     SG2_CHECK(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "sg2_conv3x3: empty shape");
@@ -317,10 +346,11 @@ extern "C" int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, i
     SG2_CHECK(Cin % 8 == 0, "sg2_conv3x3: Cin must be a multiple of 8");
     SG2_CHECK(((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0, "sg2_conv3x3: 16-byte alignment required");
     SG2_CHECK(act == 0 || act == 1, "sg2_conv3x3: act must be 0 (linear) or 1 (lrelu)");
+    SG2_CHECK((dot_src == nullptr) == (dot_out == nullptr), "sg2_conv3x3: dot_src and dot_out go together");
     SG2_CHECK((int64_t)N * H * W < INT32_MAX / 2, "sg2_conv3x3: tensor too large");
     Conv3Args a{};
     a.x = x; a.w = w; a.y = y; a.y_raw = y_raw; a.in_scale = in_scale; a.out_scale = out_scale; a.noise = noise;
-    a.bias = bias; a.noise_gain = noise_gain; a.alpha = alpha; a.gain = gain; a.clamp = clamp; a.act = act;
+    a.bias = bias; a.dot_src = dot_src; a.dot_out = dot_out; a.noise_gain = noise_gain; a.alpha = alpha; a.gain = gain; a.clamp = clamp; a.act = act;
     a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
     hipStream_t s = as_stream(stream);
     if (dtype == SG2_F16) return dispatch<f16_t>(a, s);

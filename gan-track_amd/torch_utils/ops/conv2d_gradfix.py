@@ -67,14 +67,15 @@ def _conv_raw(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose):
     return y
 
 
-def _wgrad_raw(g, x, kh, kw, stride, pad):
-    """dw[a, b, ky, kx] = sum g[n,a,oy,ox] x[n,b,oy*s+ky-p,ox*s+kx-p]; returns f32 [A,B,kh,kw] (NHWC-packed)."""
+def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None):
+    """dw[a, b, ky, kx] = sum g[n,a,oy,ox] x[n,b,oy*s+ky-p,ox*s+kx-p] (* x_scale[n,b]);
+    returns f32 [A,B,kh,kw] (NHWC-packed)."""
     n, a, oh, ow = g.shape
     _, b, h, w = x.shape
     dw = torch.empty([a, kh, kw, b], dtype=torch.float32, device=g.device)
     _hip.check(_hip.lib().sg2_conv2d_wgrad(
         _hip.ptr(dw), _hip.ptr(g), _hip.ptr(x), _hip.dtype_code(g), n, a, oh, ow, b, h, w, kh, kw, stride,
-        pad[0], pad[1], _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad')
+        pad[0], pad[1], _hip.ptr(x_scale), _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad')
     return dw.permute(0, 3, 1, 2)
 
 
@@ -94,16 +95,41 @@ def _halo_ok(x, kh, kw, stride, pad, out_hw):
 
 
 def conv3x3_fused(x, wp, cout, in_scale=None, out_scale=None, noise=None, noise_gain=0.0, bias=None, act=0,
-                  alpha=0.2, gain=1.0, clamp=-1.0, want_raw=False):
-    """sg2_conv3x3 launch.  x NHWC 16-bit, wp packed [Cout][3][3][Cin]; returns (y, raw or None)."""
+                  alpha=0.2, gain=1.0, clamp=-1.0, want_raw=False, dot_src=None):
+    """sg2_conv3x3 launch.  x NHWC 16-bit, wp packed [Cout][3][3][Cin].
+    Returns (y, raw or None, dot or None) with dot[n,o] = sum_p conv(x)[n,o,p] * dot_src[n,o,p]."""
     n, cin, h, w = x.shape
     y = torch.empty([n, cout, h, w], dtype=x.dtype, device=x.device, memory_format=_CL)
     raw = torch.empty_like(y) if want_raw else None
+    dot = None
+    if dot_src is not None:
+        dot_src = _nhwc(dot_src)
+        dot = torch.empty([n, cout], dtype=torch.float32, device=x.device)
     _hip.check(_hip.lib().sg2_conv3x3(
         _hip.ptr(y), _hip.ptr(raw), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout,
         _hip.ptr(in_scale), _hip.ptr(out_scale), _hip.ptr(noise), float(noise_gain), _hip.ptr(bias), int(act),
-        float(alpha), float(gain), float(clamp), _hip.stream_ptr(x.device)), 'sg2_conv3x3')
-    return y, raw
+        float(alpha), float(gain), float(clamp), _hip.ptr(dot_src), _hip.ptr(dot), _hip.stream_ptr(x.device)),
+        'sg2_conv3x3')
+    return (y, raw, dot) if dot_src is not None else (y, raw)
+
+
+def layer_bwd(dy, y, c=None, d=None, act=1, alpha=0.2, gain=1.0, clamp=-1.0, want_db=True, want_dd=True,
+              want_dnoise=True):
+    """sg2_layer_bwd: returns (dc, db[C] or None, dd[N,C] or None, dnoise[N,1,H,W] or None)."""
+    y = _nhwc(y)
+    dy = _nhwc(dy)
+    n, ch, h, w = y.shape
+    dc = torch.empty_like(y)
+    f32 = dict(dtype=torch.float32, device=y.device)
+    db = torch.empty([ch], **f32) if want_db else None
+    dd = torch.empty([n, ch], **f32) if (want_dd and d is not None) else None
+    dn = torch.empty([n, 1, h, w], **f32) if want_dnoise else None
+    c = _nhwc(c) if c is not None else None
+    _hip.check(_hip.lib().sg2_layer_bwd(
+        _hip.ptr(dc), _hip.ptr(db), _hip.ptr(dd), _hip.ptr(dn), _hip.ptr(dy), _hip.ptr(y), _hip.ptr(c),
+        _hip.ptr(d), _hip.dtype_code(y), n, h * w, ch, int(act), float(alpha), float(gain), float(clamp),
+        _hip.stream_ptr(y.device)), 'sg2_layer_bwd')
+    return dc, db, dd, dn
 
 
 class _Conv2d(torch.autograd.Function):
@@ -114,7 +140,7 @@ class _Conv2d(torch.autograd.Function):
         assert x.shape[1] == i and x.dtype == w.dtype
         oh, ow = out_hw
         if _halo_ok(x, kh, kw, stride, pad, out_hw):
-            y, _ = conv3x3_fused(x, _pack_conv(w), o)
+            y = conv3x3_fused(x, _pack_conv(w), o)[0]
         else:
             y = _conv_raw(x, _pack_conv(w), o, oh, ow, kh, kw, stride, pad, False)
         ctx.save_for_backward(x, w)
@@ -143,7 +169,7 @@ class _ConvT2d(torch.autograd.Function):
         oh, ow = out_hw
         if _halo_ok(x, kh, kw, stride, pad, out_hw):
             # stride-1 transposed conv == correlation with the spatially flipped, transposed kernel
-            y, _ = conv3x3_fused(x, _pack_convT(w.flip([2, 3])), o)
+            y = conv3x3_fused(x, _pack_convT(w.flip([2, 3])), o)[0]
         else:
             y = _conv_raw(x, _pack_convT(w), o, oh, ow, kh, kw, stride, pad, True)
         ctx.save_for_backward(x, w)

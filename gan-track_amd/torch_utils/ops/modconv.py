@@ -53,6 +53,8 @@ class ModConvLayer(torch.autograd.Function):
         n, cin, h, w = x.shape
         dt = x.dtype
         need = ctx.needs_input_grad
+        if not torch.is_grad_enabled() and fast_backward:
+            return _fast_backward(ctx, dy, x, styles, weight, dcoefs, noise, bias, y, c, alpha, gain, clamp)
         dz = _ba.bias_act_grad(dy, y, act='lrelu', alpha=alpha, gain=gain, clamp=clamp)
         dx = ds = dw = dd = dnoise = db = None
         if need[5]:
@@ -76,6 +78,37 @@ class ModConvLayer(torch.autograd.Function):
         if need[2] and not _cg.weight_gradients_disabled:
             dw = _cg._WGrad.apply(dc, x * s_, (3, 3), 1, (1, 1)).to(weight.dtype)
         return dx, ds, dw, dd, dnoise, db, None, None, None
+
+
+def _fast_backward(ctx, dy, x, styles, weight, dcoefs, noise, bias, y, c, alpha, gain, clamp):
+    """First-order backward in three kernels (no create_graph):
+      sg2_layer_bwd  : dz, dc = dz*d, db, dd = sum dz*c, dnoise         (one pass over dy, y, c)
+      sg2_conv3x3    : dx = convT(dc, W) * s, ds = sum convT(dc, W) * x  (dgrad with scale + dot epilogue)
+      sg2_conv2d_wgrad: dw = sum dc (x) (x * s)                          (modulation applied to the B operand)
+    """
+    need = ctx.needs_input_grad
+    n, cin, h, w = x.shape
+    dt = x.dtype
+    d32 = dcoefs.float().contiguous() if dcoefs is not None else None
+    dc, db, dd, dn = _cg.layer_bwd(dy.to(dt), y, c if (need[3] and d32 is not None) else None, d32, act=1,
+                                   alpha=alpha, gain=gain, clamp=clamp, want_db=need[5],
+                                   want_dd=need[3] and d32 is not None, want_dnoise=need[4] and noise is not None)
+    dx = ds = dw = None
+    s32 = styles.float().contiguous()
+    if need[0] or need[1]:
+        wT = _cg._pack_convT(weight.to(dt).flip([2, 3]))
+        dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
+        ds = ds.to(styles.dtype) if need[1] else None
+        dx = dx if need[0] else None
+    if need[2] and not _cg.weight_gradients_disabled:
+        dw = _cg._wgrad_raw(dc, x, 3, 3, 1, (1, 1), x_scale=s32).to(weight.dtype)
+    db = db.to(bias.dtype) if db is not None else None
+    dd = dd.to(dcoefs.dtype) if dd is not None else None
+    dn = dn.to(noise.dtype) if dn is not None else None
+    return dx, ds, dw, dd, dn, db, None, None, None
+
+
+fast_backward = True   # first-order backward through the fused kernels (A/B switch)
 
 
 def modconv_layer(x, styles, weight, dcoefs, noise, bias, alpha, gain, clamp):

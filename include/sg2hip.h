@@ -88,17 +88,30 @@ int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int N, int Cin,
  *   y_raw  = c                                              (optional second output, may be NULL)
  *   y      = clamp(act(c * out_scale[n,o] + noise[n,y,x] * noise_gain + bias[o]) * gain, +-clamp)
  * in_scale / out_scale / bias are float32 (NULL = off); noise has the activation dtype, [N,H,W]
- * (NULL = off); act 0 = linear, 1 = lrelu(alpha); clamp < 0 = off.  dtype: SG2_F16 or SG2_BF16. */
+ * (NULL = off); act 0 = linear, 1 = lrelu(alpha); clamp < 0 = off.  dtype: SG2_F16 or SG2_BF16.
+ * dot_src / dot_out (both or neither): dot_out[n,o] = sum_{y,x} c[n,y,x,o] * dot_src[n,y,x,o] (float,
+ * zeroed by the call) -- the modulation gradient of the layer when this kernel runs its dgrad. */
 int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
                 int Cout, const float* in_scale, const float* out_scale, const void* noise, float noise_gain,
-                const float* bias, int act, float alpha, float gain, float clamp, void* stream);
+                const float* bias, int act, float alpha, float gain, float clamp, const void* dot_src,
+                float* dot_out, void* stream);
 
 /* Weight gradient of sg2_conv2d (transpose = 0 form):
- *   dw[a][ky][kx][b] = sum_{n,oy,ox} g[n,oy,ox,a] * x[n, oy*stride+ky-pad_y, ox*stride+kx-pad_x, b]
+ *   dw[a][ky][kx][b] = sum_{n,oy,ox} g[n,oy,ox,a] * x[n, oy*stride+ky-pad_y, ox*stride+kx-pad_x, b] * s[n,b]
+ *   s = x_scale [N, B] float32 (the layer's modulation), or NULL for 1.
  *   g [N, OH, OW, A] NHWC, x [N, H, W, B] NHWC; dw is float32 [A][KH][KW][B], overwritten.
  *   The conv_transpose2d weight gradient is the same call with (g, x) = (x_of_convT, dy). */
 int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
-                     int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, void* stream);
+                     int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* x_scale,
+                     void* stream);
+
+/* Fused first-order backward of the layer epilogue z = c*d + noise + b, y = clamp(act(z)*gain):
+ *   dc = dz * d;  db[o] = sum dz;  dd[n,o] = sum_p dz*c;  dnoise[n,p] = sum_o dz
+ * where dz = dy * act'(y) * gain masked by |y| < clamp.  dy, y, c, dc: [N, HW, C] 16-bit NHWC,
+ * C % 8 == 0.  c / d / db / dd / dnoise may be NULL; db and dd are zeroed by the call. */
+int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, const void* dy, const void* y, const void* c,
+                  const float* d, int dtype, int N, int HW, int C, int act, float alpha, float gain, float clamp,
+                  void* stream);
 
 /* Bilinear grid sample, zeros padding, align_corners = False (the only mode the reference uses,
  * grid_sample_gradfix.py:9-12).  in [N,C,Hi,Wi] any strides; grid float32 [N,Ho,Wo,2] contiguous;

@@ -24,5 +24,22 @@ try:
     busy += cur_e - cur_s
     span = ts[-1][1] - ts[0][0]
     print(f'trace span {span/1e6:.1f} ms, GPU busy {busy/1e6:.1f} ms ({100*busy/span:.1f}%)')
+    if len(sys.argv) > 3:   # busy fraction inside the last <tail_ms> of the trace (the timed steps)
+        tail = float(sys.argv[3]) * 1e6
+        t0 = ts[-1][1] - tail
+        busy2, ce = 0, None
+        cs = None
+        for s_, e_ in ts:
+            s_, e_ = max(s_, t0), e_
+            if e_ <= t0:
+                continue
+            if ce is None or s_ > ce:
+                if ce is not None:
+                    busy2 += ce - cs
+                cs, ce = s_, e_
+            else:
+                ce = max(ce, e_)
+        busy2 += ce - cs
+        print(f'last {tail/1e6:.0f} ms: GPU busy {busy2/1e6:.1f} ms ({100*busy2/tail:.1f}%)')
 except Exception as e:  # noqa: BLE001
     print('no trace:', e)

@@ -369,3 +369,84 @@ def test_fused_synthesis_layer_matches_composed(dtype):
             continue
         assert a_ is not None
         assert rel_err(a_, b_) < 4 * tol
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(4, 32, 16, 16, 48), (2, 64, 32, 32, 64), (2, 512, 16, 16, 256)])
+def test_fused_synthesis_layer_fast_backward(dtype, shape):
+    """First-order backward through sg2_layer_bwd + dgrad(dot epilogue) + scaled wgrad vs the composed
+    differentiable backward of the same fused forward: every parameter and input gradient."""
+    from training import networks_stylegan2 as net
+    from torch_utils.ops import modconv
+    N, Cin, H, W, Cout = shape
+    torch.manual_seed(11)
+    layer = net.SynthesisLayer(Cin, Cout, w_dim=16, resolution=H, conv_clamp=256).to(DEV)
+    with torch.no_grad():
+        layer.noise_strength.fill_(0.3)
+        layer.bias.copy_(torch.randn(Cout) * 0.2)
+    x0 = torch.randn(N, Cin, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    w0 = torch.randn(N, 16, device=DEV)
+    noise = torch.randn(N, 1, H, W, device=DEV)
+    dy = torch.randn(N, Cout, H, W, device=DEV)
+    params = [layer.weight, layer.bias, layer.noise_strength, layer.affine.weight, layer.affine.bias]
+    res = []
+    # fast (fused kernels), composed (differentiable primitives), f32 reference (composed, fp32 activations)
+    for fast, dt in [(True, dtype), (False, dtype), (False, torch.float32)]:
+        modconv.fast_backward = fast
+        x = x0.clone().to(dt).requires_grad_(True)
+        wv = w0.clone().requires_grad_(True)
+        orig = torch.randn
+        torch.randn = lambda *a, **k: noise.clone()
+        try:
+            y = layer(x, wv)
+        finally:
+            torch.randn = orig
+        grads = torch.autograd.grad((y.float() * dy).sum(), [x, wv] + params)
+        res.append([g.float() for g in grads])
+    modconv.fast_backward = True
+    tol = 1e-2 if dtype == torch.float16 else 4e-2
+    for a_, b_, r_ in zip(*res):
+        # the fused path keeps dz in f32 where the composed one rounds it to 16 bits: it may only be closer
+        assert rel_err(a_, r_) < max(tol, 1.25 * rel_err(b_, r_))
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(2, 16, 24, 8), (3, 64, 7, 512), (1, 1024, 2, 64)])
+def test_layer_bwd(dtype, shape):
+    from torch_utils.ops import conv2d_gradfix as cg
+    N, H, W, C = shape
+    torch.manual_seed(3)
+    y = (torch.randn(N, C, H, W, device=DEV) * 2).to(dtype).contiguous(memory_format=torch.channels_last)
+    c = torch.randn(N, C, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, C, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    d = torch.rand(N, C, device=DEV) + 0.5
+    dc, db, dd, dn = cg.layer_bwd(dy, y, c, d, act=1, alpha=0.2, gain=1.5, clamp=2.5)
+    yf = y.float()
+    dz = dy.float() * 1.5 * torch.where(yf > 0, 1.0, 0.2) * ((yf > -2.5) & (yf < 2.5)).float()
+    tol = 5e-3 if dtype == torch.float16 else 2e-2
+    assert rel_err(dc.float(), dz * d[:, :, None, None]) < tol
+    assert rel_err(db, dz.sum([0, 2, 3])) < 1e-4
+    assert rel_err(dd, (dz * c.float()).sum([2, 3])) < 1e-4
+    assert rel_err(dn, dz.sum(1, keepdim=True)) < 1e-4
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_conv3x3_dot_and_scaled_wgrad(dtype):
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(4)
+    N, Cin, H, W, Cout = 2, 64, 20, 33, 96
+    x = torch.randn(N, Cin, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, 3, 3, device=DEV) / np.sqrt(Cin * 9)).to(dtype)
+    src = torch.randn(N, Cout, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    s = torch.rand(N, Cout, device=DEV) + 0.5
+    y, raw, dot = cg.conv3x3_fused(x, cg._pack_conv(w), Cout, out_scale=s, dot_src=src)
+    c = F.conv2d(x.double(), w.double(), padding=1)
+    tol = 5e-3 if dtype == torch.float16 else 2e-2
+    assert rel_err(y.float(), c * s[:, :, None, None].double()) < tol
+    assert rel_err(dot, (c.to(dtype).double() * src.double()).sum([2, 3])) < tol
+    g = torch.randn(N, Cout, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    xs = torch.rand(N, Cin, device=DEV) + 0.5
+    dw = cg._wgrad_raw(g, x, 3, 3, 1, (1, 1), x_scale=xs)
+    xsc = (x.float() * xs[:, :, None, None]).to(dtype)
+    ref = torch.nn.grad.conv2d_weight(xsc.double(), w.shape, g.double(), padding=1)
+    assert rel_err(dw, ref) < tol
