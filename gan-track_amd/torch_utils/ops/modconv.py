@@ -38,10 +38,10 @@ class ModConvLayer(torch.autograd.Function):
         if noise is not None:
             nz = noise.to(x.dtype).reshape(n, h, w).contiguous()
         want_raw = any(ctx.needs_input_grad[:6])
-        y, c = _cg.conv3x3_fused(x, _cg._pack_conv(wT), cout, in_scale=styles.float().contiguous(),
-                                 out_scale=dcoefs.float().contiguous() if dcoefs is not None else None,
-                                 noise=nz, noise_gain=1.0, bias=bias.float().contiguous(), act=1, alpha=alpha,
-                                 gain=gain, clamp=clamp, want_raw=want_raw)
+        want_raw = want_raw and dcoefs is not None     # c only feeds dL/dd
+        y, c = _cg.conv3x3_fused(x, _cg._pack_conv(wT), cout, in_scale=_f32(styles), out_scale=_f32(dcoefs),
+                                 noise=nz, noise_gain=1.0, bias=_f32(bias), act=1, alpha=alpha, gain=gain,
+                                 clamp=clamp, want_raw=want_raw)
         ctx.save_for_backward(x, styles, weight, dcoefs, noise, bias, y, c)
         ctx.cfg = (alpha, gain, clamp)
         return y
@@ -57,14 +57,14 @@ class ModConvLayer(torch.autograd.Function):
             return _fast_backward(ctx, dy, x, styles, weight, dcoefs, noise, bias, y, c, alpha, gain, clamp)
         dz = _ba.bias_act_grad(dy, y, act='lrelu', alpha=alpha, gain=gain, clamp=clamp)
         dx = ds = dw = dd = dnoise = db = None
-        if need[5]:
+        if need[5] and bias is not None:
             db = dz.sum([0, 2, 3], dtype=torch.float32).to(bias.dtype)
         if need[4] and noise is not None:
             dnoise = dz.sum(1, keepdim=True, dtype=torch.float32).to(noise.dtype)
-        s_ = styles.to(dt).reshape(n, -1, 1, 1)
+        s_ = styles.to(dt).reshape(n, -1, 1, 1) if styles is not None else None
         if need[3] and dcoefs is not None:
             if torch.is_grad_enabled():
-                c_ = _cg._Conv2d.apply(x * s_, weight.to(dt), 1, (1, 1), (h, w))
+                c_ = _cg._Conv2d.apply(_mul(x, s_), weight.to(dt), 1, (1, 1), (h, w))
             else:
                 c_ = c
             dd = (dz * c_).sum([2, 3], dtype=torch.float32).to(dcoefs.dtype)
@@ -72,11 +72,11 @@ class ModConvLayer(torch.autograd.Function):
         if need[0] or need[1]:
             dxs = _cg._ConvT2d.apply(dc, weight.to(dt), 1, (1, 1), (h, w))
             if need[0]:
-                dx = dxs * s_
-            if need[1]:
+                dx = _mul(dxs, s_)
+            if need[1] and styles is not None:
                 ds = (dxs * x).sum([2, 3], dtype=torch.float32).to(styles.dtype)
         if need[2] and not _cg.weight_gradients_disabled:
-            dw = _cg._WGrad.apply(dc, x * s_, (3, 3), 1, (1, 1)).to(weight.dtype)
+            dw = _cg._WGrad.apply(dc, _mul(x, s_), (3, 3), 1, (1, 1)).to(weight.dtype)
         return dx, ds, dw, dd, dnoise, db, None, None, None
 
 
@@ -91,14 +91,18 @@ def _fast_backward(ctx, dy, x, styles, weight, dcoefs, noise, bias, y, c, alpha,
     dt = x.dtype
     d32 = dcoefs.float().contiguous() if dcoefs is not None else None
     dc, db, dd, dn = _cg.layer_bwd(dy.to(dt), y, c if (need[3] and d32 is not None) else None, d32, act=1,
-                                   alpha=alpha, gain=gain, clamp=clamp, want_db=need[5],
+                                   alpha=alpha, gain=gain, clamp=clamp, want_db=need[5] and bias is not None,
                                    want_dd=need[3] and d32 is not None, want_dnoise=need[4] and noise is not None)
     dx = ds = dw = None
-    s32 = styles.float().contiguous()
-    if need[0] or need[1]:
+    s32 = _f32(styles)
+    want_ds = need[1] and styles is not None
+    if need[0] or want_ds:
         wT = _cg._pack_convT(weight.to(dt).flip([2, 3]))
-        dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
-        ds = ds.to(styles.dtype) if need[1] else None
+        if want_ds:
+            dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
+            ds = ds.to(styles.dtype)
+        else:
+            dx, _ = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32)
         dx = dx if need[0] else None
     if need[2] and not _cg.weight_gradients_disabled:
         dw = _cg._wgrad_raw(dc, x, 3, 3, 1, (1, 1), x_scale=s32).to(weight.dtype)
@@ -111,6 +115,16 @@ def _fast_backward(ctx, dy, x, styles, weight, dcoefs, noise, bias, y, c, alpha,
 fast_backward = True   # first-order backward through the fused kernels (A/B switch)
 
 
+def _f32(t):
+    return t.float().contiguous() if t is not None else None
+
+
+def _mul(a, s):
+    return a * s if s is not None else a
+
+
 def modconv_layer(x, styles, weight, dcoefs, noise, bias, alpha, gain, clamp):
+    """styles / dcoefs / noise / bias may be None: with styles = dcoefs = noise = None this is the
+    discriminator's plain 3x3 Conv2dLayer + bias + lrelu (networks_stylegan2.py:172-181) in one kernel."""
     return ModConvLayer.apply(x, styles, weight, dcoefs, noise, bias, float(alpha), float(gain),
                               float(clamp if clamp is not None else -1.0))

@@ -117,6 +117,11 @@ class Conv2dLayer(torch.nn.Module):
 
     def forward(self, x, gain=1):
         w = self.weight * self.weight_gain
+        if (self.up == 1 and self.down == 1 and self.activation == 'lrelu' and w.shape[2] == 3 and
+                modconv.supported(x, w, 1)):
+            # conv + bias + lrelu + gain + clamp in one LDS-halo kernel launch
+            clamp = self.conv_clamp * gain if self.conv_clamp is not None else -1.0
+            return modconv.modconv_layer(x, None, w, None, None, self.bias, 0.2, self.act_gain * gain, clamp)
         b = self.bias.to(x.dtype) if self.bias is not None else None
         x = conv2d_resample.conv2d_resample(x=x, w=w.to(x.dtype), f=self.resample_filter, up=self.up, down=self.down,
                                             padding=self.padding, flip_weight=(self.up == 1))

@@ -450,3 +450,33 @@ def test_conv3x3_dot_and_scaled_wgrad(dtype):
     xsc = (x.float() * xs[:, :, None, None]).to(dtype)
     ref = torch.nn.grad.conv2d_weight(xsc.double(), w.shape, g.double(), padding=1)
     assert rel_err(dw, ref) < tol
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_fused_d_conv_layer_matches_composed(dtype):
+    """Discriminator 3x3 Conv2dLayer (bias + lrelu + clamp) through one sg2_conv3x3 launch and the fused
+    backward vs the composed path (conv kernel + bias_act kernel): output, input/param grads and the
+    R1-style second-order grads."""
+    from training import networks_stylegan2 as net
+    from torch_utils.ops import modconv
+    torch.manual_seed(13)
+    layer = net.Conv2dLayer(32, 48, kernel_size=3, activation='lrelu', conv_clamp=256).to(DEV)
+    with torch.no_grad():
+        layer.bias.copy_(torch.randn(48) * 0.2)
+    x0 = torch.randn(4, 32, 24, 16, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(4, 48, 24, 16, device=DEV)
+    params = [layer.weight, layer.bias]
+    res = []
+    for fused in [True, False]:
+        modconv.enabled = fused
+        x = x0.clone().requires_grad_(True)
+        y = layer(x, gain=np.sqrt(0.5))
+        gx, = torch.autograd.grad((y.float() * dy).sum(), [x], create_graph=True)
+        g2 = torch.autograd.grad(gx.float().square().sum(), params)
+        y = layer(x)
+        g1 = torch.autograd.grad((y.float() * dy).sum(), [x] + params)
+        res.append([y.float(), gx.float()] + [g.float() for g in g1] + [g.float() for g in g2])
+    modconv.enabled = True
+    tol = 1e-2 if dtype == torch.float16 else 4e-2
+    for a_, b_ in zip(*res):
+        assert rel_err(a_, b_) < tol
