@@ -480,3 +480,21 @@ def test_fused_d_conv_layer_matches_composed(dtype):
     tol = 1e-2 if dtype == torch.float16 else 4e-2
     for a_, b_ in zip(*res):
         assert rel_err(a_, b_) < tol
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(2, 64, 64, 32, 32), (3, 128, 96, 20, 37), (1, 512, 512, 32, 32), (2, 8, 40, 16, 16),
+                                   (2, 72, 64, 17, 48)])
+@pytest.mark.parametrize('scaled', [False, True])
+def test_wgrad3x3_halo(dtype, shape, scaled):
+    """sg2_conv2d_wgrad on the 3x3/s1/p1 halo path (all nine taps per tile) vs an f64 reference."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    N, A, B, H, W = shape
+    torch.manual_seed(21)
+    g = torch.randn(N, A, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    x = torch.randn(N, B, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    s = (torch.rand(N, B, device=DEV) + 0.5) if scaled else None
+    dw = cg._wgrad_raw(g, x, 3, 3, 1, (1, 1), x_scale=s)
+    xs = (x.float() * s[:, :, None, None]).to(dtype) if scaled else x
+    ref = torch.nn.grad.conv2d_weight(xs.double(), [A, B, 3, 3], g.double(), padding=1)
+    assert rel_err(dw, ref) < (2e-3 if dtype == torch.float16 else 1e-2)

@@ -40,8 +40,8 @@ for sh in args.shapes.split(','):
     wp = cg._pack_conv(w)
     flops = 2.0 * N * C * C * 9 * res * res
     out = []
+    s_ = torch.rand([N, C], device=dev) + 0.5
     if 'halo' in args.which:
-        s_ = torch.rand([N, C], device=dev) + 0.5
         d_ = torch.rand([N, C], device=dev) + 0.5
         nz_ = torch.randn([N, res, res], device=dev, dtype=dt)
         b_ = torch.zeros([C], device=dev)
@@ -57,6 +57,8 @@ for sh in args.shapes.split(','):
     if 'wgrad' in args.which:
         ms = timeit(lambda: cg._wgrad_raw(x, x, 3, 3, 1, (1, 1)), args.reps)
         out.append(f'wgrad {ms:.3f}ms {flops / ms / 1e9:.0f}TF')
+        ms = timeit(lambda: cg._wgrad_raw(x, x, 3, 3, 1, (1, 1), x_scale=s_), args.reps)
+        out.append(f'wgrad-scaled {ms:.3f}ms {flops / ms / 1e9:.0f}TF')
     if 'convT' in args.which and res >= 64:
         xh = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
         wt = w.transpose(0, 1).contiguous()
