@@ -29,10 +29,25 @@ namespace sg2 {
 namespace {
 
 constexpr int kMaxTaps = 64;
+constexpr int kMaxPhases = 4;
 
-struct TapTable {
-    int n;
-    int dy[kMaxTaps], dx[kMaxTaps], w[kMaxTaps];
+struct Tap { int8_t dy, dx, w, pad_; };
+
+struct Phase {
+    int QH, QW, M;           // phase grid, M = N*QH*QW
+    int osy, osx, oy0, ox0;  // output coordinate = q*os + o0
+    int tap0, ntaps, nk;     // taps [tap0, tap0 + ntaps) of the shared table; nk = ntaps * nck
+};
+
+// Fused epilogue (mirror of sg2_epilogue in include/sg2hip.h).
+struct Epi {
+    const float* out_scale;  // [N, Cout]
+    const void* noise;       // [N, OH, OW] (T)
+    const float* bias;       // [Cout]
+    const void* residual;    // [N, OH, OW, Cout] (T), added after rounding the activation
+    void* aux;               // [N, OH, OW, Cout] (T): aux_mode 1 = conv result, 2 = activation before residual
+    float noise_gain, alpha, gain, clamp;
+    int act, aux_mode, on;
 };
 
 struct ConvArgs {
@@ -40,15 +55,15 @@ struct ConvArgs {
     const void* w;
     void* y;       // T output (non-split)
     float* acc;    // f32 output for split-K (zeroed)
+    const float* in_scale;   // [N, Cin] modulation of the A operand, or null
+    Epi e;
     int N, H, W, Cin, Cout, OH, OW;
-    int QH, QW, M;           // phase grid, M = N*QH*QW
-    int osy, osx, oy0, ox0;  // output coordinate = q*os + o0
     int isy, isx;            // input coordinate  = q*is + tap.d
     int wtaps;               // taps per output channel in the packed weight (KH*KW)
     int nck;                 // ceil(Cin / BK)
-    int nk;                  // taps.n * nck
-    int kper;                // K-chunks per split
-    TapTable taps;
+    int splits, kper;        // K split: kper chunks per split
+    Phase ph[kMaxPhases];
+    Tap taps[kMaxTaps];
 };
 
 template <typename T> struct Traits;
@@ -108,6 +123,20 @@ struct Loader {
     }
 };
 
+// The fused epilogue of one output element: z = clamp(act(c * out_scale + noise * g + bias) * gain).
+template <typename T>
+__device__ __forceinline__ float epi_full(const Epi& e, float c, int n, int o, int64_t pix, int Cout) {
+    float v = c;
+    if (e.out_scale) v *= e.out_scale[(int64_t)n * Cout + o];
+    if (e.noise) v += (float)((const T*)e.noise)[pix] * e.noise_gain;
+    if (e.bias) v += e.bias[o];
+    if (e.act == 1) v = v > 0.f ? v : v * e.alpha;
+    v *= e.gain;
+    if (e.clamp >= 0.f) v = fminf(fmaxf(v, -e.clamp), e.clamp);
+    return v;
+}
+
+// Implicit-GEMM convolution.  grid = (M tiles, Cout tiles, phases * splits).
 template <typename T, int BM, int BN, bool VEC, bool SPLIT>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
@@ -118,11 +147,18 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
     typedef typename Loader<T, VEC>::vecT vecT;
 
-    __shared__ __attribute__((aligned(16))) T lds[2][(BM + BN) * LDK];
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    T* lds = (T*)smem_raw;               // [2][(BM + BN) * LDK], reused by the epilogue
+    constexpr int BUF = (BM + BN) * LDK;
+
+    const int phase = blockIdx.z / a.splits, split = blockIdx.z - phase * a.splits;
+    const int QH = a.ph[phase].QH, QW = a.ph[phase].QW, M = a.ph[phase].M;
+    const int tap0 = a.ph[phase].tap0, nk = a.ph[phase].nk;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    if (m0 >= M) return;                 // phases have slightly different M; the whole block leaves
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     const T* __restrict__ x = (const T*)a.x;
     const T* __restrict__ w = (const T*)a.w;
 
@@ -133,27 +169,29 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
         const int m = m0 + lrow + i * RPP;
-        a_ok[i] = m < a.M;
+        a_ok[i] = m < M;
         const int mm = a_ok[i] ? m : 0;
-        const int per = a.QH * a.QW;
+        const int per = QH * QW;
         a_n[i] = mm / per;
         const int r = mm - a_n[i] * per;
-        a_qy[i] = (r / a.QW) * a.isy;
-        a_qx[i] = (r % a.QW) * a.isx;
+        a_qy[i] = (r / QW) * a.isy;
+        a_qx[i] = (r % QW) * a.isx;
     }
     const int64_t wrow = (int64_t)a.wtaps * a.Cin;
 
-    const int k_begin = blockIdx.z * a.kper;
-    const int k_end = min(a.nk, k_begin + a.kper);
+    const int k_begin = split * a.kper;
+    const int k_end = min(nk, k_begin + a.kper);
 
     vecT ra[PA], rb[PB];
     bool ra_ok[PA], rb_ok[PB];
+    float rsc[PA][V];
     int cur_c = 0;
     auto gload = [&](int kc) {
         const int t = kc / a.nck;
         const int c = (kc - t * a.nck) * BK + lcol;
         cur_c = c;
-        const int dy = a.taps.dy[t], dx = a.taps.dx[t], wt = a.taps.w[t];
+        const Tap tp = a.taps[tap0 + t];
+        const int dy = tp.dy, dx = tp.dx, wt = tp.w;
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             const int iy = a_qy[i] + dy, ix = a_qx[i] + dx;
@@ -161,6 +199,11 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
             ra_ok[i] = ok;
             const T* row = x + (((int64_t)a_n[i] * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.Cin;
             ra[i] = Loader<T, VEC>::load(row, c, a.Cin);
+            if (a.in_scale) {
+                const float* sp = a.in_scale + (int64_t)a_n[i] * a.Cin;
+#pragma unroll
+                for (int j = 0; j < V; ++j) rsc[i][j] = sp[c + j < a.Cin ? c + j : 0];
+            }
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
@@ -172,11 +215,17 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
         }
     };
     auto sstore = [&](int buf) {
-        T* As = lds[buf];
-        T* Bs = lds[buf] + BM * LDK;
+        T* As = lds + buf * BUF;
+        T* Bs = As + BM * LDK;
 #pragma unroll
-        for (int i = 0; i < PA; ++i)
-            *(vecT*)(As + (lrow + i * RPP) * LDK + lcol) = Loader<T, VEC>::mask(ra[i], cur_c, a.Cin, ra_ok[i]);
+        for (int i = 0; i < PA; ++i) {
+            vecT v = Loader<T, VEC>::mask(ra[i], cur_c, a.Cin, ra_ok[i]);
+            if (a.in_scale) {
+#pragma unroll
+                for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * rsc[i][j]);
+            }
+            *(vecT*)(As + (lrow + i * RPP) * LDK + lcol) = v;
+        }
 #pragma unroll
         for (int i = 0; i < PB; ++i)
             *(vecT*)(Bs + (lrow + i * RPP) * LDK + lcol) = Loader<T, VEC>::mask(rb[i], cur_c, a.Cin, rb_ok[i]);
@@ -196,8 +245,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
             const int cur = (kc - k_begin) & 1;
             const bool more = kc + 1 < k_end;
             if (more) gload(kc + 1);
-            const T* As = lds[cur] + (wm * WM) * LDK;
-            const T* Bs = lds[cur] + BM * LDK + (wn * WN) * LDK;
+            const T* As = lds + cur * BUF + (wm * WM) * LDK;
+            const T* Bs = lds + cur * BUF + BM * LDK + (wn * WN) * LDK;
             if constexpr (std::is_same<T, float>::value) {
 #pragma unroll
                 for (int kk = 0; kk < BK; kk += 4) {
@@ -227,48 +276,152 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     }
 
     // --- epilogue ---
-    const int per = a.QH * a.QW;
+    const int per = QH * QW;
+    const int osy = a.ph[phase].osy, osx = a.ph[phase].osx, oy0 = a.ph[phase].oy0, ox0 = a.ph[phase].ox0;
+    if (SPLIT || std::is_same<T, float>::value) {
+        // f32 tiles / split-K partial sums: direct stores (the split-K epilogue runs in the finalize kernel)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + r;
+                if (m >= M) continue;
+                const int n = m / per;
+                const int rr = m - n * per;
+                const int oy = (rr / QW) * osy + oy0, ox = (rr % QW) * osx + ox0;
+                const int64_t pix = ((int64_t)n * a.OH + oy) * a.OW + ox;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int o = n0 + wn * WN + j * 16 + (lane & 15);
+                    if (o >= a.Cout) continue;
+                    const float c = acc[i][j][r];
+                    if (SPLIT) {
+                        atomicAdd(a.acc + pix * a.Cout + o, c);
+                    } else {
+                        float v = c;
+                        if (a.e.on) {
+                            v = epi_full<T>(a.e, c, n, o, pix, a.Cout);
+                            if (a.e.aux_mode == 1) ((T*)a.e.aux)[pix * a.Cout + o] = (T)c;
+                            if (a.e.aux_mode == 2) ((T*)a.e.aux)[pix * a.Cout + o] = (T)v;
+                            if (a.e.residual) v = (float)(T)v + (float)((const T*)a.e.residual)[pix * a.Cout + o];
+                        }
+                        ((T*)a.y)[pix * a.Cout + o] = (T)v;
+                    }
+                }
+            }
+        }
+        return;
+    }
+    // 16-bit: epilogue math in registers, tile transposed through LDS, 16-byte row stores
+    constexpr int OS = BN + 8;
+    T* ot = lds;                 // [BM][OS]
+    T* xt = lds + BM * OS;       // [BM][OS] aux tile
+    const bool want_aux = a.e.on && a.e.aux_mode != 0;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + r;
-            if (m >= a.M) continue;
+            const int ml = wm * WM + i * 16 + 4 * (lane >> 4) + r;
+            const int m = min(m0 + ml, M - 1);
             const int n = m / per;
             const int rr = m - n * per;
-            const int oy = (rr / a.QW) * a.osy + a.oy0, ox = (rr % a.QW) * a.osx + a.ox0;
-            const int64_t obase = (((int64_t)n * a.OH + oy) * a.OW + ox) * a.Cout;
+            const int oy = (rr / QW) * osy + oy0, ox = (rr % QW) * osx + ox0;
+            const int64_t pix = ((int64_t)n * a.OH + oy) * a.OW + ox;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int o = n0 + wn * WN + j * 16 + (lane & 15);
-                if (o >= a.Cout) continue;
-                if (SPLIT)
-                    atomicAdd(a.acc + obase + o, acc[i][j][r]);
-                else
-                    ((T*)a.y)[obase + o] = (T)acc[i][j][r];
+                const int ol = wn * WN + j * 16 + (lane & 15);
+                const int o = min(n0 + ol, a.Cout - 1);
+                const float c = acc[i][j][r];
+                float v = c;
+                if (a.e.on) v = epi_full<T>(a.e, c, n, o, pix, a.Cout);
+                ot[ml * OS + ol] = (T)v;
+                if (want_aux) xt[ml * OS + ol] = (T)(a.e.aux_mode == 1 ? c : v);
+            }
+        }
+    }
+    __syncthreads();
+    typedef T vec8o __attribute__((ext_vector_type(8)));
+    const bool cvec = (a.Cout % 8) == 0;
+    constexpr int CPR = BN / 8;                      // 16-byte chunks per tile row
+#pragma unroll
+    for (int k = 0; k < BM * CPR / 256; ++k) {
+        const int idx = tid + k * 256;
+        const int ml = idx / CPR, c8 = (idx % CPR) * 8;
+        const int m = m0 + ml, o = n0 + c8;
+        if (m >= M || o >= a.Cout) continue;
+        const int n = m / per;
+        const int rr = m - n * per;
+        const int oy = (rr / QW) * osy + oy0, ox = (rr % QW) * osx + ox0;
+        const int64_t dst = (((int64_t)n * a.OH + oy) * a.OW + ox) * a.Cout + o;
+        if (cvec) {
+            vec8o v = *(const vec8o*)(ot + ml * OS + c8);
+            if (a.e.on && a.e.residual) {
+                const vec8o rv = *(const vec8o*)((const T*)a.e.residual + dst);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = (T)((float)v[e] + (float)rv[e]);
+            }
+            *(vec8o*)((T*)a.y + dst) = v;
+            if (want_aux) *(vec8o*)((T*)a.e.aux + dst) = *(const vec8o*)(xt + ml * OS + c8);
+        } else {
+            for (int e = 0; e < 8 && o + e < a.Cout; ++e) {
+                float v = (float)ot[ml * OS + c8 + e];
+                if (a.e.on && a.e.residual) v += (float)((const T*)a.e.residual)[dst + e];
+                ((T*)a.y)[dst + e] = (T)v;
+                if (want_aux) ((T*)a.e.aux)[dst + e] = xt[ml * OS + c8 + e];
             }
         }
     }
 }
 
+// Split-K finalize: f32 partial sums -> T with the fused epilogue.
 template <typename T>
-__global__ void f32_to_t_kernel(T* y, const float* src, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        y[i] = (T)src[i];
+__global__ void conv_finalize_kernel(T* y, const float* src, Epi e, int64_t n_el, int Cout, int64_t pix_per_n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_el; i += (int64_t)gridDim.x * blockDim.x) {
+        const float c = src[i];
+        float v = c;
+        if (e.on) {
+            const int64_t pix = i / Cout;
+            const int o = (int)(i - pix * Cout);
+            const int n = (int)(pix / pix_per_n);
+            v = epi_full<T>(e, c, n, o, pix, Cout);
+            if (e.aux_mode == 1) ((T*)e.aux)[i] = (T)c;
+            if (e.aux_mode == 2) ((T*)e.aux)[i] = (T)v;
+            if (e.residual) v = (float)(T)v + (float)((const T*)e.residual)[i];
+        }
+        y[i] = (T)v;
+    }
 }
 
 template <typename T, int BM, int BN>
-int launch_fwd(ConvArgs& a, bool vec, int splits, hipStream_t s) {
-    dim3 grid((unsigned)cdiv(a.M, BM), (unsigned)cdiv(a.Cout, BN), (unsigned)splits);
-    a.kper = (int)cdiv(a.nk, splits);
-    if (splits > 1) {
-        if (vec) conv_fwd_kernel<T, BM, BN, true, true><<<grid, 256, 0, s>>>(a);
-        else conv_fwd_kernel<T, BM, BN, false, true><<<grid, 256, 0, s>>>(a);
-    } else {
-        if (vec) conv_fwd_kernel<T, BM, BN, true, false><<<grid, 256, 0, s>>>(a);
-        else conv_fwd_kernel<T, BM, BN, false, false><<<grid, 256, 0, s>>>(a);
+size_t fwd_lds_bytes() {
+    constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
+    const size_t main = 2 * (size_t)(BM + BN) * (BK + V) * sizeof(T);
+    const size_t epi = std::is_same<T, float>::value ? 0 : 2 * (size_t)BM * (BN + 8) * sizeof(T);
+    return std::max(main, epi);
+}
+
+template <typename T, int BM, int BN, bool VEC, bool SPLIT>
+int launch_fwd_k(ConvArgs& a, dim3 grid, hipStream_t s) {
+    auto kern = conv_fwd_kernel<T, BM, BN, VEC, SPLIT>;
+    const size_t lds = fwd_lds_bytes<T, BM, BN>();
+    static bool attr_set = false;   // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
     }
+    kern<<<grid, 256, lds, s>>>(a);
     return launch_status("sg2_conv2d");
+}
+
+template <typename T, int BM, int BN>
+int launch_fwd(ConvArgs& a, bool vec, hipStream_t s) {
+    int maxM = 0;
+    int nph = 0;
+    for (int i = 0; i < kMaxPhases; ++i)
+        if (a.ph[i].M > 0) { maxM = std::max(maxM, a.ph[i].M); nph = i + 1; }
+    dim3 grid((unsigned)cdiv(maxM, BM), (unsigned)cdiv(a.Cout, BN), (unsigned)(nph * a.splits));
+    if (a.splits > 1) return vec ? launch_fwd_k<T, BM, BN, true, true>(a, grid, s) : launch_fwd_k<T, BM, BN, false, true>(a, grid, s);
+    return vec ? launch_fwd_k<T, BM, BN, true, false>(a, grid, s) : launch_fwd_k<T, BM, BN, false, false>(a, grid, s);
 }
 
 // ------------------------------------------------------------------------------------ wgrad
@@ -467,63 +620,73 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* scale,
                     int B, hipStream_t s);   // wgrad3x3.hip
 }  // namespace sg2
 
-extern "C" int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W, int Cout,
-                          int OH, int OW, int KH, int KW, int stride, int pad_y, int pad_x, int transpose,
-                          float* workspace, int64_t workspace_elems, void* stream) {
+extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
+                                int Cout, int OH, int OW, int KH, int KW, int stride, int pad_y, int pad_x,
+                                int transpose, const float* in_scale, const sg2_epilogue* epi, float* workspace,
+                                int64_t workspace_elems, void* stream) {
     using namespace sg2;
     SG2_CHECK(y && x && w, "sg2_conv2d: null pointer");
     SG2_CHECK(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0 && OH > 0 && OW > 0, "sg2_conv2d: empty shape");
     SG2_CHECK(KH >= 1 && KW >= 1 && KH * KW <= kMaxTaps, "sg2_conv2d: kernel too large");
     SG2_CHECK(stride >= 1 && stride <= 4, "sg2_conv2d: unsupported stride");
+    SG2_CHECK(pad_y > -64 && pad_y < 64 && pad_x > -64 && pad_x < 64, "sg2_conv2d: padding out of range");
     SG2_CHECK((int64_t)N * OH * OW * Cout < INT32_MAX && (int64_t)N * H * W * Cin < ((int64_t)1 << 40),
               "sg2_conv2d: tensor too large");
+    if (epi) {
+        SG2_CHECK(epi->act == 0 || epi->act == 1, "sg2_conv2d: epilogue act must be 0 (linear) or 1 (lrelu)");
+        SG2_CHECK(epi->aux_mode >= 0 && epi->aux_mode <= 2 && (epi->aux_mode == 0 || epi->aux),
+                  "sg2_conv2d: bad epilogue aux output");
+    }
     hipStream_t s = as_stream(stream);
 
-    // Output phases.
-    struct Phase { ConvArgs a; };
-    Phase ph[16];  // stride <= 4
-    int nph = 0;
     ConvArgs base{};
-    base.x = x; base.w = w; base.y = y; base.acc = nullptr;
+    base.x = x; base.w = w; base.y = y; base.acc = nullptr; base.in_scale = in_scale;
     base.N = N; base.H = H; base.W = W; base.Cin = Cin; base.Cout = Cout; base.OH = OH; base.OW = OW;
     base.wtaps = KH * KW;
+    if (epi) {
+        Epi& e = base.e;
+        e.out_scale = epi->out_scale; e.noise = epi->noise; e.bias = epi->bias; e.residual = epi->residual;
+        e.aux = epi->aux; e.noise_gain = epi->noise_gain; e.alpha = epi->alpha; e.gain = epi->gain;
+        e.clamp = epi->clamp; e.act = epi->act; e.aux_mode = epi->aux_mode; e.on = 1;
+    }
+    // Output phases (one for a plain conv; stride^2 for a transposed conv, launched 4 at a time).
+    struct PhaseDef { Phase p; int ntaps; Tap taps[kMaxTaps]; };
+    PhaseDef defs[16];
+    int nph = 0;
     if (!transpose) {
-        ConvArgs a = base;
-        a.QH = OH; a.QW = OW; a.osy = a.osx = 1; a.oy0 = a.ox0 = 0; a.isy = a.isx = stride;
+        PhaseDef& d = defs[nph++];
+        d.p = Phase{};
+        d.p.QH = OH; d.p.QW = OW; d.p.osy = d.p.osx = 1; d.p.oy0 = d.p.ox0 = 0;
         SG2_CHECK((int64_t)(OH - 1) * stride - pad_y + KH - 1 >= 0, "sg2_conv2d: bad geometry");
-        a.taps.n = 0;
+        d.ntaps = 0;
         for (int ky = 0; ky < KH; ++ky)
-            for (int kx = 0; kx < KW; ++kx) {
-                a.taps.dy[a.taps.n] = ky - pad_y;
-                a.taps.dx[a.taps.n] = kx - pad_x;
-                a.taps.w[a.taps.n] = ky * KW + kx;
-                a.taps.n++;
-            }
-        ph[nph++].a = a;
+            for (int kx = 0; kx < KW; ++kx)
+                d.taps[d.ntaps++] = Tap{(int8_t)(ky - pad_y), (int8_t)(kx - pad_x), (int8_t)(ky * KW + kx), 0};
+        base.isy = base.isx = stride;
     } else {
         // y[oy] = sum_{iy,ky: oy = iy*S + ky - P} x[iy] w[ky]  ->  phase py = oy mod S
         for (int py = 0; py < stride; ++py)
             for (int px = 0; px < stride; ++px) {
-                ConvArgs a = base;
-                a.QH = (OH - py + stride - 1) / stride;
-                a.QW = (OW - px + stride - 1) / stride;
-                if (a.QH <= 0 || a.QW <= 0) continue;
-                a.osy = a.osx = stride; a.oy0 = py; a.ox0 = px; a.isy = a.isx = 1;
-                a.taps.n = 0;
+                PhaseDef& d = defs[nph];
+                d.p = Phase{};
+                d.p.QH = (OH - py + stride - 1) / stride;
+                d.p.QW = (OW - px + stride - 1) / stride;
+                if (d.p.QH <= 0 || d.p.QW <= 0) continue;
+                d.p.osy = d.p.osx = stride; d.p.oy0 = py; d.p.ox0 = px;
+                d.ntaps = 0;
                 for (int ky = 0; ky < KH; ++ky) {
                     const int ny = py + pad_y - ky;
                     if (((ny % stride) + stride) % stride) continue;
                     for (int kx = 0; kx < KW; ++kx) {
                         const int nx = px + pad_x - kx;
                         if (((nx % stride) + stride) % stride) continue;
-                        a.taps.dy[a.taps.n] = floordiv_h(ny, stride);
-                        a.taps.dx[a.taps.n] = floordiv_h(nx, stride);
-                        a.taps.w[a.taps.n] = ky * KW + kx;
-                        a.taps.n++;
+                        d.taps[d.ntaps++] = Tap{(int8_t)floordiv_h(ny, stride), (int8_t)floordiv_h(nx, stride),
+                                                (int8_t)(ky * KW + kx), 0};
                     }
                 }
-                ph[nph++].a = a;
+                ++nph;
             }
+        base.isy = base.isx = 1;
     }
 
     int rc = 0;
@@ -531,48 +694,59 @@ extern "C" int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int 
         constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
         const bool vec = (Cin % V == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)w % 16 == 0);
         const bool wide = Cout > 64;
+        const int BN_ = wide ? 128 : 64;
+        base.nck = (Cin + BK - 1) / BK;
         // split-K when the grid is too small to fill 256 CUs
         int64_t blocks = 0;
-        int64_t minnk = INT32_MAX;
+        int maxnk = 1;
         for (int i = 0; i < nph; ++i) {
-            ConvArgs& a = ph[i].a;
-            a.M = N * a.QH * a.QW;
-            a.nck = (Cin + BK - 1) / BK;
-            a.nk = a.taps.n * a.nck;
-            blocks += cdiv(a.M, wide ? 128 : 128) * cdiv(Cout, wide ? 128 : 64);
-            minnk = std::min<int64_t>(minnk, std::max(1, a.nk));
+            const int M = N * defs[i].p.QH * defs[i].p.QW;
+            blocks += cdiv(M, 128) * cdiv(Cout, BN_);
+            maxnk = std::max(maxnk, defs[i].ntaps * base.nck);
         }
         int splits = 1;
         const int64_t total_out = (int64_t)N * OH * OW * Cout;
         if (blocks < 512 && workspace != nullptr && workspace_elems >= total_out)
-            splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(1024, blocks), minnk / 4));
+            splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(1024, blocks), maxnk / 4));
         const bool split = splits > 1;
         if (split) {
             hipError_t e = hipMemsetAsync(workspace, 0, total_out * sizeof(float), s);
             if (e != hipSuccess) { set_error("sg2_conv2d: memset failed"); return (int)e; }
-        } else if (transpose) {
-            // phases with no taps produce zeros
-            for (int i = 0; i < nph; ++i)
-                if (ph[i].a.taps.n == 0) {
-                    hipError_t e = hipMemsetAsync(y, 0, total_out * sizeof(T), s);
-                    if (e != hipSuccess) { set_error("sg2_conv2d: memset failed"); return (int)e; }
-                    break;
-                }
         }
-        for (int i = 0; i < nph && rc == 0; ++i) {
-            ConvArgs& a = ph[i].a;
+        for (int g0 = 0; g0 < nph && rc == 0; g0 += kMaxPhases) {
+            ConvArgs a = base;
             a.acc = split ? workspace : nullptr;
-            if (a.taps.n == 0) continue;
-            if (wide) rc = launch_fwd<T, 128, 128>(a, vec, split ? splits : 1, s);
-            else rc = launch_fwd<T, 128, 64>(a, vec, split ? splits : 1, s);
+            a.splits = splits;
+            a.kper = (int)cdiv(maxnk, splits);
+            int nt = 0;
+            for (int i = 0; i < kMaxPhases; ++i) {
+                a.ph[i] = Phase{};
+                if (g0 + i >= nph) continue;
+                const PhaseDef& d = defs[g0 + i];
+                a.ph[i] = d.p;
+                a.ph[i].M = N * d.p.QH * d.p.QW;
+                a.ph[i].tap0 = nt;
+                a.ph[i].ntaps = d.ntaps;
+                a.ph[i].nk = d.ntaps * base.nck;
+                for (int t = 0; t < d.ntaps; ++t) a.taps[nt++] = d.taps[t];
+            }
+            if (wide) rc = launch_fwd<T, 128, 128>(a, vec, s);
+            else rc = launch_fwd<T, 128, 64>(a, vec, s);
         }
         if (rc == 0 && split) {
             const int g = (int)std::min<int64_t>(cdiv(total_out, 256), 4096);
-            f32_to_t_kernel<T><<<g, 256, 0, s>>>((T*)y, workspace, total_out);
+            conv_finalize_kernel<T><<<g, 256, 0, s>>>((T*)y, workspace, base.e, total_out, Cout, (int64_t)OH * OW);
             rc = launch_status("sg2_conv2d finalize");
         }
     });
     return rc;
+}
+
+extern "C" int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W, int Cout,
+                          int OH, int OW, int KH, int KW, int stride, int pad_y, int pad_x, int transpose,
+                          float* workspace, int64_t workspace_elems, void* stream) {
+    return sg2_conv2d_fused(y, x, w, dtype, N, Cin, H, W, Cout, OH, OW, KH, KW, stride, pad_y, pad_x, transpose,
+                            nullptr, nullptr, workspace, workspace_elems, stream);
 }
 
 extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,

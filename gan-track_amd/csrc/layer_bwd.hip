@@ -10,7 +10,7 @@
 //   dnoise[n,p] = sum_o dz              (noise-strength gradient; written, each pixel owned by one WG)
 // Replaces: bias_act grad kernel + db reduction + noise reduction + (dz*c).sum + dz*d of the
 // composed reference path (five to seven passes over the activation).
-// NHWC layout: a lane owns 8 consecutive channels of one pixel (16-byte loads); C % 8 == 0.
+// NHWC layout: a lane owns 8 consecutive channels of one pixel (16-byte loads, 32 for f32); C % 8 == 0.
 #include "sg2_common.h"
 
 namespace sg2 {
@@ -112,7 +112,6 @@ extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, cons
     SG2_CHECK(dc && dy && y, "sg2_layer_bwd: null pointer");
     SG2_CHECK(C % 8 == 0 && C <= 2048 && C >= 8, "sg2_layer_bwd: C must be a multiple of 8 (<= 2048)");
     SG2_CHECK(dtype == SG2_F16 || dtype == SG2_BF16 || dtype == SG2_F32, "sg2_layer_bwd: bad dtype");
-    SG2_CHECK(!(dtype == SG2_F32), "sg2_layer_bwd: 16-bit activations only");
     SG2_CHECK(act == 0 || act == 1, "sg2_layer_bwd: act must be linear or lrelu");
     if ((int64_t)N * HW == 0) return 0;
     hipStream_t s = as_stream(stream);
@@ -128,6 +127,7 @@ extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, cons
     dim3 grid((unsigned)cdiv(HW, a.pix_per_block), (unsigned)N);
     const size_t lds = (2 * C + a.pix_per_block) * sizeof(float);
     if (dtype == SG2_F16) layer_bwd_kernel<f16_t><<<grid, 256, lds, s>>>(a);
-    else layer_bwd_kernel<bf16_t><<<grid, 256, lds, s>>>(a);
+    else if (dtype == SG2_BF16) layer_bwd_kernel<bf16_t><<<grid, 256, lds, s>>>(a);
+    else layer_bwd_kernel<float><<<grid, 256, lds, s>>>(a);
     return launch_status("sg2_layer_bwd");
 }

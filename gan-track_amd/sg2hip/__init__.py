@@ -16,6 +16,15 @@ F32, F16, BF16 = 0, 1, 2
 _DTYPES = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16}
 
 _c_i64p = ctypes.POINTER(ctypes.c_int64)
+
+
+class Epilogue(ctypes.Structure):
+    """sg2_epilogue (include/sg2hip.h)."""
+    _fields_ = [('out_scale', ctypes.c_void_p), ('noise', ctypes.c_void_p), ('bias', ctypes.c_void_p),
+                ('residual', ctypes.c_void_p), ('aux', ctypes.c_void_p), ('noise_gain', ctypes.c_float),
+                ('alpha', ctypes.c_float), ('gain', ctypes.c_float), ('clamp', ctypes.c_float),
+                ('act', ctypes.c_int), ('aux_mode', ctypes.c_int)]
+
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _i64 = ctypes.c_int64
@@ -28,6 +37,8 @@ SIGNATURES = {
     'sg2_upfirdn2d': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i,
                       _i, _f, _vp],
     'sg2_conv2d': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i64, _vp],
+    'sg2_conv2d_fused': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp,
+                         ctypes.POINTER(Epilogue), _vp, _i64, _vp],
     'sg2_conv3x3': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _f, _f, _f, _vp, _vp,
                     _vp],
     'sg2_conv2d_wgrad': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp],

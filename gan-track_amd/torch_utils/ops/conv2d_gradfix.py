@@ -15,6 +15,7 @@ Activations are NHWC in memory (torch channels_last); weights are packed K-conti
 channel before each launch (a few MB at most).
 """
 import contextlib
+import ctypes
 
 import torch
 
@@ -65,6 +66,31 @@ def _conv_raw(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose):
         stride, pad[0], pad[1], int(transpose), _hip.ptr(ws), ws.numel() if ws is not None else 0,
         _hip.stream_ptr(x.device)), 'sg2_conv2d')
     return y
+
+
+def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_scale=None, out_scale=None,
+               noise=None, noise_gain=1.0, bias=None, act=0, alpha=0.2, gain=1.0, clamp=-1.0, residual=None,
+               aux_mode=0):
+    """sg2_conv2d_fused: y = round(clamp(act(conv(x * in_scale, w) * out_scale + noise * g + bias) * gain))
+    + residual.  Returns (y, aux) with aux = conv result (aux_mode 1) or activation (aux_mode 2)."""
+    n, cin, h, w = x.shape
+    y = torch.empty([n, cout, oh, ow], dtype=x.dtype, device=x.device, memory_format=_CL)
+    aux = torch.empty_like(y) if aux_mode else None
+    if residual is not None:
+        residual = _nhwc(residual)
+        assert residual.shape == y.shape and residual.dtype == y.dtype
+    epi = None
+    if any(v is not None for v in (out_scale, noise, bias, residual)) or act != 0 or gain != 1.0 or clamp >= 0 \
+            or aux_mode:
+        epi = _hip.Epilogue(_hip.ptr(out_scale), _hip.ptr(noise), _hip.ptr(bias), _hip.ptr(residual), _hip.ptr(aux),
+                            float(noise_gain), float(alpha), float(gain), float(clamp), int(act), int(aux_mode))
+    total = n * cout * oh * ow
+    ws = torch.empty([total], dtype=torch.float32, device=x.device) if total <= _WS_LIMIT else None
+    _hip.check(_hip.lib().sg2_conv2d_fused(
+        _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
+        stride, pad[0], pad[1], int(transpose), _hip.ptr(in_scale), ctypes.byref(epi) if epi is not None else None,
+        _hip.ptr(ws), ws.numel() if ws is not None else 0, _hip.stream_ptr(x.device)), 'sg2_conv2d_fused')
+    return y, aux
 
 
 def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None):

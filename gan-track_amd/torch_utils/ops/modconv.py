@@ -1,15 +1,23 @@
-"""Fused StyleGAN2 synthesis layer (3x3, up = 1) on the LDS-halo MFMA kernel (sg2_conv3x3).
+"""Fused StyleGAN2 conv layers: convolution + modulation + demodulation + noise + bias + activation
+(+ resnet residual) in one kernel launch, with a fused first-order backward.
 
-Forward, ONE kernel (reference SG3/training/networks_stylegan2.py:309-328 and modulated_conv2d
-:32-77, non-fused training form):
-    c = conv2d(x * s[n, ci], W)                  (modulation applied while staging x into LDS)
-    y = clamp(lrelu(c * d[n, co] + noise + b) * gain, +-clamp)
-where the reference runs x*s, conv, fma(x, d, noise) and bias_act as four passes over HBM.
+Forward (reference SG3/training/networks_stylegan2.py: SynthesisLayer :309-328 with
+modulated_conv2d :32-77 in its non-fused training form; Conv2dLayer :172-181; the resnet add of
+DiscriminatorBlock :621-627):
+    c = conv(x * s[n, ci], W)                      (modulation applied while staging x)
+    z = clamp(act(c * d[n, co] + noise + b) * gain, +-clamp)
+    y = z + residual                               (optional)
+where the reference runs x*s, conv, fma(x, d, noise), bias_act and add as separate HBM passes.
+The 3x3 / stride-1 16-bit layers run on the LDS-halo kernel (sg2_conv3x3); every other geometry and
+f32 runs on the implicit-GEMM kernel with the same epilogue (sg2_conv2d_fused).
 
-Backward is composed of differentiable primitives (bias_act grad op, HIP conv / transposed conv /
-weight-gradient Functions, small torch reductions), so second-order passes (path-length
-regulariser) differentiate through it.  The conv result c is kept from the forward for the first
-order; under create_graph it is recomputed as a differentiable conv so d(dL/dd)/dW, /ds, /dx exist.
+Backward:
+  * first order (no create_graph): sg2_layer_bwd (dz, dc = dz*d, db, dd, dnoise in one pass), then
+    the data gradient with the `*s` scale (and on the halo kernel the `ds` dot reduction) in its
+    epilogue, and the weight gradient with the modulation applied to its B operand;
+  * under create_graph (path-length / R1 double backward) the same gradient is composed of
+    differentiable primitives (bias_act grad op, HIP conv / transposed conv / weight-gradient
+    Functions), and c is recomputed as a differentiable conv so d(dL/dd)/dW, /ds, /dx exist.
 """
 import torch
 
@@ -17,102 +25,28 @@ from . import bias_act as _ba
 from . import conv2d_gradfix as _cg
 
 _CL = torch.channels_last
-enabled = True   # switch for A/B tests against the composed (unfused) path
+enabled = True         # switch for A/B tests against the composed (unfused) path
+fast_backward = True   # first-order backward through the fused kernels (A/B switch)
+_ACT = {0: 'linear', 1: 'lrelu'}
 
 
 def supported(x, weight, up):
+    """The 3x3 up=1 synthesis / D layer on the LDS-halo kernel (16-bit, >= 16^2)."""
     n, cin, h, w = x.shape
     cout, _, kh, kw = weight.shape
     return (enabled and up == 1 and kh == 3 and kw == 3 and x.dtype in (torch.float16, torch.bfloat16) and x.is_cuda and
             cin % 8 == 0 and cout % 8 == 0 and h >= 16 and w >= 16)
 
 
-class ModConvLayer(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, styles, weight, dcoefs, noise, bias, alpha, gain, clamp):
-        x = _cg._nhwc(x)
-        n, cin, h, w = x.shape
-        cout = weight.shape[0]
-        wT = weight.to(x.dtype)
-        nz = None
-        if noise is not None:
-            nz = noise.to(x.dtype).reshape(n, h, w).contiguous()
-        want_raw = any(ctx.needs_input_grad[:6])
-        want_raw = want_raw and dcoefs is not None     # c only feeds dL/dd
-        y, c = _cg.conv3x3_fused(x, _cg._pack_conv(wT), cout, in_scale=_f32(styles), out_scale=_f32(dcoefs),
-                                 noise=nz, noise_gain=1.0, bias=_f32(bias), act=1, alpha=alpha, gain=gain,
-                                 clamp=clamp, want_raw=want_raw)
-        ctx.save_for_backward(x, styles, weight, dcoefs, noise, bias, y, c)
-        ctx.cfg = (alpha, gain, clamp)
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, styles, weight, dcoefs, noise, bias, y, c = ctx.saved_tensors
-        alpha, gain, clamp = ctx.cfg
-        n, cin, h, w = x.shape
-        dt = x.dtype
-        need = ctx.needs_input_grad
-        if not torch.is_grad_enabled() and fast_backward:
-            return _fast_backward(ctx, dy, x, styles, weight, dcoefs, noise, bias, y, c, alpha, gain, clamp)
-        dz = _ba.bias_act_grad(dy, y, act='lrelu', alpha=alpha, gain=gain, clamp=clamp)
-        dx = ds = dw = dd = dnoise = db = None
-        if need[5] and bias is not None:
-            db = dz.sum([0, 2, 3], dtype=torch.float32).to(bias.dtype)
-        if need[4] and noise is not None:
-            dnoise = dz.sum(1, keepdim=True, dtype=torch.float32).to(noise.dtype)
-        s_ = styles.to(dt).reshape(n, -1, 1, 1) if styles is not None else None
-        if need[3] and dcoefs is not None:
-            if torch.is_grad_enabled():
-                c_ = _cg._Conv2d.apply(_mul(x, s_), weight.to(dt), 1, (1, 1), (h, w))
-            else:
-                c_ = c
-            dd = (dz * c_).sum([2, 3], dtype=torch.float32).to(dcoefs.dtype)
-        dc = dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None else dz
-        if need[0] or need[1]:
-            dxs = _cg._ConvT2d.apply(dc, weight.to(dt), 1, (1, 1), (h, w))
-            if need[0]:
-                dx = _mul(dxs, s_)
-            if need[1] and styles is not None:
-                ds = (dxs * x).sum([2, 3], dtype=torch.float32).to(styles.dtype)
-        if need[2] and not _cg.weight_gradients_disabled:
-            dw = _cg._WGrad.apply(dc, _mul(x, s_), (3, 3), 1, (1, 1)).to(weight.dtype)
-        return dx, ds, dw, dd, dnoise, db, None, None, None
+def supported_generic(x, weight):
+    """Any other geometry / dtype on the implicit-GEMM kernel."""
+    return enabled and x.is_cuda
 
 
-def _fast_backward(ctx, dy, x, styles, weight, dcoefs, noise, bias, y, c, alpha, gain, clamp):
-    """First-order backward in three kernels (no create_graph):
-      sg2_layer_bwd  : dz, dc = dz*d, db, dd = sum dz*c, dnoise         (one pass over dy, y, c)
-      sg2_conv3x3    : dx = convT(dc, W) * s, ds = sum convT(dc, W) * x  (dgrad with scale + dot epilogue)
-      sg2_conv2d_wgrad: dw = sum dc (x) (x * s)                          (modulation applied to the B operand)
-    """
-    need = ctx.needs_input_grad
+def _halo(x, kh, kw, stride, pad):
     n, cin, h, w = x.shape
-    dt = x.dtype
-    d32 = dcoefs.float().contiguous() if dcoefs is not None else None
-    dc, db, dd, dn = _cg.layer_bwd(dy.to(dt), y, c if (need[3] and d32 is not None) else None, d32, act=1,
-                                   alpha=alpha, gain=gain, clamp=clamp, want_db=need[5] and bias is not None,
-                                   want_dd=need[3] and d32 is not None, want_dnoise=need[4] and noise is not None)
-    dx = ds = dw = None
-    s32 = _f32(styles)
-    want_ds = need[1] and styles is not None
-    if need[0] or want_ds:
-        wT = _cg._pack_convT(weight.to(dt).flip([2, 3]))
-        if want_ds:
-            dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
-            ds = ds.to(styles.dtype)
-        else:
-            dx, _ = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32)
-        dx = dx if need[0] else None
-    if need[2] and not _cg.weight_gradients_disabled:
-        dw = _cg._wgrad_raw(dc, x, 3, 3, 1, (1, 1), x_scale=s32).to(weight.dtype)
-    db = db.to(bias.dtype) if db is not None else None
-    dd = dd.to(dcoefs.dtype) if dd is not None else None
-    dn = dn.to(noise.dtype) if dn is not None else None
-    return dx, ds, dw, dd, dn, db, None, None, None
-
-
-fast_backward = True   # first-order backward through the fused kernels (A/B switch)
+    return (kh == 3 and kw == 3 and stride == 1 and pad == 1 and x.dtype in (torch.float16, torch.bfloat16) and
+            cin % 8 == 0 and h >= 16 and w >= 16)
 
 
 def _f32(t):
@@ -123,8 +57,135 @@ def _mul(a, s):
     return a * s if s is not None else a
 
 
+class FusedConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, styles, weight, dcoefs, noise, bias, residual, stride, pad, act, alpha, gain, clamp):
+        x = _cg._nhwc(x)
+        n, cin, h, w = x.shape
+        cout, _, kh, kw = weight.shape
+        oh = (h + 2 * pad - kh) // stride + 1
+        ow = (w + 2 * pad - kw) // stride + 1
+        dt = x.dtype
+        wT = weight.to(dt)
+        nz = noise.to(dt).reshape(n, oh, ow).contiguous() if noise is not None else None
+        any_grad = any(ctx.needs_input_grad[:7])
+        want_c = any_grad and dcoefs is not None          # c feeds dL/dd
+        want_z = any_grad and residual is not None        # z = y - residual feeds the activation grad
+        assert not (want_c and want_z), 'demodulation and a residual in one layer are not supported'
+        b32 = _f32(bias.to(dt)) if bias is not None else None   # the reference adds the bias rounded to x.dtype
+        if _halo(x, kh, kw, stride, pad) and residual is None:
+            y, aux = _cg.conv3x3_fused(x, _cg._pack_conv(wT), cout, in_scale=_f32(styles), out_scale=_f32(dcoefs),
+                                       noise=nz, noise_gain=1.0, bias=b32, act=act, alpha=alpha, gain=gain,
+                                       clamp=clamp, want_raw=want_c)
+        else:
+            y, aux = _cg.conv_fused(x, _cg._pack_conv(wT), cout, oh, ow, kh, kw, stride, (pad, pad),
+                                    in_scale=_f32(styles), out_scale=_f32(dcoefs), noise=nz, noise_gain=1.0,
+                                    bias=b32, act=act, alpha=alpha, gain=gain, clamp=clamp, residual=residual,
+                                    aux_mode=1 if want_c else (2 if want_z else 0))
+        ctx.save_for_backward(x, styles, weight, dcoefs, noise, bias, y, aux)
+        ctx.cfg = (stride, pad, act, alpha, gain, clamp, residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, styles, weight, dcoefs, noise, bias, y, aux = ctx.saved_tensors
+        stride, pad, act, alpha, gain, clamp, has_res = ctx.cfg
+        need = ctx.needs_input_grad
+        dres = dy if need[6] else None
+        zsrc = aux if has_res else y
+        c = aux if (dcoefs is not None and not has_res) else None
+        if not torch.is_grad_enabled() and fast_backward:
+            g = _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain,
+                               clamp)
+        else:
+            g = _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha,
+                                   gain, clamp)
+        return g + (dres, None, None, None, None, None, None)
+
+
+def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain, clamp):
+    """First order in three kernels: sg2_layer_bwd; dgrad with the *s scale (+ ds); scaled wgrad."""
+    n, cin, h, w = x.shape
+    cout, _, kh, kw = weight.shape
+    dt = x.dtype
+    d32 = _f32(dcoefs)
+    want_dd = need[3] and d32 is not None
+    want_db, want_dn = need[5] and bias is not None, need[4] and noise is not None
+    if zsrc.shape[1] % 8 == 0:
+        dc, db, dd, dn = _cg.layer_bwd(dy.to(dt), zsrc, c if want_dd else None, d32, act=act, alpha=alpha, gain=gain,
+                                       clamp=clamp, want_db=want_db, want_dd=want_dd, want_dnoise=want_dn)
+    else:   # narrow outputs (toRGB): plain kernels
+        dz = _ba.bias_act_grad(dy, zsrc, act=_ACT[act], alpha=alpha, gain=gain, clamp=clamp)
+        db = dz.sum([0, 2, 3], dtype=torch.float32) if want_db else None
+        dd = (dz * c).sum([2, 3], dtype=torch.float32) if want_dd else None
+        dn = dz.sum(1, keepdim=True, dtype=torch.float32) if want_dn else None
+        dc = _cg._nhwc(dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None else dz)
+    dx = ds = dw = None
+    s32 = _f32(styles)
+    want_ds = need[1] and styles is not None
+    if need[0] or want_ds:
+        if _halo(dc, kh, kw, stride, pad):
+            wT = _cg._pack_convT(weight.to(dt).flip([2, 3]))
+            if want_ds:
+                dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
+            else:
+                dx, _ = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32)
+        else:
+            dx, craw = _cg.conv_fused(dc, _cg._pack_convT(weight.to(dt)), cin, h, w, kh, kw, stride, (pad, pad),
+                                      transpose=True, out_scale=s32, aux_mode=1 if want_ds else 0)
+            if want_ds:
+                ds = (craw.float() * x.float()).sum([2, 3])
+        ds = ds.to(styles.dtype) if want_ds else None
+        dx = dx if need[0] else None
+    if need[2] and not _cg.weight_gradients_disabled:
+        dw = _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32).to(weight.dtype)
+    db = db.to(bias.dtype) if db is not None else None
+    dd = dd.to(dcoefs.dtype) if dd is not None else None
+    dn = dn.to(noise.dtype) if dn is not None else None
+    return dx, ds, dw, dd, dn, db
+
+
+def _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain,
+                       clamp):
+    """Differentiable form (used under create_graph)."""
+    n, cin, h, w = x.shape
+    cout, _, kh, kw = weight.shape
+    oh, ow = zsrc.shape[2], zsrc.shape[3]
+    dt = x.dtype
+    dz = _ba.bias_act_grad(dy, zsrc, act=_ACT[act], alpha=alpha, gain=gain, clamp=clamp)
+    dx = ds = dw = dd = dnoise = db = None
+    if need[5] and bias is not None:
+        db = dz.sum([0, 2, 3], dtype=torch.float32).to(bias.dtype)
+    if need[4] and noise is not None:
+        dnoise = dz.sum(1, keepdim=True, dtype=torch.float32).to(noise.dtype)
+    s_ = styles.to(dt).reshape(n, -1, 1, 1) if styles is not None else None
+    if need[3] and dcoefs is not None:
+        if torch.is_grad_enabled():
+            c_ = _cg._Conv2d.apply(_mul(x, s_), weight.to(dt), stride, (pad, pad), (oh, ow))
+        else:
+            c_ = c
+        dd = (dz * c_).sum([2, 3], dtype=torch.float32).to(dcoefs.dtype)
+    dc = dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None else dz
+    if need[0] or need[1]:
+        dxs = _cg._ConvT2d.apply(dc, weight.to(dt), stride, (pad, pad), (h, w))
+        if need[0]:
+            dx = _mul(dxs, s_)
+        if need[1] and styles is not None:
+            ds = (dxs * x).sum([2, 3], dtype=torch.float32).to(styles.dtype)
+    if need[2] and not _cg.weight_gradients_disabled:
+        dw = _cg._WGrad.apply(dc, _mul(x, s_), (kh, kw), stride, (pad, pad)).to(weight.dtype)
+    return dx, ds, dw, dd, dnoise, db
+
+
+def fused_conv(x, weight, styles=None, dcoefs=None, noise=None, bias=None, residual=None, stride=1, padding=0,
+               act='linear', alpha=0.2, gain=1.0, clamp=None):
+    return FusedConv.apply(x, styles, weight, dcoefs, noise, bias, residual, int(stride), int(padding),
+                           1 if act == 'lrelu' else 0, float(alpha), float(gain),
+                           float(clamp if clamp is not None else -1.0))
+
+
 def modconv_layer(x, styles, weight, dcoefs, noise, bias, alpha, gain, clamp):
-    """styles / dcoefs / noise / bias may be None: with styles = dcoefs = noise = None this is the
-    discriminator's plain 3x3 Conv2dLayer + bias + lrelu (networks_stylegan2.py:172-181) in one kernel."""
-    return ModConvLayer.apply(x, styles, weight, dcoefs, noise, bias, float(alpha), float(gain),
-                              float(clamp if clamp is not None else -1.0))
+    """3x3 modulated synthesis layer (lrelu).  With styles = dcoefs = noise = None this is the
+    discriminator's plain 3x3 Conv2dLayer + bias + lrelu (networks_stylegan2.py:172-181)."""
+    return fused_conv(x, weight, styles=styles, dcoefs=dcoefs, noise=noise, bias=bias, padding=1, act='lrelu',
+                      alpha=alpha, gain=gain, clamp=clamp)

@@ -115,18 +115,31 @@ class Conv2dLayer(torch.nn.Module):
             else:
                 self.bias = None
 
-    def forward(self, x, gain=1):
+    def forward(self, x, gain=1, residual=None):
+        """residual (DiscriminatorBlock's resnet skip, :621-627) is added to the activated output."""
         w = self.weight * self.weight_gain
-        if (self.up == 1 and self.down == 1 and self.activation == 'lrelu' and w.shape[2] == 3 and
-                modconv.supported(x, w, 1)):
-            # conv + bias + lrelu + gain + clamp in one LDS-halo kernel launch
-            clamp = self.conv_clamp * gain if self.conv_clamp is not None else -1.0
-            return modconv.modconv_layer(x, None, w, None, None, self.bias, 0.2, self.act_gain * gain, clamp)
+        clamp = self.conv_clamp * gain if self.conv_clamp is not None else None
+        kh = w.shape[2]
+        if self.activation in ('lrelu', 'linear') and self.up == 1 and modconv.supported_generic(x, w):
+            # conv + bias + act + gain + clamp (+ residual) in one kernel; the FIR of a down-2 layer runs
+            # first (conv2d_resample.py:94-97 / :106-109 plans, same padding algebra)
+            stride, pad = 1, self.padding
+            if self.down > 1:
+                x0, x1, y0, y1 = conv2d_resample._frame_padding(self.padding, self.resample_filter, 1, self.down)
+                if kh == 1:
+                    x = upfirdn2d.upfirdn2d(x, self.resample_filter, down=self.down, padding=[x0, x1, y0, y1])
+                else:
+                    x = upfirdn2d.upfirdn2d(x, self.resample_filter, padding=[x0, x1, y0, y1])
+                    stride = self.down
+                pad = 0
+            return modconv.fused_conv(x, w, bias=self.bias, residual=residual, stride=stride, padding=pad,
+                                      act=self.activation, alpha=bias_act.activation_funcs[self.activation].def_alpha or 0.2,
+                                      gain=self.act_gain * gain, clamp=clamp)
         b = self.bias.to(x.dtype) if self.bias is not None else None
         x = conv2d_resample.conv2d_resample(x=x, w=w.to(x.dtype), f=self.resample_filter, up=self.up, down=self.down,
                                             padding=self.padding, flip_weight=(self.up == 1))
-        clamp = self.conv_clamp * gain if self.conv_clamp is not None else None
-        return bias_act.bias_act(x, b, act=self.activation, gain=self.act_gain * gain, clamp=clamp)
+        x = bias_act.bias_act(x, b, act=self.activation, gain=self.act_gain * gain, clamp=clamp)
+        return x if residual is None else residual.add_(x)
 
     def extra_repr(self):
         return (f'in_channels={self.in_channels:d}, out_channels={self.out_channels:d}, '
@@ -213,8 +226,8 @@ class SynthesisLayer(torch.nn.Module):
             noise = torch.randn([x.shape[0], 1, self.resolution, self.resolution], device=x.device) * self.noise_strength
         if self.use_noise and noise_mode == 'const':
             noise = self.noise_const * self.noise_strength
-        if self.activation == 'lrelu' and modconv.supported(x, self.weight, self.up):
-            # one-kernel modulated conv + demod + noise + bias + lrelu + clamp (sg2_conv3x3)
+        if self.activation == 'lrelu' and self.up == 1 and modconv.supported_generic(x, self.weight):
+            # one-kernel modulated conv + demod + noise + bias + lrelu + clamp (sg2_conv3x3 / sg2_conv2d_fused)
             weight = self.weight
             if x.dtype == torch.float16:   # fp16 range pre-normalisation (:52-54)
                 weight = weight * (1 / np.sqrt(self.in_channels * 9) / weight.norm(float('inf'), dim=[1, 2, 3],
@@ -252,6 +265,10 @@ class ToRGBLayer(torch.nn.Module):
 
     def forward(self, x, w, fused_modconv=True):
         styles = self.affine(w) * self.weight_gain
+        if modconv.supported_generic(x, self.weight):
+            # modulation folded into the conv's operand staging, bias + clamp into its epilogue
+            return modconv.fused_conv(x, self.weight, styles=styles, bias=self.bias,
+                                      padding=self.weight.shape[-1] // 2, clamp=self.conv_clamp)
         x = modulated_conv2d(x=x, weight=self.weight, styles=styles, demodulate=False, fused_modconv=fused_modconv)
         return bias_act.bias_act(x, self.bias.to(x.dtype), clamp=self.conv_clamp)
 
@@ -438,8 +455,7 @@ class DiscriminatorBlock(torch.nn.Module):
         if self.architecture == 'resnet':
             y = self.skip(x, gain=np.sqrt(0.5))
             x = self.conv0(x)
-            x = self.conv1(x, gain=np.sqrt(0.5))
-            x = y.add_(x)
+            x = self.conv1(x, gain=np.sqrt(0.5), residual=y)   # y + conv1(x), the add fused into conv1
         else:
             x = self.conv0(x)
             x = self.conv1(x)

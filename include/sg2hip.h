@@ -82,6 +82,31 @@ int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int N, int Cin,
                int OH, int OW, int KH, int KW, int stride, int pad_y, int pad_x, int transpose,
                float* workspace, int64_t workspace_elems, void* stream);
 
+/* Fused epilogue of sg2_conv2d_fused (all pointers optional):
+ *   z   = clamp(act(c * out_scale[n,o] + noise[n,oy,ox] * noise_gain + bias[o]) * gain, +-clamp)
+ *   y   = round(z) + residual[n,oy,ox,o]          (residual: the resnet skip of the D block)
+ *   aux = c (aux_mode 1) or z (aux_mode 2)        (saved for the fused backward)
+ * Replaces the fma / bias_act / add passes the reference runs after each conv
+ * (networks_stylegan2.py:68-76, :172-181, :621-627). */
+typedef struct sg2_epilogue {
+    const float* out_scale;  /* [N, Cout] float32 */
+    const void* noise;       /* [N, OH, OW], activation dtype */
+    const float* bias;       /* [Cout] float32 */
+    const void* residual;    /* [N, OH, OW, Cout] NHWC, activation dtype */
+    void* aux;               /* [N, OH, OW, Cout] NHWC, activation dtype */
+    float noise_gain, alpha, gain, clamp;   /* clamp < 0: off */
+    int act;                 /* 0 linear, 1 lrelu(alpha) */
+    int aux_mode;            /* 0 none, 1 conv result c, 2 activation z */
+} sg2_epilogue;
+
+/* sg2_conv2d with the A operand modulated by in_scale[n, ci] (float32 [N, Cin], or NULL) and the
+ * fused epilogue above (epi may be NULL = plain convolution).  Transposed convolutions run all their
+ * stride x stride output phases in one launch (up to 4 phases per launch). */
+int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W, int Cout,
+                     int OH, int OW, int KH, int KW, int stride, int pad_y, int pad_x, int transpose,
+                     const float* in_scale, const sg2_epilogue* epi, float* workspace, int64_t workspace_elems,
+                     void* stream);
+
 /* 3x3 / stride 1 / pad 1 convolution of 16-bit NHWC activations with an LDS halo tile, optional
  * modulation of the input and the fused StyleGAN2 layer epilogue (networks_stylegan2.py:309-328):
  *   c      = conv(x[n,:,:,ci] * in_scale[n,ci], w)          w packed [Cout][3][3][Cin], Cin % 8 == 0
@@ -107,7 +132,7 @@ int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, 
 
 /* Fused first-order backward of the layer epilogue z = c*d + noise + b, y = clamp(act(z)*gain):
  *   dc = dz * d;  db[o] = sum dz;  dd[n,o] = sum_p dz*c;  dnoise[n,p] = sum_o dz
- * where dz = dy * act'(y) * gain masked by |y| < clamp.  dy, y, c, dc: [N, HW, C] 16-bit NHWC,
+ * where dz = dy * act'(y) * gain masked by |y| < clamp.  dy, y, c, dc: [N, HW, C] NHWC (any dtype),
  * C % 8 == 0.  c / d / db / dd / dnoise may be NULL; db and dd are zeroed by the call. */
 int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, const void* dy, const void* y, const void* c,
                   const float* d, int dtype, int N, int HW, int C, int act, float alpha, float gain, float clamp,
