@@ -46,6 +46,8 @@ struct Epi {
     const float* bias;       // [Cout]
     const void* residual;    // [N, OH, OW, Cout] (T), added after rounding the activation
     void* aux;               // [N, OH, OW, Cout] (T): aux_mode 1 = conv result, 2 = activation before residual
+    const void* dot_src;     // [N, OH, OW, Cout] (T): dot_out[n, o] += sum_p c * dot_src
+    float* dot_out;          // [N, Cout] float, zeroed by the host
     float noise_gain, alpha, gain, clamp;
     int act, aux_mode, on;
 };
@@ -137,8 +139,8 @@ __device__ __forceinline__ float epi_full(const Epi& e, float c, int n, int o, i
 }
 
 // Implicit-GEMM convolution.  grid = (M tiles, Cout tiles, phases * splits).
-template <typename T, int BM, int BN, bool VEC, bool SPLIT>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
+template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI>
+__global__ __launch_bounds__(256, 3) void conv_fwd_kernel(ConvArgs a) {
     constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
     constexpr int LPR = BK / V;          // lanes per tile row
     constexpr int RPP = 256 / LPR;       // rows per load pass
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
 
     vecT ra[PA], rb[PB];
     bool ra_ok[PA], rb_ok[PB];
-    float rsc[PA][V];
+    float rsc[SI ? PA : 1][V];
     int cur_c = 0;
     auto gload = [&](int kc) {
         const int t = kc / a.nck;
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
             ra_ok[i] = ok;
             const T* row = x + (((int64_t)a_n[i] * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.Cin;
             ra[i] = Loader<T, VEC>::load(row, c, a.Cin);
-            if (a.in_scale) {
+            if (SI) {
                 const float* sp = a.in_scale + (int64_t)a_n[i] * a.Cin;
 #pragma unroll
                 for (int j = 0; j < V; ++j) rsc[i][j] = sp[c + j < a.Cin ? c + j : 0];
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             vecT v = Loader<T, VEC>::mask(ra[i], cur_c, a.Cin, ra_ok[i]);
-            if (a.in_scale) {
+            if (SI) {
 #pragma unroll
                 for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * rsc[i][j]);
             }
@@ -299,6 +301,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
                         atomicAdd(a.acc + pix * a.Cout + o, c);
                     } else {
                         float v = c;
+                        if (a.e.dot_out)
+                            atomicAdd(a.e.dot_out + (int64_t)n * a.Cout + o,
+                                      c * (float)((const T*)a.e.dot_src)[pix * a.Cout + o]);
                         if (a.e.on) {
                             v = epi_full<T>(a.e, c, n, o, pix, a.Cout);
                             if (a.e.aux_mode == 1) ((T*)a.e.aux)[pix * a.Cout + o] = (T)c;
@@ -312,63 +317,111 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
         }
         return;
     }
-    // 16-bit: epilogue math in registers, tile transposed through LDS, 16-byte row stores
-    constexpr int OS = BN + 8;
+    // 16-bit: epilogue math in registers, tile transposed through LDS (64 columns at a time, inside
+    // the main loop's LDS budget so occupancy is unchanged), 16-byte row stores
+    constexpr int EH = 64, NHALF = BN / EH, OS = EH + 8, CPR = EH / 8;
     T* ot = lds;                 // [BM][OS]
-    T* xt = lds + BM * OS;       // [BM][OS] aux tile
+    T* xt = lds + BM * OS;       // [BM][OS] aux tile (also holds c for the dot reduction)
+    float* red = (float*)(lds + 2 * BM * OS);   // [EH] dot partial sums
     const bool want_aux = a.e.on && a.e.aux_mode != 0;
+    const bool want_dot = a.e.dot_out != nullptr;
+    const bool keep_c = want_aux || want_dot;
+    // the dot reduction goes through LDS when the whole tile belongs to one sample
+    const int n_first = m0 / per, n_last = (min(m0 + BM, M) - 1) / per;
+    const bool dot_uniform = n_first == n_last;
+    float bj[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int j = 0; j < TN; ++j) {
+        const int o = min(n0 + wn * WN + j * 16 + (lane & 15), a.Cout - 1);
+        bj[j] = (a.e.on && a.e.bias) ? a.e.bias[o] : 0.f;
+    }
+    typedef T vec8o __attribute__((ext_vector_type(8)));
+    const bool cvec = (a.Cout % 8) == 0;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int ml = wm * WM + i * 16 + 4 * (lane >> 4) + r;
-            const int m = min(m0 + ml, M - 1);
+    for (int h = 0; h < NHALF; ++h) {
+        if (h) __syncthreads();                      // the previous half's stores have read the tile
+        if (wn * WN >= h * EH && wn * WN < (h + 1) * EH) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int ml = wm * WM + i * 16 + 4 * (lane >> 4) + r;
+                    const int m = min(m0 + ml, M - 1);
+                    const int n = m / per;
+                    const int rr = m - n * per;
+                    const int oy = (rr / QW) * osy + oy0, ox = (rr % QW) * osx + ox0;
+                    const int64_t pix = ((int64_t)n * a.OH + oy) * a.OW + ox;
+                    const float nv = (a.e.on && a.e.noise) ? (float)((const T*)a.e.noise)[pix] * a.e.noise_gain : 0.f;
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const int ol = wn * WN + j * 16 + (lane & 15);
+                        const int o = min(n0 + ol, a.Cout - 1);
+                        const float c = acc[i][j][r];
+                        float v = c;
+                        if (a.e.on) {
+                            if (a.e.out_scale) v *= a.e.out_scale[(int64_t)n * a.Cout + o];
+                            v += nv + bj[j];
+                            if (a.e.act == 1) v = v > 0.f ? v : v * a.e.alpha;
+                            v *= a.e.gain;
+                            if (a.e.clamp >= 0.f) v = fminf(fmaxf(v, -a.e.clamp), a.e.clamp);
+                        }
+                        ot[ml * OS + ol - h * EH] = (T)v;
+                        if (keep_c) xt[ml * OS + ol - h * EH] = (T)(a.e.aux_mode == 2 ? v : c);
+                    }
+                }
+            }
+        }
+        if (want_dot && tid < EH) red[tid] = 0.f;
+        __syncthreads();
+        float dacc[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dacc[e] = 0.f;
+#pragma unroll
+        for (int k = 0; k < BM * CPR / 256; ++k) {
+            const int idx = tid + k * 256;
+            const int ml = idx / CPR, c8 = (idx % CPR) * 8;
+            const int m = m0 + ml, o = n0 + h * EH + c8;
+            if (m >= M || o >= a.Cout) continue;
+            if (want_dot) {
+                const int n = m / per;
+                const int rr = m - n * per;
+                const int oy = (rr / QW) * osy + oy0, ox = (rr % QW) * osx + ox0;
+                const int64_t src = (((int64_t)n * a.OH + oy) * a.OW + ox) * a.Cout + o;
+                for (int e = 0; e < 8 && o + e < a.Cout; ++e) {
+                    const float pr = (float)xt[ml * OS + c8 + e] * (float)((const T*)a.e.dot_src)[src + e];
+                    if (dot_uniform) dacc[e] += pr;
+                    else atomicAdd(a.e.dot_out + (int64_t)n * a.Cout + o + e, pr);
+                }
+            }
             const int n = m / per;
             const int rr = m - n * per;
             const int oy = (rr / QW) * osy + oy0, ox = (rr % QW) * osx + ox0;
-            const int64_t pix = ((int64_t)n * a.OH + oy) * a.OW + ox;
+            const int64_t dst = (((int64_t)n * a.OH + oy) * a.OW + ox) * a.Cout + o;
+            if (cvec) {
+                vec8o v = *(const vec8o*)(ot + ml * OS + c8);
+                if (a.e.on && a.e.residual) {
+                    const vec8o rv = *(const vec8o*)((const T*)a.e.residual + dst);
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int ol = wn * WN + j * 16 + (lane & 15);
-                const int o = min(n0 + ol, a.Cout - 1);
-                const float c = acc[i][j][r];
-                float v = c;
-                if (a.e.on) v = epi_full<T>(a.e, c, n, o, pix, a.Cout);
-                ot[ml * OS + ol] = (T)v;
-                if (want_aux) xt[ml * OS + ol] = (T)(a.e.aux_mode == 1 ? c : v);
+                    for (int e = 0; e < 8; ++e) v[e] = (T)((float)v[e] + (float)rv[e]);
+                }
+                *(vec8o*)((T*)a.y + dst) = v;
+                if (want_aux) *(vec8o*)((T*)a.e.aux + dst) = *(const vec8o*)(xt + ml * OS + c8);
+            } else {
+                for (int e = 0; e < 8 && o + e < a.Cout; ++e) {
+                    float v = (float)ot[ml * OS + c8 + e];
+                    if (a.e.on && a.e.residual) v += (float)((const T*)a.e.residual)[dst + e];
+                    ((T*)a.y)[dst + e] = (T)v;
+                    if (want_aux) ((T*)a.e.aux)[dst + e] = xt[ml * OS + c8 + e];
+                }
             }
         }
-    }
-    __syncthreads();
-    typedef T vec8o __attribute__((ext_vector_type(8)));
-    const bool cvec = (a.Cout % 8) == 0;
-    constexpr int CPR = BN / 8;                      // 16-byte chunks per tile row
+        if (want_dot && dot_uniform) {
+            const int c8 = (tid % CPR) * 8;
 #pragma unroll
-    for (int k = 0; k < BM * CPR / 256; ++k) {
-        const int idx = tid + k * 256;
-        const int ml = idx / CPR, c8 = (idx % CPR) * 8;
-        const int m = m0 + ml, o = n0 + c8;
-        if (m >= M || o >= a.Cout) continue;
-        const int n = m / per;
-        const int rr = m - n * per;
-        const int oy = (rr / QW) * osy + oy0, ox = (rr % QW) * osx + ox0;
-        const int64_t dst = (((int64_t)n * a.OH + oy) * a.OW + ox) * a.Cout + o;
-        if (cvec) {
-            vec8o v = *(const vec8o*)(ot + ml * OS + c8);
-            if (a.e.on && a.e.residual) {
-                const vec8o rv = *(const vec8o*)((const T*)a.e.residual + dst);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = (T)((float)v[e] + (float)rv[e]);
-            }
-            *(vec8o*)((T*)a.y + dst) = v;
-            if (want_aux) *(vec8o*)((T*)a.e.aux + dst) = *(const vec8o*)(xt + ml * OS + c8);
-        } else {
-            for (int e = 0; e < 8 && o + e < a.Cout; ++e) {
-                float v = (float)ot[ml * OS + c8 + e];
-                if (a.e.on && a.e.residual) v += (float)((const T*)a.e.residual)[dst + e];
-                ((T*)a.y)[dst + e] = (T)v;
-                if (want_aux) ((T*)a.e.aux)[dst + e] = xt[ml * OS + c8 + e];
-            }
+            for (int e = 0; e < 8; ++e) atomicAdd(&red[c8 + e], dacc[e]);
+            __syncthreads();
+            const int o = n0 + h * EH + tid;
+            if (tid < EH && o < a.Cout) atomicAdd(a.e.dot_out + (int64_t)n_first * a.Cout + o, red[tid]);
         }
     }
 }
@@ -379,6 +432,11 @@ __global__ void conv_finalize_kernel(T* y, const float* src, Epi e, int64_t n_el
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_el; i += (int64_t)gridDim.x * blockDim.x) {
         const float c = src[i];
         float v = c;
+        if (e.dot_out) {
+            const int64_t pix = i / Cout;
+            const int o = (int)(i - pix * Cout);
+            atomicAdd(e.dot_out + (pix / pix_per_n) * Cout + o, c * (float)((const T*)e.dot_src)[i]);
+        }
         if (e.on) {
             const int64_t pix = i / Cout;
             const int o = (int)(i - pix * Cout);
@@ -396,13 +454,13 @@ template <typename T, int BM, int BN>
 size_t fwd_lds_bytes() {
     constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
     const size_t main = 2 * (size_t)(BM + BN) * (BK + V) * sizeof(T);
-    const size_t epi = std::is_same<T, float>::value ? 0 : 2 * (size_t)BM * (BN + 8) * sizeof(T);
+    const size_t epi = std::is_same<T, float>::value ? 0 : 2 * (size_t)BM * (64 + 8) * sizeof(T) + 64 * sizeof(float);
     return std::max(main, epi);
 }
 
-template <typename T, int BM, int BN, bool VEC, bool SPLIT>
+template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI>
 int launch_fwd_k(ConvArgs& a, dim3 grid, hipStream_t s) {
-    auto kern = conv_fwd_kernel<T, BM, BN, VEC, SPLIT>;
+    auto kern = conv_fwd_kernel<T, BM, BN, VEC, SPLIT, SI>;
     const size_t lds = fwd_lds_bytes<T, BM, BN>();
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
@@ -420,8 +478,11 @@ int launch_fwd(ConvArgs& a, bool vec, hipStream_t s) {
     for (int i = 0; i < kMaxPhases; ++i)
         if (a.ph[i].M > 0) { maxM = std::max(maxM, a.ph[i].M); nph = i + 1; }
     dim3 grid((unsigned)cdiv(maxM, BM), (unsigned)cdiv(a.Cout, BN), (unsigned)(nph * a.splits));
-    if (a.splits > 1) return vec ? launch_fwd_k<T, BM, BN, true, true>(a, grid, s) : launch_fwd_k<T, BM, BN, false, true>(a, grid, s);
-    return vec ? launch_fwd_k<T, BM, BN, true, false>(a, grid, s) : launch_fwd_k<T, BM, BN, false, false>(a, grid, s);
+#define LF(V_, S_) return a.in_scale ? launch_fwd_k<T, BM, BN, V_, S_, true>(a, grid, s) \
+                                     : launch_fwd_k<T, BM, BN, V_, S_, false>(a, grid, s)
+    if (a.splits > 1) { if (vec) LF(true, true); else LF(false, true); }
+    if (vec) LF(true, false); else LF(false, false);
+#undef LF
 }
 
 // ------------------------------------------------------------------------------------ wgrad
@@ -431,6 +492,7 @@ struct WgradArgs {
     const void* x;   // [N, H, W, B]
     float* dw;       // [A][KK][B]
     const float* b_scale;   // optional [N, B]: x operand multiplied by b_scale[n, b]
+    const float* a_scale;   // optional [N, A]: g operand multiplied by a_scale[n, a]
     int N, A, OH, OW, B, H, W, KH, KW, stride, pady, padx;
     int M;           // N*OH*OW
     int kper;        // pixels per split (multiple of BK)
@@ -476,7 +538,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 
     vecT ra[PA], rb[PB];
     bool ra_ok[PA], rb_ok[PB];
-    float rsc[PB][V];
+    float rsc[PB][V], asc[PA][V];
     auto gload = [&](int p0) {
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
@@ -486,6 +548,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
             ra_ok[i] = ok;
             const T* row = g + (int64_t)(ok ? m : 0) * a.A;
             ra[i] = Loader<T, VEC>::load(row, a0 + ga_col, a.A);
+            if (a.a_scale) {
+                const int n = (ok ? m : 0) / (a.OH * a.OW);
+                const float* sp = a.a_scale + (int64_t)n * a.A;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const int c = a0 + ga_col + j;
+                    asc[i][j] = sp[c < a.A ? c : 0];
+                }
+            }
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
@@ -521,7 +592,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             const int r = ga_row + i * RPA;
-            if (r < BK) *(vecT*)(As + r * LDA + ga_col) = Loader<T, VEC>::mask(ra[i], a0 + ga_col, a.A, ra_ok[i]);
+            vecT v = Loader<T, VEC>::mask(ra[i], a0 + ga_col, a.A, ra_ok[i]);
+            if (a.a_scale) {
+#pragma unroll
+                for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * asc[i][j]);
+            }
+            if (r < BK) *(vecT*)(As + r * LDA + ga_col) = v;
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
@@ -648,6 +724,13 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
         e.out_scale = epi->out_scale; e.noise = epi->noise; e.bias = epi->bias; e.residual = epi->residual;
         e.aux = epi->aux; e.noise_gain = epi->noise_gain; e.alpha = epi->alpha; e.gain = epi->gain;
         e.clamp = epi->clamp; e.act = epi->act; e.aux_mode = epi->aux_mode; e.on = 1;
+        e.dot_src = epi->dot_src; e.dot_out = epi->dot_out;
+        SG2_CHECK((e.dot_src == nullptr) == (e.dot_out == nullptr), "sg2_conv2d: dot_src and dot_out go together");
+        SG2_CHECK(!(e.dot_out && e.aux_mode == 2), "sg2_conv2d: the dot reduction needs aux_mode 0 or 1");
+        if (e.dot_out) {
+            hipError_t er = hipMemsetAsync(e.dot_out, 0, (size_t)N * Cout * sizeof(float), s);
+            if (er != hipSuccess) { set_error("sg2_conv2d: memset failed"); return (int)er; }
+        }
     }
     // Output phases (one for a plain conv; stride^2 for a transposed conv, launched 4 at a time).
     struct PhaseDef { Phase p; int ntaps; Tap taps[kMaxTaps]; };
@@ -750,8 +833,8 @@ extern "C" int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int 
 }
 
 extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
-                                int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* x_scale,
-                                void* stream) {
+                                int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* g_scale,
+                                const float* x_scale, void* stream) {
     using namespace sg2;
     SG2_CHECK(dw && g && x, "sg2_conv2d_wgrad: null pointer");
     SG2_CHECK(N > 0 && A > 0 && B > 0 && OH > 0 && OW > 0 && H > 0 && W > 0, "sg2_conv2d_wgrad: empty shape");
@@ -760,11 +843,11 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     hipError_t e = hipMemsetAsync(dw, 0, (int64_t)A * KH * KW * B * sizeof(float), s);
     if (e != hipSuccess) { set_error("sg2_conv2d_wgrad: memset failed"); return (int)e; }
     WgradArgs a{};
-    a.g = g; a.x = x; a.dw = dw; a.b_scale = x_scale;
+    a.g = g; a.x = x; a.dw = dw; a.b_scale = x_scale; a.a_scale = g_scale;
     a.N = N; a.A = A; a.OH = OH; a.OW = OW; a.B = B; a.H = H; a.W = W; a.KH = KH; a.KW = KW;
     a.stride = stride; a.pady = pad_y; a.padx = pad_x;
     a.M = N * OH * OW;
-    const bool halo = dtype != SG2_F32 && KH == 3 && KW == 3 && stride == 1 && pad_y == 1 && pad_x == 1 &&
+    const bool halo = dtype != SG2_F32 && g_scale == nullptr && KH == 3 && KW == 3 && stride == 1 && pad_y == 1 && pad_x == 1 &&
                       OH == H && OW == W && W >= 16 && A % 8 == 0 && B % 8 == 0 && (uintptr_t)x % 16 == 0 &&
                       (uintptr_t)g % 16 == 0;
     if (halo) return wgrad3x3_launch(dw, g, x, x_scale, dtype, N, A, H, W, B, s);

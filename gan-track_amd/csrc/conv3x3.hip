@@ -174,30 +174,6 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // Epilogue operands are fetched before the main loop so their latency hides behind the MFMAs:
-    // per-lane channel parameters (n is fixed per workgroup) and the 16 noise values of this lane's rows.
-    float dsc[4], bsc[4], nvs[4][4];
-    const T* nz = (const T*)a.noise;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int o = o0 + j * 16 + (lane & 15);
-        const int oc = o < a.Cout ? o : 0;
-        dsc[j] = (EPI && a.out_scale) ? a.out_scale[(int64_t)n * a.Cout + oc] : 1.f;
-        bsc[j] = (EPI && a.bias) ? a.bias[oc] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            nvs[i][r] = 0.f;
-            if (EPI && nz) {
-                const int m = wave * 64 + i * 16 + 4 * (lane >> 4) + r;
-                const int py = m / TW, px = m - py * TW;
-                const int oy = min(ty0 + py, a.H - 1), ox = min(tx0 + px, a.W - 1);
-                nvs[i][r] = (float)nz[((int64_t)n * a.H + oy) * a.W + ox] * a.noise_gain;
-            }
-        }
-
     gload(0);
     sstore(0);
     __syncthreads();
@@ -230,10 +206,21 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
     }
 
     // ---- epilogue: fused math in registers, transpose through LDS, 16-byte row stores ----
+    // per-lane channel parameters (n is fixed per workgroup).  (Fetching these and the noise before
+    // the main loop raised register pressure past two workgroups per CU: measured slower.)
+    float dsc[4], bsc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int o = o0 + j * 16 + (lane & 15);
+        const int oc = o < a.Cout ? o : 0;
+        dsc[j] = (EPI && a.out_scale) ? a.out_scale[(int64_t)n * a.Cout + oc] : 1.f;
+        bsc[j] = (EPI && a.bias) ? a.bias[oc] : 0.f;
+    }
     constexpr int OS = BN + 8;                 // LDS row stride (elements) of the output tile
     T* ot = smem;                              // y tile  [256][OS]
     T* rt = smem + 256 * OS;                   // raw tile [256][OS] (y_raw and/or dot)
     float* red = (float*)(smem + 2 * 256 * OS);   // [BN] dot partial sums
+    const T* nz = (const T*)a.noise;
     const bool want_raw = a.y_raw != nullptr;
     const bool want_dot = a.dot_out != nullptr;
     const bool keep_raw = want_raw || want_dot;
@@ -243,7 +230,12 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int m = wave * 64 + i * 16 + 4 * (lane >> 4) + r;
-            const float nv = nvs[i][r];
+            float nv = 0.f;
+            if (EPI && nz) {
+                const int py = m / TW, px = m - py * TW;
+                const int oy = min(ty0 + py, a.H - 1), ox = min(tx0 + px, a.W - 1);
+                nv = (float)nz[((int64_t)n * a.H + oy) * a.W + ox] * a.noise_gain;
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 float v = acc[i][j][r];

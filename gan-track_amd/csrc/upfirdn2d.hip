@@ -30,6 +30,14 @@ struct UpfParams {
     int upx, upy, downx, downy, padx0, pady0;
     int flip;
     float gain;
+    // fused layer epilogue (nhwc_vec kernel only; include/sg2hip.h sg2_epilogue)
+    const float* out_scale;   // [N, C]
+    const void* noise;        // [N, OH, OW]
+    const float* bias;        // [C]
+    const void* residual;     // like y
+    void* aux;                // like y
+    float noise_gain, alpha, egain, clamp;
+    int act, aux_mode, epi;
 };
 
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
@@ -89,6 +97,39 @@ __global__ __launch_bounds__(256) void upfirdn_generic(UpfParams p) {
 template <typename T> struct VecN { static constexpr int N = 8; };
 template <> struct VecN<float> { static constexpr int N = 4; };
 
+// Shared epilogue of the vectorised kernels: z = clamp(act(c * out_scale + noise * g + bias) * gain),
+// y = round(z) + residual, aux = c or z.
+template <typename T, int V, typename vecT>
+__device__ __forceinline__ void store_out(const UpfParams& p, T* y, const float* acc, int n, int oy, int ox, int cv) {
+    const int64_t dst = n * p.ys_n + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w + cv * V;
+    vecT o;
+    if (p.epi) {
+        const float nv = p.noise ? (float)((const T*)p.noise)[((int64_t)n * p.OH + oy) * p.OW + ox] * p.noise_gain : 0.f;
+        vecT ax, rv;
+        if (p.residual) rv = *(const vecT*)((const T*)p.residual + dst);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int c = cv * V + j;
+            float v = acc[j];
+            if (p.out_scale) v *= p.out_scale[(int64_t)n * p.C + c];
+            v += nv;
+            if (p.bias) v += p.bias[c];
+            if (p.act == 1) v = v > 0.f ? v : v * p.alpha;
+            v *= p.egain;
+            if (p.clamp >= 0.f) v = fminf(fmaxf(v, -p.clamp), p.clamp);
+            ax[j] = (T)(p.aux_mode == 1 ? acc[j] : v);
+            o[j] = (T)v;
+            if (p.residual) o[j] = (T)((float)o[j] + (float)rv[j]);
+        }
+        if (p.aux_mode) *(vecT*)((T*)p.aux + dst) = ax;
+    } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = (T)acc[j];
+    }
+    *(vecT*)(y + dst) = o;
+}
+
+
 // channels-last, C % V == 0, xs_c == ys_c == 1.
 template <typename T>
 __global__ __launch_bounds__(256) void upfirdn_nhwc_vec(UpfParams p) {
@@ -125,15 +166,80 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_vec(UpfParams p) {
                 for (int j = 0; j < V; ++j) acc[j] += (float)v[j] * wt;
             }
         }
-        vecT o;
+        store_out<T, V, vecT>(p, y, acc, n, oy, ox, cv);
+    }
+}
+
+// up = 1, down = DOWN (1 or 2), channels-last: a thread owns one channel vector of one output column
+// and ROWS consecutive output rows, and slides down the input rows it needs, so every input vector it
+// loads feeds all the output rows whose window covers it: (ROWS*DOWN + fh - DOWN) * fw loads per
+// ROWS outputs instead of fh * fw per output.
+template <typename T, int DOWN>
+__global__ __launch_bounds__(256) void upfirdn_nhwc_slide(UpfParams p) {
+    constexpr int V = VecN<T>::N;
+    constexpr int ROWS = 8;
+    typedef T vecT __attribute__((ext_vector_type(V)));
+    __shared__ float sf[kMaxTaps];
+    stage_filter(sf, p);
+    const T* x = (const T*)p.x;
+    T* y = (T*)p.y;
+    const int CV = p.C / V;
+    const int RB = (p.OH + ROWS - 1) / ROWS;
+    const int64_t total = (int64_t)p.N * RB * p.OW * CV;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        int64_t r = idx;
+        const int cv = (int)(r % CV); r /= CV;
+        const int ox = (int)(r % p.OW); r /= p.OW;
+        const int rb = (int)(r % RB); r /= RB;
+        const int n = (int)r;
+        const int oy0 = rb * ROWS;
+        const int nrows = min(ROWS, p.OH - oy0);
+        const T* xb = x + n * p.xs_n + cv * V;
+        float acc[ROWS][V];
 #pragma unroll
-        for (int j = 0; j < V; ++j) o[j] = (T)acc[j];
-        *(vecT*)(y + n * p.ys_n + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w + cv * V) = o;
+        for (int k = 0; k < ROWS; ++k)
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[k][j] = 0.f;
+        const int ix0 = ox * p.downx - p.padx0;
+        const int iy_begin = oy0 * DOWN - p.pady0;
+        const int iy_end = (oy0 + nrows - 1) * DOWN - p.pady0 + p.fh;   // exclusive
+        for (int iy = iy_begin; iy < iy_end; ++iy) {
+            if (iy < 0 || iy >= p.H) continue;
+            const T* xr = xb + iy * p.xs_h;
+            for (int tx = 0; tx < p.fw; ++tx) {
+                const int ix = ix0 + tx;
+                if (ix < 0 || ix >= p.W) continue;
+                const vecT v = *(const vecT*)(xr + ix * p.xs_w);
+                float vf[V];
+#pragma unroll
+                for (int j = 0; j < V; ++j) vf[j] = (float)v[j];
+#pragma unroll
+                for (int k = 0; k < ROWS; ++k) {
+                    const int ty = iy - ((oy0 + k) * DOWN - p.pady0);
+                    if (k < nrows && ty >= 0 && ty < p.fh) {
+                        const float wt = sf[ty * p.fw + tx];
+#pragma unroll
+                        for (int j = 0; j < V; ++j) acc[k][j] += vf[j] * wt;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k)
+            if (k < nrows) store_out<T, V, vecT>(p, y, acc[k], n, oy0 + k, ox, cv);
     }
 }
 
 template <typename T>
 int launch(const UpfParams& p, bool vec, hipStream_t s) {
+    if (vec && p.upx == 1 && p.upy == 1 && (p.downy == 1 || p.downy == 2)) {
+        const int64_t work = (int64_t)p.N * ((p.OH + 7) / 8) * p.OW * (p.C / VecN<T>::N);
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 256 * 32));
+        if (p.downy == 1) upfirdn_nhwc_slide<T, 1><<<grid, 256, 0, s>>>(p);
+        else upfirdn_nhwc_slide<T, 2><<<grid, 256, 0, s>>>(p);
+        return launch_status("sg2_upfirdn2d");
+    }
     const int64_t work = vec ? (int64_t)p.N * p.OH * p.OW * (p.C / VecN<T>::N) : (int64_t)p.N * p.C * p.OH * p.OW;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 256 * 32));
     if (vec)
@@ -146,10 +252,11 @@ int launch(const UpfParams& p, bool vec, hipStream_t s) {
 }  // namespace
 }  // namespace sg2
 
-extern "C" int sg2_upfirdn2d(void* y, const void* x, const float* f, int dtype, const int64_t* in_size,
-                             const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride, int fw,
-                             int fh, int upx, int upy, int downx, int downy, int padx0, int padx1, int pady0,
-                             int pady1, int flip, float gain, void* stream) {
+extern "C" int sg2_upfirdn2d_fused(void* y, const void* x, const float* f, int dtype, const int64_t* in_size,
+                                   const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
+                                   int fw, int fh, int upx, int upy, int downx, int downy, int padx0, int padx1,
+                                   int pady0, int pady1, int flip, float gain, const sg2_epilogue* epi,
+                                   void* stream) {
     using namespace sg2;
     SG2_CHECK(x && y && f && in_size && in_stride && out_size && out_stride, "sg2_upfirdn2d: null argument");
     SG2_CHECK(upx >= 1 && upy >= 1 && downx >= 1 && downy >= 1, "sg2_upfirdn2d: up/down must be >= 1");
@@ -168,6 +275,16 @@ extern "C" int sg2_upfirdn2d(void* y, const void* x, const float* f, int dtype, 
     p.ys_n = out_stride[0]; p.ys_c = out_stride[1]; p.ys_h = out_stride[2]; p.ys_w = out_stride[3];
     p.fw = fw; p.fh = fh; p.upx = upx; p.upy = upy; p.downx = downx; p.downy = downy;
     p.padx0 = padx0; p.pady0 = pady0; p.flip = flip; p.gain = gain;
+    p.out_scale = nullptr; p.noise = nullptr; p.bias = nullptr; p.residual = nullptr; p.aux = nullptr;
+    p.noise_gain = 0.f; p.alpha = 0.f; p.egain = 1.f; p.clamp = -1.f; p.act = 0; p.aux_mode = 0; p.epi = 0;
+    if (epi) {
+        SG2_CHECK(epi->act == 0 || epi->act == 1, "sg2_upfirdn2d: epilogue act must be 0 or 1");
+        SG2_CHECK(epi->aux_mode >= 0 && epi->aux_mode <= 2 && (epi->aux_mode == 0 || epi->aux),
+                  "sg2_upfirdn2d: bad epilogue aux output");
+        p.out_scale = epi->out_scale; p.noise = epi->noise; p.bias = epi->bias; p.residual = epi->residual;
+        p.aux = epi->aux; p.noise_gain = epi->noise_gain; p.alpha = epi->alpha; p.egain = epi->gain;
+        p.clamp = epi->clamp; p.act = epi->act; p.aux_mode = epi->aux_mode; p.epi = 1;
+    }
     if ((int64_t)p.N * p.C * p.OH * p.OW == 0) return 0;
     hipStream_t s = as_stream(stream);
     SG2_DISPATCH(dtype, T, {
@@ -176,7 +293,16 @@ extern "C" int sg2_upfirdn2d(void* y, const void* x, const float* f, int dtype, 
                          ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
                          p.xs_w % V == 0 && p.xs_h % V == 0 && p.xs_n % V == 0 &&
                          p.ys_w % V == 0 && p.ys_h % V == 0 && p.ys_n % V == 0;
+        SG2_CHECK(vec || !p.epi, "sg2_upfirdn2d: the fused epilogue needs NHWC activations with C % 8 == 0");
         return launch<T>(p, vec, s);
     });
     return 0;
+}
+
+extern "C" int sg2_upfirdn2d(void* y, const void* x, const float* f, int dtype, const int64_t* in_size,
+                             const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride, int fw,
+                             int fh, int upx, int upy, int downx, int downy, int padx0, int padx1, int pady0,
+                             int pady1, int flip, float gain, void* stream) {
+    return sg2_upfirdn2d_fused(y, x, f, dtype, in_size, in_stride, out_size, out_stride, fw, fh, upx, upy, downx,
+                               downy, padx0, padx1, pady0, pady1, flip, gain, nullptr, stream);
 }

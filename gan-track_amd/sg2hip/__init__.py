@@ -23,7 +23,8 @@ class Epilogue(ctypes.Structure):
     _fields_ = [('out_scale', ctypes.c_void_p), ('noise', ctypes.c_void_p), ('bias', ctypes.c_void_p),
                 ('residual', ctypes.c_void_p), ('aux', ctypes.c_void_p), ('noise_gain', ctypes.c_float),
                 ('alpha', ctypes.c_float), ('gain', ctypes.c_float), ('clamp', ctypes.c_float),
-                ('act', ctypes.c_int), ('aux_mode', ctypes.c_int)]
+                ('act', ctypes.c_int), ('aux_mode', ctypes.c_int), ('dot_src', ctypes.c_void_p),
+                ('dot_out', ctypes.c_void_p)]
 
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
@@ -41,7 +42,9 @@ SIGNATURES = {
                          ctypes.POINTER(Epilogue), _vp, _i64, _vp],
     'sg2_conv3x3': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _f, _f, _f, _vp, _vp,
                     _vp],
-    'sg2_conv2d_wgrad': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp],
+    'sg2_conv2d_wgrad': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp],
+    'sg2_upfirdn2d_fused': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _i, _i, _i, _i, _i, _i, _i, _i, _i,
+                            _i, _i, _f, ctypes.POINTER(Epilogue), _vp],
     'sg2_layer_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _f, _vp],
     'sg2_grid_sample_fwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp],
     'sg2_grid_sample_bwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp],

@@ -70,38 +70,45 @@ def _conv_raw(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose):
 
 def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_scale=None, out_scale=None,
                noise=None, noise_gain=1.0, bias=None, act=0, alpha=0.2, gain=1.0, clamp=-1.0, residual=None,
-               aux_mode=0):
+               aux_mode=0, dot_src=None):
     """sg2_conv2d_fused: y = round(clamp(act(conv(x * in_scale, w) * out_scale + noise * g + bias) * gain))
-    + residual.  Returns (y, aux) with aux = conv result (aux_mode 1) or activation (aux_mode 2)."""
+    + residual.  Returns (y, aux) with aux = conv result (aux_mode 1) or activation (aux_mode 2); with
+    dot_src also dot[n, o] = sum_p conv(...)[n, o, p] * dot_src[n, o, p] -> (y, aux, dot)."""
     n, cin, h, w = x.shape
     y = torch.empty([n, cout, oh, ow], dtype=x.dtype, device=x.device, memory_format=_CL)
     aux = torch.empty_like(y) if aux_mode else None
     if residual is not None:
         residual = _nhwc(residual)
         assert residual.shape == y.shape and residual.dtype == y.dtype
+    dot = None
+    if dot_src is not None:
+        dot_src = _nhwc(dot_src)
+        assert dot_src.shape == y.shape and dot_src.dtype == y.dtype
+        dot = torch.empty([n, cout], dtype=torch.float32, device=x.device)
     epi = None
-    if any(v is not None for v in (out_scale, noise, bias, residual)) or act != 0 or gain != 1.0 or clamp >= 0 \
-            or aux_mode:
+    if any(v is not None for v in (out_scale, noise, bias, residual, dot_src)) or act != 0 or gain != 1.0 or \
+            clamp >= 0 or aux_mode:
         epi = _hip.Epilogue(_hip.ptr(out_scale), _hip.ptr(noise), _hip.ptr(bias), _hip.ptr(residual), _hip.ptr(aux),
-                            float(noise_gain), float(alpha), float(gain), float(clamp), int(act), int(aux_mode))
+                            float(noise_gain), float(alpha), float(gain), float(clamp), int(act), int(aux_mode),
+                            _hip.ptr(dot_src), _hip.ptr(dot))
     total = n * cout * oh * ow
     ws = torch.empty([total], dtype=torch.float32, device=x.device) if total <= _WS_LIMIT else None
     _hip.check(_hip.lib().sg2_conv2d_fused(
         _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
         stride, pad[0], pad[1], int(transpose), _hip.ptr(in_scale), ctypes.byref(epi) if epi is not None else None,
         _hip.ptr(ws), ws.numel() if ws is not None else 0, _hip.stream_ptr(x.device)), 'sg2_conv2d_fused')
-    return y, aux
+    return (y, aux, dot) if dot_src is not None else (y, aux)
 
 
-def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None):
-    """dw[a, b, ky, kx] = sum g[n,a,oy,ox] x[n,b,oy*s+ky-p,ox*s+kx-p] (* x_scale[n,b]);
+def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None):
+    """dw[a, b, ky, kx] = sum g[n,a,oy,ox] (* g_scale[n,a]) x[n,b,oy*s+ky-p,ox*s+kx-p] (* x_scale[n,b]);
     returns f32 [A,B,kh,kw] (NHWC-packed)."""
     n, a, oh, ow = g.shape
     _, b, h, w = x.shape
     dw = torch.empty([a, kh, kw, b], dtype=torch.float32, device=g.device)
     _hip.check(_hip.lib().sg2_conv2d_wgrad(
         _hip.ptr(dw), _hip.ptr(g), _hip.ptr(x), _hip.dtype_code(g), n, a, oh, ow, b, h, w, kh, kw, stride,
-        pad[0], pad[1], _hip.ptr(x_scale), _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad')
+        pad[0], pad[1], _hip.ptr(g_scale), _hip.ptr(x_scale), _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad')
     return dw.permute(0, 3, 1, 2)
 
 

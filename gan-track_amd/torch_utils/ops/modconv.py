@@ -23,6 +23,7 @@ import torch
 
 from . import bias_act as _ba
 from . import conv2d_gradfix as _cg
+from . import upfirdn2d as _up
 
 _CL = torch.channels_last
 enabled = True         # switch for A/B tests against the composed (unfused) path
@@ -131,10 +132,12 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
             else:
                 dx, _ = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32)
         else:
-            dx, craw = _cg.conv_fused(dc, _cg._pack_convT(weight.to(dt)), cin, h, w, kh, kw, stride, (pad, pad),
-                                      transpose=True, out_scale=s32, aux_mode=1 if want_ds else 0)
             if want_ds:
-                ds = (craw.float() * x.float()).sum([2, 3])
+                dx, _, ds = _cg.conv_fused(dc, _cg._pack_convT(weight.to(dt)), cin, h, w, kh, kw, stride, (pad, pad),
+                                           transpose=True, out_scale=s32, dot_src=x)
+            else:
+                dx, _ = _cg.conv_fused(dc, _cg._pack_convT(weight.to(dt)), cin, h, w, kh, kw, stride, (pad, pad),
+                                       transpose=True, out_scale=s32)
         ds = ds.to(styles.dtype) if want_ds else None
         dx = dx if need[0] else None
     if need[2] and not _cg.weight_gradients_disabled:
@@ -189,3 +192,111 @@ def modconv_layer(x, styles, weight, dcoefs, noise, bias, alpha, gain, clamp):
     discriminator's plain 3x3 Conv2dLayer + bias + lrelu (networks_stylegan2.py:172-181)."""
     return fused_conv(x, weight, styles=styles, dcoefs=dcoefs, noise=noise, bias=bias, padding=1, act='lrelu',
                       alpha=alpha, gain=gain, clamp=clamp)
+
+
+# ---------------------------------------------------------------------------------------------- up-2
+def _up_geometry(h, w, kh, kw, f):
+    """Padding algebra of conv2d_resample's transposed plan (conv2d_resample.py:112-129) for a
+    padding-1 / up-2 layer: transposed-conv padding, its output size and the FIR padding."""
+    from . import conv2d_resample as _cr
+    x0, x1, y0, y1 = _cr._frame_padding(kw // 2, f, 2, 1)
+    x0, x1 = x0 - (kw - 1), x1 - (kw - 2)
+    y0, y1 = y0 - (kh - 1), y1 - (kh - 2)
+    cx = max(-max(x0, x1), 0)
+    cy = max(-max(y0, y1), 0)
+    th, tw = (h - 1) * 2 - 2 * cy + kh, (w - 1) * 2 - 2 * cx + kw
+    return (cy, cx), (th, tw), [x0 + cx, x1 + cx, y0 + cy, y1 + cy]
+
+
+def supported_up(x, weight, f):
+    n, cin, h, w = x.shape
+    cout = weight.shape[0]
+    vec = 8 if x.dtype != torch.float32 else 4
+    return enabled and x.is_cuda and f is not None and f.ndim == 2 and cout % vec == 0 and cout % 8 == 0
+
+
+class UpModConv(torch.autograd.Function):
+    """Up-2 synthesis layer (networks_stylegan2.py:309-328; modulated_conv2d :66-76 with
+    conv2d_resample's transposed plan :112-129):
+        t = conv_transpose2d(x * s, W^T, stride 2)     modulation folded into the conv's operand staging
+        c = FIR(t) * 4                                 4x4 [1,3,3,1] filter
+        y = clamp(lrelu(c * d + noise + b) * gain)     epilogue of the FIR kernel
+    Two launches where the reference runs x*s, conv_transpose2d, upfirdn2d, fma and bias_act."""
+
+    @staticmethod
+    def forward(ctx, x, styles, weight, dcoefs, noise, bias, f, alpha, gain, clamp):
+        x = _cg._nhwc(x)
+        n, cin, h, w = x.shape
+        cout, _, kh, kw = weight.shape
+        dt = x.dtype
+        tpad, (th, tw), fpad = _up_geometry(h, w, kh, kw, f)
+        t, _ = _cg.conv_fused(x, _cg._pack_conv(weight.to(dt)), cout, th, tw, kh, kw, 2, tpad, transpose=True,
+                              in_scale=_f32(styles))
+        oh, ow = th + fpad[2] + fpad[3] - f.shape[0] + 1, tw + fpad[0] + fpad[1] - f.shape[1] + 1
+        nz = noise.to(dt).reshape(n, oh, ow).contiguous() if noise is not None else None
+        want_c = any(ctx.needs_input_grad[:6]) and dcoefs is not None
+        b32 = _f32(bias.to(dt)) if bias is not None else None
+        y, c = _up.fir_fused(t, f, fpad, gain=4.0, out_scale=_f32(dcoefs), noise=nz, bias=b32, act=1, alpha=alpha,
+                             act_gain=gain, clamp=clamp, aux_mode=1 if want_c else 0)
+        ctx.save_for_backward(x, styles, weight, dcoefs, noise, bias, f, y, c)
+        ctx.cfg = (alpha, gain, clamp, tpad, (th, tw), fpad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, styles, weight, dcoefs, noise, bias, f, y, c = ctx.saved_tensors
+        alpha, gain, clamp, tpad, (th, tw), fpad = ctx.cfg
+        need = ctx.needs_input_grad
+        n, cin, h, w = x.shape
+        cout, _, kh, kw = weight.shape
+        dt = x.dtype
+        oh, ow = y.shape[2], y.shape[3]
+        aup, adown, apad, aflip = _up.adjoint_params(f, (th, tw), (oh, ow), 1, 1, fpad, False)
+        wt = weight.to(dt).transpose(0, 1)                    # conv_transpose2d weight [Cin, Cout, kh, kw]
+        dx = ds = dw = dd = dn = db = None
+        if not torch.is_grad_enabled() and fast_backward:
+            d32, s32 = _f32(dcoefs), _f32(styles)
+            want_dd = need[3] and d32 is not None
+            dc, db, dd, dn = _cg.layer_bwd(dy.to(dt), y, c if want_dd else None, d32, act=1, alpha=alpha, gain=gain,
+                                           clamp=clamp, want_db=need[5] and bias is not None, want_dd=want_dd,
+                                           want_dnoise=need[4] and noise is not None)
+            dt_ = _up.upfirdn2d(dc, f, up=aup, down=adown, padding=apad, flip_filter=aflip, gain=4)
+            if need[0] or need[1]:
+                if need[1]:
+                    dx, _, ds = _cg.conv_fused(dt_, _cg._pack_conv(wt), cin, h, w, kh, kw, 2, tpad, out_scale=s32,
+                                               dot_src=x)
+                else:
+                    dx, _ = _cg.conv_fused(dt_, _cg._pack_conv(wt), cin, h, w, kh, kw, 2, tpad, out_scale=s32)
+                dx = dx if need[0] else None
+            if need[2] and not _cg.weight_gradients_disabled:
+                dw = _cg._wgrad_raw(x, dt_, kh, kw, 2, tpad, g_scale=s32).transpose(0, 1).to(weight.dtype)
+        else:
+            dz = _ba.bias_act_grad(dy, y, act='lrelu', alpha=alpha, gain=gain, clamp=clamp)
+            if need[5] and bias is not None:
+                db = dz.sum([0, 2, 3], dtype=torch.float32)
+            if need[4] and noise is not None:
+                dn = dz.sum(1, keepdim=True, dtype=torch.float32)
+            s_ = styles.to(dt).reshape(n, -1, 1, 1)
+            xs = x * s_
+            if need[3] and dcoefs is not None:
+                t_ = _cg._ConvT2d.apply(xs, wt, 2, tpad, (th, tw))
+                c_ = _up.upfirdn2d(t_, f, padding=fpad, gain=4)
+                dd = (dz * c_).sum([2, 3], dtype=torch.float32)
+            dc = dz * dcoefs.to(dt).reshape(n, -1, 1, 1)
+            dt_ = _up.upfirdn2d(dc, f, up=aup, down=adown, padding=apad, flip_filter=aflip, gain=4)
+            if need[0] or need[1]:
+                dxs = _cg._Conv2d.apply(dt_, wt, 2, tpad, (h, w))
+                if need[0]:
+                    dx = dxs * s_
+                if need[1]:
+                    ds = (dxs * x).sum([2, 3], dtype=torch.float32)
+            if need[2] and not _cg.weight_gradients_disabled:
+                dw = _cg._WGrad.apply(xs, dt_, (kh, kw), 2, tpad).transpose(0, 1)
+        cast = lambda g, ref: g.to(ref.dtype) if (g is not None and ref is not None) else g
+        return (dx, cast(ds, styles), cast(dw, weight), cast(dd, dcoefs), cast(dn, noise), cast(db, bias),
+                None, None, None, None)
+
+
+def up_modconv_layer(x, styles, weight, dcoefs, noise, bias, f, alpha, gain, clamp):
+    return UpModConv.apply(x, styles, weight, dcoefs, noise, bias, f, float(alpha), float(gain),
+                           float(clamp if clamp is not None else -1.0))

@@ -6,6 +6,8 @@ of any order w.r.t. x (the op is linear; its adjoint is again an upfirdn2d with 
 and the filter flipped, reference :250-269).  Separable (1-D) filters run as a horizontal then a
 vertical pass, like the reference plugin (:243-245).
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -79,6 +81,38 @@ def _raw(x, f2, upx, upy, downx, downy, px0, px1, py0, py1, flip, gain):
     return y
 
 
+def fir_fused(x, f2, padding, gain=1.0, flip_filter=False, out_scale=None, noise=None, noise_gain=1.0, bias=None,
+              act=0, alpha=0.2, act_gain=1.0, clamp=-1.0, aux_mode=0):
+    """2-D FIR (up = down = 1) with the fused layer epilogue (sg2_upfirdn2d_fused):
+    c = FIR(x) * gain;  y = clamp(act(c * out_scale[n,c] + noise * g + bias) * act_gain).
+    x NHWC (channels_last) with C % 8 == 0.  Returns (y, aux) with aux = c (aux_mode 1) / y (2)."""
+    px0, px1, py0, py1 = _parse_padding(padding)
+    n, c, h, w = x.shape
+    fh, fw = f2.shape
+    oh, ow = h + py0 + py1 - fh + 1, w + px0 + px1 - fw + 1
+    y = torch.empty([n, c, oh, ow], dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    aux = torch.empty_like(y) if aux_mode else None
+    epi = _hip.Epilogue(_hip.ptr(out_scale), _hip.ptr(noise), _hip.ptr(bias), None, _hip.ptr(aux), float(noise_gain),
+                        float(alpha), float(act_gain), float(clamp), int(act), int(aux_mode))
+    _hip.check(_hip.lib().sg2_upfirdn2d_fused(
+        _hip.ptr(y), _hip.ptr(x), _hip.ptr(f2), _hip.dtype_code(x), _hip.i64arr(x.shape), _hip.i64arr(x.stride()),
+        _hip.i64arr(y.shape), _hip.i64arr(y.stride()), fw, fh, 1, 1, 1, 1, px0, px1, py0, py1, int(bool(flip_filter)),
+        float(gain), ctypes.byref(epi), _hip.stream_ptr(x.device)), 'sg2_upfirdn2d_fused')
+    return y, aux
+
+
+def adjoint_params(f, x_hw, y_hw, up, down, padding, flip_filter):
+    """(up, down, padding, flip) of the adjoint upfirdn2d (reference upfirdn2d.py:250-269)."""
+    upx, upy = _parse_scaling(up)
+    downx, downy = _parse_scaling(down)
+    px0, px1, py0, py1 = _parse_padding(padding)
+    fw, fh = _get_filter_size(f)
+    ih, iw = x_hw
+    oh, ow = y_hw
+    p = [fw - px0 - 1, iw * upx - ow * downx + px0 - upx + 1, fh - py0 - 1, ih * upy - oh * downy + py0 - upy + 1]
+    return [downx, downy], [upx, upy], p, not flip_filter
+
+
 _cache = {}
 
 
@@ -113,14 +147,12 @@ def _upfirdn2d_fn(up=1, down=1, padding=0, flip_filter=False, gain=1):
             f, = ctx.saved_tensors
             _, _, ih, iw = ctx.x_shape
             _, _, oh, ow = dy.shape
-            fw, fh = _get_filter_size(f)
             # adjoint: upsample by `down`, filter with the flipped taps, decimate by `up`
-            p = [fw - px0 - 1, iw * upx - ow * downx + px0 - upx + 1,
-                 fh - py0 - 1, ih * upy - oh * downy + py0 - upy + 1]
+            aup, adown, p, aflip = adjoint_params(f, (ih, iw), (oh, ow), [upx, upy], [downx, downy],
+                                                  [px0, px1, py0, py1], flip_filter)
             dx = None
             if ctx.needs_input_grad[0]:
-                dx = _upfirdn2d_fn(up=[downx, downy], down=[upx, upy], padding=p, flip_filter=(not flip_filter),
-                                   gain=gain).apply(dy, f)
+                dx = _upfirdn2d_fn(up=aup, down=adown, padding=p, flip_filter=aflip, gain=gain).apply(dy, f)
             assert not ctx.needs_input_grad[1]
             return dx, None
 

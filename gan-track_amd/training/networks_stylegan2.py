@@ -226,7 +226,8 @@ class SynthesisLayer(torch.nn.Module):
             noise = torch.randn([x.shape[0], 1, self.resolution, self.resolution], device=x.device) * self.noise_strength
         if self.use_noise and noise_mode == 'const':
             noise = self.noise_const * self.noise_strength
-        if self.activation == 'lrelu' and self.up == 1 and modconv.supported_generic(x, self.weight):
+        up_fused = self.up == 2 and modconv.supported_up(x, self.weight, self.resample_filter)
+        if self.activation == 'lrelu' and (up_fused or (self.up == 1 and modconv.supported_generic(x, self.weight))):
             # one-kernel modulated conv + demod + noise + bias + lrelu + clamp (sg2_conv3x3 / sg2_conv2d_fused)
             weight = self.weight
             if x.dtype == torch.float16:   # fp16 range pre-normalisation (:52-54)
@@ -236,6 +237,11 @@ class SynthesisLayer(torch.nn.Module):
             if noise is not None and noise.ndim == 2:
                 noise = noise.reshape(1, 1, *noise.shape).expand(x.shape[0], 1, -1, -1)
             clamp = self.conv_clamp * gain if self.conv_clamp is not None else None
+            if up_fused:
+                return modconv.up_modconv_layer(x, styles, weight, _demod(weight, styles), noise, self.bias,
+                                                self.resample_filter,
+                                                alpha=bias_act.activation_funcs[self.activation].def_alpha,
+                                                gain=self.act_gain * gain, clamp=clamp)
             return modconv.modconv_layer(x, styles, weight, _demod(weight, styles), noise, self.bias,
                                          alpha=bias_act.activation_funcs[self.activation].def_alpha,
                                          gain=self.act_gain * gain, clamp=clamp)

@@ -71,6 +71,16 @@ int sg2_upfirdn2d(void* y, const void* x, const float* f, int dtype, const int64
                   int upx, int upy, int downx, int downy, int padx0, int padx1, int pady0, int pady1, int flip,
                   float gain, void* stream);
 
+/* sg2_upfirdn2d followed by the fused layer epilogue (sg2_epilogue, defined below) -- the FIR of
+ * an up-2 synthesis layer with its demodulation, noise, bias, lrelu and clamp
+ * (networks_stylegan2.py:68-76 + :325-327).  epi may be NULL; with an epilogue the activations
+ * must be NHWC with C % 8 == 0 (C % 4 for f32). */
+typedef struct sg2_epilogue sg2_epilogue;
+int sg2_upfirdn2d_fused(void* y, const void* x, const float* f, int dtype, const int64_t* in_size,
+                        const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride, int fw, int fh,
+                        int upx, int upy, int downx, int downy, int padx0, int padx1, int pady0, int pady1, int flip,
+                        float gain, const sg2_epilogue* epi, void* stream);
+
 /* Dense 2-D convolution on NHWC activations (implicit GEMM on MFMA).
  *   transpose = 0: y = conv2d(x, w, stride, padding)            (torch.nn.functional.conv2d)
  *                  w packed [Cout][KH][KW][Cin]  (= OIHW weight in channels_last memory)
@@ -86,9 +96,10 @@ int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int N, int Cin,
  *   z   = clamp(act(c * out_scale[n,o] + noise[n,oy,ox] * noise_gain + bias[o]) * gain, +-clamp)
  *   y   = round(z) + residual[n,oy,ox,o]          (residual: the resnet skip of the D block)
  *   aux = c (aux_mode 1) or z (aux_mode 2)        (saved for the fused backward)
+ *   dot_out[n,o] = sum_{oy,ox} c * dot_src        (the modulation gradient when the call is a dgrad)
  * Replaces the fma / bias_act / add passes the reference runs after each conv
  * (networks_stylegan2.py:68-76, :172-181, :621-627). */
-typedef struct sg2_epilogue {
+struct sg2_epilogue {
     const float* out_scale;  /* [N, Cout] float32 */
     const void* noise;       /* [N, OH, OW], activation dtype */
     const float* bias;       /* [Cout] float32 */
@@ -97,7 +108,9 @@ typedef struct sg2_epilogue {
     float noise_gain, alpha, gain, clamp;   /* clamp < 0: off */
     int act;                 /* 0 linear, 1 lrelu(alpha) */
     int aux_mode;            /* 0 none, 1 conv result c, 2 activation z */
-} sg2_epilogue;
+    const void* dot_src;     /* [N, OH, OW, Cout] or NULL (sg2_conv2d_fused only; needs aux_mode 0 or 1) */
+    float* dot_out;          /* [N, Cout] float32: sum over pixels of c * dot_src, zeroed by the call */
+};
 
 /* sg2_conv2d with the A operand modulated by in_scale[n, ci] (float32 [N, Cin], or NULL) and the
  * fused epilogue above (epi may be NULL = plain convolution).  Transposed convolutions run all their
@@ -122,13 +135,13 @@ int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, int dtype, i
                 float* dot_out, void* stream);
 
 /* Weight gradient of sg2_conv2d (transpose = 0 form):
- *   dw[a][ky][kx][b] = sum_{n,oy,ox} g[n,oy,ox,a] * x[n, oy*stride+ky-pad_y, ox*stride+kx-pad_x, b] * s[n,b]
- *   s = x_scale [N, B] float32 (the layer's modulation), or NULL for 1.
+ *   dw[a][ky][kx][b] = sum_{n,oy,ox} g[n,oy,ox,a] * u[n,a] * x[n, oy*stride+ky-pad_y, ox*stride+kx-pad_x, b] * s[n,b]
+ *   u = g_scale [N, A], s = x_scale [N, B] float32 (a layer's modulation), or NULL for 1.
  *   g [N, OH, OW, A] NHWC, x [N, H, W, B] NHWC; dw is float32 [A][KH][KW][B], overwritten.
  *   The conv_transpose2d weight gradient is the same call with (g, x) = (x_of_convT, dy). */
 int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
-                     int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* x_scale,
-                     void* stream);
+                     int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* g_scale,
+                     const float* x_scale, void* stream);
 
 /* Fused first-order backward of the layer epilogue z = c*d + noise + b, y = clamp(act(z)*gain):
  *   dc = dz * d;  db[o] = sum dz;  dd[n,o] = sum_p dz*c;  dnoise[n,p] = sum_o dz

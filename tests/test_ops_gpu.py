@@ -498,3 +498,141 @@ def test_wgrad3x3_halo(dtype, shape, scaled):
     xs = (x.float() * s[:, :, None, None]).to(dtype) if scaled else x
     ref = torch.nn.grad.conv2d_weight(xs.double(), [A, B, 3, 3], g.double(), padding=1)
     assert rel_err(dw, ref) < (2e-3 if dtype == torch.float16 else 1e-2)
+
+
+def _layer_grads(fwd, params, x0, dy, second_order):
+    """Output, first-order grads (input + params) and, optionally, PL-style second-order grads."""
+    x = x0.clone().requires_grad_(True)
+    y = fwd(x)
+    out = [y.float()]
+    if second_order:
+        gx, = torch.autograd.grad((y.float() * dy).sum(), [x], create_graph=True)
+        g2 = torch.autograd.grad(gx.float().square().sum(), params, allow_unused=True)
+        # a parameter outside the second-order graph (e.g. a bias under lrelu) has a zero gradient
+        out += [(g if g is not None else torch.zeros_like(p_)).float() for g, p_ in zip(g2, params)]
+        x = x0.clone().requires_grad_(True)
+        y = fwd(x)
+    out += [g.float() for g in torch.autograd.grad((y.float() * dy).sum(), [x] + params)]
+    return out
+
+
+def _fused_vs_composed(fwd, params, x0, dy, dtype, second_order=True, fwd32=None):
+    """Fused vs composed path.  For 16-bit layers both are also compared with the composed path run in
+    f32 (fwd32, or fwd on x0.float()): sums with heavy cancellation (e.g. the noise-strength gradient)
+    carry the 16-bit rounding of the composed path, so the fused path must be within tolerance of the
+    composed one OR no further from the f32 result than the composed path is."""
+    from torch_utils.ops import modconv
+    res = []
+    for fused in [True, False]:
+        modconv.enabled = fused
+        try:
+            res.append(_layer_grads(fwd, params, x0, dy, second_order))
+        finally:
+            modconv.enabled = True
+    tol = {torch.float32: 1e-4, torch.float16: 1e-2, torch.bfloat16: 4e-2}[dtype]
+    ref = None
+    if dtype != torch.float32:
+        modconv.enabled = False
+        try:
+            ref = _layer_grads(fwd32 or fwd, params, x0.float(), dy, second_order)
+        finally:
+            modconv.enabled = True
+    assert len(res[0]) == len(res[1])
+    for k, (a_, b_) in enumerate(zip(*res)):
+        t = tol if k == 0 else 2 * tol
+        if ref is None:
+            assert rel_err(a_, b_) < t, k
+        else:
+            assert rel_err(a_, b_) < t or rel_err(a_, ref[k]) <= 1.25 * rel_err(b_, ref[k]) + 1e-3, k
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
+def test_fused_up_synthesis_layer(dtype):
+    """Up-2 SynthesisLayer: conv_transpose with the modulation in its operand staging + FIR with the
+    demod/noise/bias/lrelu/clamp epilogue (UpModConv) vs the composed reference path."""
+    from training import networks_stylegan2 as net
+    torch.manual_seed(17)
+    layer = net.SynthesisLayer(32, 48, w_dim=16, resolution=32, up=2, conv_clamp=256).to(DEV)
+    with torch.no_grad():
+        layer.noise_strength.fill_(0.3)
+        layer.bias.copy_(torch.randn(48) * 0.2)
+    x0 = torch.randn(4, 32, 16, 16, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    wv = torch.randn(4, 16, device=DEV)
+    dy = 0.1 * (torch.randn(4, 48, 32, 32, device=DEV) + 0.5)   # positive-mean dy and |noise|: the noise-strength
+    params = [layer.weight, layer.bias, layer.noise_strength, layer.affine.weight]   # gradient is then
+    noise = torch.randn(4, 1, 32, 32, device=DEV).abs()    # well conditioned
+
+    def fwd(x):
+        orig = torch.randn
+        torch.randn = lambda *a, **k: noise.clone()
+        try:
+            return layer(x, wv)
+        finally:
+            torch.randn = orig
+    _fused_vs_composed(fwd, params, x0, dy, dtype)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
+def test_fused_discriminator_block(dtype):
+    """Resnet DiscriminatorBlock: skip (FIR-down + 1x1, gain epilogue), conv0 and conv1 (FIR + stride-2
+    conv with bias/lrelu/clamp epilogue and the skip added in the epilogue) vs the composed path."""
+    from training import networks_stylegan2 as net
+    torch.manual_seed(19)
+    blk = net.DiscriminatorBlock(32, 32, 64, resolution=32, img_channels=1, first_layer_idx=0, conv_clamp=256,
+                                 use_fp16=(dtype != torch.float32), fp16_dtype=dtype if dtype != torch.float32 else torch.float16).to(DEV)
+    with torch.no_grad():
+        for m in [blk.conv0, blk.conv1]:
+            m.bias.copy_(torch.randn_like(m.bias) * 0.2)
+    x0 = torch.randn(4, 32, 32, 32, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(4, 64, 16, 16, device=DEV)
+    params = [blk.conv0.weight, blk.conv1.weight, blk.conv1.bias, blk.skip.weight]
+    _fused_vs_composed(lambda x: blk(x, None)[0], params, x0, dy, dtype,
+                       fwd32=lambda x: blk(x, None, force_fp32=True)[0])
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16])
+def test_fused_torgb_and_f32_layer(dtype):
+    from training import networks_stylegan2 as net
+    torch.manual_seed(23)
+    torgb = net.ToRGBLayer(32, 1, w_dim=16, conv_clamp=256).to(DEV)
+    with torch.no_grad():
+        torgb.bias.fill_(0.1)
+    x0 = torch.randn(4, 32, 16, 16, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    wv = torch.randn(4, 16, device=DEV)
+    dy = torch.randn(4, 1, 16, 16, device=DEV)
+    _fused_vs_composed(lambda x: torgb(x, wv), [torgb.weight, torgb.bias, torgb.affine.weight], x0, dy, dtype)
+    layer = net.SynthesisLayer(32, 32, w_dim=16, resolution=8, conv_clamp=256).to(DEV)
+    with torch.no_grad():
+        layer.noise_strength.fill_(0.3)
+    x1 = torch.randn(4, 32, 8, 8, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    dy1 = torch.randn(4, 32, 8, 8, device=DEV)
+    _fused_vs_composed(lambda x: layer(x, wv, noise_mode='const'), [layer.weight, layer.bias, layer.noise_strength,
+                                                                    layer.affine.weight], x1, dy1, dtype)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16])
+@pytest.mark.parametrize('geom', [(3, 2, 0, True), (3, 2, 0, False), (3, 1, 1, False), (1, 1, 0, False)])
+def test_conv_fused_dot_and_scale(dtype, geom):
+    """sg2_conv2d_fused: out_scale epilogue + per-(n, o) dot reduction against dot_src (the modulation
+    gradient of a dgrad), for plain / strided / transposed geometries."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    k, stride, pad, transpose = geom
+    torch.manual_seed(29)
+    N, Cin, Cout, H, W = 3, 32, 48, 12, 10
+    x = torch.randn(N, Cin, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    if transpose:
+        w = (torch.randn(Cin, Cout, k, k, device=DEV) / (Cin * k * k) ** 0.5).to(dtype)
+        ref = F.conv_transpose2d(x.double(), w.double(), stride=stride, padding=pad)
+        wp = cg._pack_convT(w)
+    else:
+        w = (torch.randn(Cout, Cin, k, k, device=DEV) / (Cin * k * k) ** 0.5).to(dtype)
+        ref = F.conv2d(x.double(), w.double(), stride=stride, padding=pad)
+        wp = cg._pack_conv(w)
+    oh, ow = ref.shape[2], ref.shape[3]
+    s = torch.rand(N, Cout, device=DEV) + 0.5
+    src = torch.randn(N, Cout, oh, ow, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    y, _, dot = cg.conv_fused(x, wp, Cout, oh, ow, k, k, stride, (pad, pad), transpose=transpose, out_scale=s,
+                              dot_src=src)
+    tol = 1e-5 if dtype == torch.float32 else 5e-3
+    assert rel_err(y.float(), ref * s.double()[:, :, None, None]) < tol
+    assert rel_err(dot, (ref.to(dtype).double() * src.double()).sum([2, 3])) < (1e-5 if dtype == torch.float32 else 5e-3)
