@@ -170,75 +170,96 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_vec(UpfParams p) {
     }
 }
 
-// up = 1, down = DOWN (1 or 2), channels-last: a thread owns one channel vector of one output column
-// and ROWS consecutive output rows, and slides down the input rows it needs, so every input vector it
-// loads feeds all the output rows whose window covers it: (ROWS*DOWN + fh - DOWN) * fw loads per
-// ROWS outputs instead of fh * fw per output.
-template <typename T, int DOWN>
-__global__ __launch_bounds__(256) void upfirdn_nhwc_slide(UpfParams p) {
+// 4x4 filter, up = 1, down = DOWN (1 or 2) on both axes, channels-last: the resample filter of every
+// G/D layer.  A workgroup owns a TW x TH output tile x CG channel vectors: it stages the
+// ((TH-1)*DOWN + 4) x ((TW-1)*DOWN + 4) input patch once in LDS with coalesced loads (CG consecutive
+// lanes = one pixel's CG*16 bytes; ~1.4 global loads per output vector at DOWN 1 instead of 16 L1
+// requests), then each lane reads its 16 taps back with conflict-free ds_read_b128.  CG = 4 keeps the
+// patch at 25 KB (DOWN 1, 32 x 8) / 39 KB (DOWN 2, 16 x 8) so several workgroups share a CU.
+template <typename T, int DOWN, int TW, int TH, int CG>
+__global__ __launch_bounds__(256) void upfirdn_nhwc_f4(UpfParams p) {
     constexpr int V = VecN<T>::N;
-    constexpr int ROWS = 8;
+    constexpr int F = 4;                              // CG channel vectors per workgroup
+    constexpr int IW = (TW - 1) * DOWN + F, IH = (TH - 1) * DOWN + F, NIN = IW * IH * CG;
     typedef T vecT __attribute__((ext_vector_type(V)));
-    __shared__ float sf[kMaxTaps];
-    stage_filter(sf, p);
-    const T* x = (const T*)p.x;
-    T* y = (T*)p.y;
+    __shared__ float sf[F * F];
+    extern __shared__ __attribute__((aligned(16))) char tile_raw[];
+    vecT* tile = (vecT*)tile_raw;                     // [IH][IW][CG]
+    const int tid = threadIdx.x;
+    if (tid < F * F) {
+        const int ty = tid / F, tx = tid % F;
+        sf[tid] = p.f[(p.flip ? ty : F - 1 - ty) * F + (p.flip ? tx : F - 1 - tx)] * p.gain;
+    }
     const int CV = p.C / V;
-    const int RB = (p.OH + ROWS - 1) / ROWS;
-    const int64_t total = (int64_t)p.N * RB * p.OW * CV;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        int64_t r = idx;
-        const int cv = (int)(r % CV); r /= CV;
-        const int ox = (int)(r % p.OW); r /= p.OW;
-        const int rb = (int)(r % RB); r /= RB;
-        const int n = (int)r;
-        const int oy0 = rb * ROWS;
-        const int nrows = min(ROWS, p.OH - oy0);
-        const T* xb = x + n * p.xs_n + cv * V;
-        float acc[ROWS][V];
+    const int ngroups = (CV + CG - 1) / CG;
+    const int tiles_x = (p.OW + TW - 1) / TW, tiles_y = (p.OH + TH - 1) / TH;
+    int64_t b = blockIdx.x;
+    const int cg = (int)(b % ngroups); b /= ngroups;
+    const int tx0 = (int)(b % tiles_x) * TW; b /= tiles_x;
+    const int ty0 = (int)(b % tiles_y) * TH; b /= tiles_y;
+    const int n = (int)b;
+    const int cv0 = cg * CG;
+    const T* xb = (const T*)p.x + n * p.xs_n;
+    const int iy0 = ty0 * DOWN - p.pady0, ix0 = tx0 * DOWN - p.padx0;
+    for (int i = tid; i < NIN; i += 256) {
+        const int c = i % CG, px = i / CG;
+        const int ry = px / IW, rx = px - ry * IW;
+        const int iy = iy0 + ry, ix = ix0 + rx;
+        const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W && cv0 + c < CV;
+        vecT v = *(const vecT*)(xb + (int64_t)(ok ? iy : 0) * p.xs_h + (int64_t)(ok ? ix : 0) * p.xs_w +
+                                (ok ? cv0 + c : 0) * V);
 #pragma unroll
-        for (int k = 0; k < ROWS; ++k)
+        for (int j = 0; j < V; ++j) v[j] = ok ? v[j] : (T)0.f;
+        tile[i] = v;
+    }
+    __syncthreads();
+    const int c = tid % CG;
+    if (cv0 + c >= CV) return;
 #pragma unroll
-            for (int j = 0; j < V; ++j) acc[k][j] = 0.f;
-        const int ix0 = ox * p.downx - p.padx0;
-        const int iy_begin = oy0 * DOWN - p.pady0;
-        const int iy_end = (oy0 + nrows - 1) * DOWN - p.pady0 + p.fh;   // exclusive
-        for (int iy = iy_begin; iy < iy_end; ++iy) {
-            if (iy < 0 || iy >= p.H) continue;
-            const T* xr = xb + iy * p.xs_h;
-            for (int tx = 0; tx < p.fw; ++tx) {
-                const int ix = ix0 + tx;
-                if (ix < 0 || ix >= p.W) continue;
-                const vecT v = *(const vecT*)(xr + ix * p.xs_w);
-                float vf[V];
+    for (int pass = 0; pass < TW * TH * CG / 256; ++pass) {
+        const int pix = tid / CG + pass * (256 / CG);
+        const int oy = ty0 + pix / TW, ox = tx0 + pix % TW;
+        if (oy >= p.OH || ox >= p.OW) continue;
+        float acc[V];
 #pragma unroll
-                for (int j = 0; j < V; ++j) vf[j] = (float)v[j];
+        for (int j = 0; j < V; ++j) acc[j] = 0.f;
+        const vecT* base = tile + ((pix / TW) * DOWN * IW + (pix % TW) * DOWN) * CG + c;
 #pragma unroll
-                for (int k = 0; k < ROWS; ++k) {
-                    const int ty = iy - ((oy0 + k) * DOWN - p.pady0);
-                    if (k < nrows && ty >= 0 && ty < p.fh) {
-                        const float wt = sf[ty * p.fw + tx];
+        for (int ky = 0; ky < F; ++ky)
 #pragma unroll
-                        for (int j = 0; j < V; ++j) acc[k][j] += vf[j] * wt;
-                    }
-                }
+            for (int kx = 0; kx < F; ++kx) {
+                const float w = sf[ky * F + kx];
+                const vecT v = base[(ky * IW + kx) * CG];
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[j] += (float)v[j] * w;
             }
-        }
-#pragma unroll
-        for (int k = 0; k < ROWS; ++k)
-            if (k < nrows) store_out<T, V, vecT>(p, y, acc[k], n, oy0 + k, ox, cv);
+        store_out<T, V, vecT>(p, (T*)p.y, acc, n, oy, ox, cv0 + c);
     }
 }
 
 template <typename T>
 int launch(const UpfParams& p, bool vec, hipStream_t s) {
-    if (vec && p.upx == 1 && p.upy == 1 && (p.downy == 1 || p.downy == 2)) {
-        const int64_t work = (int64_t)p.N * ((p.OH + 7) / 8) * p.OW * (p.C / VecN<T>::N);
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 256 * 32));
-        if (p.downy == 1) upfirdn_nhwc_slide<T, 1><<<grid, 256, 0, s>>>(p);
-        else upfirdn_nhwc_slide<T, 2><<<grid, 256, 0, s>>>(p);
-        return launch_status("sg2_upfirdn2d");
+    if (vec && p.upx == 1 && p.upy == 1 && p.downx == p.downy && (p.downy == 1 || p.downy == 2) && p.fw == 4 &&
+        p.fh == 4) {
+        constexpr int CG = 4;
+        const int d = p.downy;
+        const int TW = d == 1 ? 32 : 16, TH = 8;
+        const int64_t blocks = (int64_t)p.N * cdiv(p.OH, TH) * cdiv(p.OW, TW) * cdiv(p.C / VecN<T>::N, CG);
+        if (blocks < INT32_MAX) {
+            const size_t lds = (size_t)((TH - 1) * d + 4) * ((TW - 1) * d + 4) * CG * 16;
+            if (d == 1) {
+                auto k = upfirdn_nhwc_f4<T, 1, 32, 8, CG>;
+                static bool set1 = false;
+                if (!set1) { (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); set1 = true; }
+                k<<<(unsigned)blocks, 256, lds, s>>>(p);
+            } else {
+                auto k = upfirdn_nhwc_f4<T, 2, 16, 8, CG>;
+                static bool set2 = false;
+                if (!set2) { (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); set2 = true; }
+                k<<<(unsigned)blocks, 256, lds, s>>>(p);
+            }
+            return launch_status("sg2_upfirdn2d");
+        }
     }
     const int64_t work = vec ? (int64_t)p.N * p.OH * p.OW * (p.C / VecN<T>::N) : (int64_t)p.N * p.C * p.OH * p.OW;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 256 * 32));
