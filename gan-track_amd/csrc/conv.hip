@@ -692,8 +692,11 @@ int floordiv_h(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 
 }  // namespace
 
-int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* scale, int dtype, int N, int A, int H, int W,
-                    int B, hipStream_t s);   // wgrad3x3.hip
+// wgrad3x3.hip: halo weight gradient (3x3 / 1x1, stride 1 or 2, 16-bit)
+bool wgrad_halo_ok(int dtype, int KH, int KW, int stride, int pad_y, int pad_x, int OW, int A, int B);
+int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale, const float* xscale, int dtype,
+                    int N, int A, int OH, int OW, int B, int H, int W, int KH, int KW, int stride, int pad_y,
+                    int pad_x, hipStream_t s);
 }  // namespace sg2
 
 extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
@@ -847,10 +850,10 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     a.N = N; a.A = A; a.OH = OH; a.OW = OW; a.B = B; a.H = H; a.W = W; a.KH = KH; a.KW = KW;
     a.stride = stride; a.pady = pad_y; a.padx = pad_x;
     a.M = N * OH * OW;
-    const bool halo = dtype != SG2_F32 && g_scale == nullptr && KH == 3 && KW == 3 && stride == 1 && pad_y == 1 && pad_x == 1 &&
-                      OH == H && OW == W && W >= 16 && A % 8 == 0 && B % 8 == 0 && (uintptr_t)x % 16 == 0 &&
+    const bool halo = wgrad_halo_ok(dtype, KH, KW, stride, pad_y, pad_x, OW, A, B) && (uintptr_t)x % 16 == 0 &&
                       (uintptr_t)g % 16 == 0;
-    if (halo) return wgrad3x3_launch(dw, g, x, x_scale, dtype, N, A, H, W, B, s);
+    if (halo) return wgrad3x3_launch(dw, g, x, g_scale, x_scale, dtype, N, A, OH, OW, B, H, W, KH, KW, stride, pad_y,
+                                     pad_x, s);
     int rc = 0;
     SG2_DISPATCH(dtype, T, {
         constexpr int V = Traits<T>::V;

@@ -1,19 +1,24 @@
-// Weight gradient of the 3x3 / stride 1 / pad 1 convolution with an LDS halo tile (16-bit layers).
+// Weight gradient of the 3x3 convolutions (stride 1 or 2, and the transposed stride-2 convolution
+// of the up layers) with an LDS halo tile, for the 16-bit layers.
 //
-//   dw[a][tap][b] = sum_{n,y,x} g[n,y,x,a] * x[n, y+ky-1, x+kx-1, b] * s[n,b]      (s optional)
+//   dw[a][ky][kx][b] = sum_{n,oy,ox} g[n,oy,ox,a] u[n,a] * x[n, oy*S + ky - P, ox*S + kx - P, b] s[n,b]
+//   (u = g_scale, s = x_scale: a layer's modulation, optional)
 //
-// The generic weight-gradient kernel (conv.hip) runs one GEMM per tap, so it re-reads g and the
-// shifted x nine times and does only 4 MFMAs per barrier at C = 64.  Here a workgroup owns a
-// 64 (a) x 64 (b) channel block and walks a range of 256-pixel tiles (TW x TH of one sample):
-// per tile it stages g[256 px][64] and the (TH+2) x (TW+2) halo of x[.][64] in LDS once, then every
-// wave accumulates ALL nine taps of its 32 x 32 (a, b) sub-block:
-//   per 16-pixel k-step: 1 A fragment (g) + 9 B fragments (x shifted by the tap) through
-//   ds_read_b64_tr_b16, 9 v_mfma_f32_32x32x16 -- 144 MFMAs per tile and wave.
-// The pixel dimension is the GEMM's K, so partial sums over tiles stay in registers (9 x 16 f32 per
-// lane) and leave through one float atomic per (a, tap, b) per workgroup at the end.
-// The next tile's global loads are issued before the current tile's MFMAs (register staging).
-// Replaces the cuDNN weight gradient of the reference's 3x3 convolutions
-// (SG3/torch_utils/ops/conv2d_gradfix.py:37-45 -> autograd of F.conv2d).
+// Split by output phase: with S = 2, tap k reads x at (o + shift) * S + phase where
+// (k - P) = shift * S + phase; for one phase the taps' shifts lie in {-1, 0, 1}.  So each phase is a
+// "stride-1 halo" problem on the phase sub-grid of x: a workgroup owns a 64 (a) x 64 (b) channel block
+// and walks a range of 256-pixel tiles of the g grid (TW x TH of one sample).  Per tile it stages
+// g[256 px][64] and the (TH+2) x (TW+2) halo of the x phase sub-grid in LDS once; every wave then
+// accumulates ALL the phase's taps for its 32 x 32 (a, b) sub-block:
+//   per 16-pixel k-step: 1 A fragment (g) + NT B fragments (x shifted by the tap) through
+//   ds_read_b64_tr_b16, NT v_mfma_f32_32x32x16.
+// Pixels are the GEMM's K, so the partial sums stay in registers (NT x 16 f32 per lane) across tiles
+// and leave through one float atomic per (a, tap, b) per workgroup.  The next tile's global loads are
+// issued before the current tile's MFMAs (register staging).
+// The generic per-tap weight-gradient kernel (conv.hip) re-reads g and x once per tap and does only 4
+// MFMAs per barrier at C = 64; this one reads them once per phase.
+// Replaces the cuDNN weight gradients of the reference's convolutions
+// (SG3/torch_utils/ops/conv2d_gradfix.py:37-45 -> autograd of F.conv2d / F.conv_transpose2d).
 #include "sg2_common.h"
 
 #include <algorithm>
@@ -28,14 +33,19 @@ typedef short s16x8w __attribute__((ext_vector_type(8)));
 constexpr int BC = 64;          // channels per block in a and in b
 constexpr int LD = BC + 8;      // LDS row pitch (elements) of both tiles
 
+struct PTap { int8_t dy, dx, out, pad_; };   // shift on the phase grid, output tap index
+
 struct W3Args {
-    const void* g;        // [N,H,W,A]
-    const void* x;        // [N,H,W,B]
-    const float* scale;   // [N,B] or null
-    float* dw;            // [A][9][B], accumulated
-    int N, H, W, A, B;
-    int tiles_x, tiles_y, tiles;   // per sample / total
+    const void* g;        // [N,GH,GW,A]
+    const void* x;        // [N,XH,XW,B]
+    const float* gscale;  // [N,A] or null
+    const float* xscale;  // [N,B] or null
+    float* dw;            // [A][KK][B], accumulated
+    int N, GH, GW, XH, XW, A, B, KK;
+    int S, PY, PX;        // stride and phase: x coordinate = (g coordinate + shift) * S + phase
+    int tiles_x, tiles_y, tiles;
     int tiles_per_block;
+    PTap taps[9];
 };
 
 template <typename T>
@@ -50,8 +60,8 @@ __device__ __forceinline__ f32x16 mma32(v8w<T> a, v8w<T> b, f32x16 c) {
 }
 
 // 32x32x16 operand fragment from a row-major (pixel-major) LDS tile: lane l gets column c0 + (l & 31)
-// at rows r(8 * (l >> 5) + j), j = 0..7, where the 8 rows of each half are consecutive starting at
-// row0[half].  ds_read_b64_tr_b16 transposes a 4-row x 16-column block inside each 16-lane group.
+// at rows row0 + j, j = 0..7, where row0 already includes the 8 * (l >> 5) half offset.
+// ds_read_b64_tr_b16 transposes a 4-row x 16-column block inside each 16-lane group.
 template <typename T>
 __device__ __forceinline__ v8w<T> frag32(const T* tile, int row0, int c0, int lane) {
     const int G = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
@@ -63,10 +73,10 @@ __device__ __forceinline__ v8w<T> frag32(const T* tile, int row0, int c0, int la
     return __builtin_bit_cast(v8w<T>, r);
 }
 
-template <typename T, int TW>
+template <typename T, int TW, int NT>
 __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
     constexpr int TH = 256 / TW;
-    constexpr int HWD = TW + 2, HP = HWD * (TH + 2);     // halo width / pixels
+    constexpr int HWD = TW + 2, HP = HWD * (TH + 2);     // halo width / pixels (g-grid coordinates)
     constexpr int GCH = 8;                               // g: 256 px x 8 chunks / 256 threads
     constexpr int XCH = (HP * 8 + 255) / 256;            // x halo chunks per thread
     typedef T vec8 __attribute__((ext_vector_type(8)));
@@ -86,7 +96,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
 
     vec8 rg[GCH], rx[XCH];
     bool okg[GCH], okx[XCH];
-    float sc[8];
+    float gsc[8], xsc[8];
     auto gload = [&](int t) {
         const int per = a.tiles_x * a.tiles_y;
         const int n = t / per, r = t - n * per;
@@ -95,23 +105,27 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
         for (int i = 0; i < GCH; ++i) {
             const int px = (tid >> 3) + i * 32;          // tile pixel
             const int oy = ty0 + px / TW, ox = tx0 + px % TW;
-            const bool ok = a_ok && oy < a.H && ox < a.W;
+            const bool ok = a_ok && oy < a.GH && ox < a.GW;
             okg[i] = ok;
-            const int64_t off = ((int64_t)(n * a.H + (ok ? oy : 0)) * a.W + (ok ? ox : 0)) * a.A + (a_ok ? a0 + cc : 0);
+            const int64_t off = ((int64_t)(n * a.GH + (ok ? oy : 0)) * a.GW + (ok ? ox : 0)) * a.A + (a_ok ? a0 + cc : 0);
             rg[i] = *(const vec8*)(gp + off);
         }
 #pragma unroll
         for (int i = 0; i < XCH; ++i) {
             const int hp = (tid >> 3) + i * 32;
-            const int iy = ty0 - 1 + hp / HWD, ix = tx0 - 1 + hp % HWD;
-            const bool ok = b_ok && hp < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            const int iy = (ty0 - 1 + hp / HWD) * a.S + a.PY, ix = (tx0 - 1 + hp % HWD) * a.S + a.PX;
+            const bool ok = b_ok && hp < HP && iy >= 0 && iy < a.XH && ix >= 0 && ix < a.XW;
             okx[i] = ok;
-            const int64_t off = ((int64_t)(n * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.B + (b_ok ? b0 + cc : 0);
+            const int64_t off = ((int64_t)(n * a.XH + (ok ? iy : 0)) * a.XW + (ok ? ix : 0)) * a.B + (b_ok ? b0 + cc : 0);
             rx[i] = *(const vec8*)(xp + off);
         }
-        if (a.scale) {
+        if (a.gscale) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) sc[j] = a.scale[(int64_t)n * a.B + (b_ok ? b0 + cc + j : 0)];
+            for (int j = 0; j < 8; ++j) gsc[j] = a.gscale[(int64_t)n * a.A + (a_ok ? a0 + cc + j : 0)];
+        }
+        if (a.xscale) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xsc[j] = a.xscale[(int64_t)n * a.B + (b_ok ? b0 + cc + j : 0)];
         }
     };
     auto sstore = [&]() {
@@ -119,7 +133,11 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
         for (int i = 0; i < GCH; ++i) {
             vec8 v = rg[i];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = okg[i] ? v[j] : (T)0.f;
+            for (int j = 0; j < 8; ++j) {
+                float f = okg[i] ? (float)v[j] : 0.f;
+                if (a.gscale) f *= gsc[j];
+                v[j] = (T)f;
+            }
             *(vec8*)(gs + ((tid >> 3) + i * 32) * LD + cc) = v;
         }
 #pragma unroll
@@ -129,16 +147,20 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 float f = okx[i] ? (float)v[j] : 0.f;
-                if (a.scale) f *= sc[j];
+                if (a.xscale) f *= xsc[j];
                 v[j] = (T)f;
             }
             if (hp < HP) *(vec8*)(xs + hp * LD + cc) = v;
         }
     };
 
-    f32x16 acc[9];
+    int toff[NT];   // halo row offset of each tap
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int t = 0; t < NT; ++t) toff[t] = (a.taps[t].dy + 1) * HWD + a.taps[t].dx + 1;
+
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
 
@@ -155,13 +177,12 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
                 const int pr = k0 + 8 * ((lane >> 4) >> 1);
                 const int py = pr / TW, px = pr % TW;
                 const v8w<T> fa = frag32<T>(gs, pr, wa * 32, lane);
+                const int hb = py * HWD + px;
 #pragma unroll
-                for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                    for (int kx = 0; kx < 3; ++kx) {
-                        const v8w<T> fb = frag32<T>(xs, (py + ky) * HWD + px + kx, wb * 32, lane);
-                        acc[ky * 3 + kx] = mma32<T>(fa, fb, acc[ky * 3 + kx]);
-                    }
+                for (int tp = 0; tp < NT; ++tp) {
+                    const v8w<T> fb = frag32<T>(xs, hb + toff[tp], wb * 32, lane);
+                    acc[tp] = mma32<T>(fa, fb, acc[tp]);
+                }
             }
             __syncthreads();
             if (more) {
@@ -179,38 +200,85 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
             const int ar = a0 + wa * 32 + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
             if (ar >= a.A) continue;
 #pragma unroll
-            for (int t = 0; t < 9; ++t) atomicAdd(a.dw + ((int64_t)ar * 9 + t) * a.B + b, acc[t][j]);
+            for (int t = 0; t < NT; ++t)
+                atomicAdd(a.dw + ((int64_t)ar * a.KK + a.taps[t].out) * a.B + b, acc[t][j]);
         }
     }
 }
 
+template <typename T, int TW, int NT>
+void launch_w3(const W3Args& a, dim3 grid, hipStream_t s) {
+    wgrad3x3_kernel<T, TW, NT><<<grid, 256, 0, s>>>(a);
+}
+
+template <typename T, int TW>
+int dispatch_nt(const W3Args& a, dim3 grid, int nt, hipStream_t s) {
+    switch (nt) {
+        case 1: launch_w3<T, TW, 1>(a, grid, s); break;
+        case 2: launch_w3<T, TW, 2>(a, grid, s); break;
+        case 4: launch_w3<T, TW, 4>(a, grid, s); break;
+        case 9: launch_w3<T, TW, 9>(a, grid, s); break;
+        default: set_error("sg2_conv2d_wgrad: unsupported tap count per phase"); return -1;
+    }
+    return 0;
+}
+
+int floordiv_w(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
 }  // namespace
 
-// Called by sg2_conv2d_wgrad for 16-bit 3x3 / s1 / p1 problems with A % 8 == 0, B % 8 == 0 and
-// 16-byte aligned operands (dw already zeroed).
-int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* scale, int dtype, int N, int A, int H, int W,
-                    int B, hipStream_t s) {
+// Is the halo weight gradient applicable?  (3x3 or 1x1 kernel, stride 1 or 2, every tap's shift on
+// its phase grid within [-1, 1], 16-bit, channels multiples of 8, g grid at least 16 wide.)
+bool wgrad_halo_ok(int dtype, int KH, int KW, int stride, int pad_y, int pad_x, int OW, int A, int B) {
+    if (dtype == SG2_F32 || KH != KW || (KH != 3 && KH != 1) || stride < 1 || stride > 2) return false;
+    if (A % 8 || B % 8 || OW < 16) return false;
+    for (int k = 0; k < KH; ++k) {
+        const int sy = floordiv_w(k - pad_y, stride), sx = floordiv_w(k - pad_x, stride);
+        if (sy < -1 || sy > 1 || sx < -1 || sx > 1) return false;
+    }
+    return true;
+}
+
+// dw already zeroed.  One launch per output phase that has taps.
+int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale, const float* xscale, int dtype,
+                    int N, int A, int OH, int OW, int B, int H, int W, int KH, int KW, int stride, int pad_y,
+                    int pad_x, hipStream_t s) {
     W3Args a{};
-    a.g = g; a.x = x; a.scale = scale; a.dw = dw;
-    a.N = N; a.H = H; a.W = W; a.A = A; a.B = B;
-    const int TW = W >= 32 ? 32 : 16;
-    a.tiles_x = (int)cdiv(W, TW);
-    a.tiles_y = (int)cdiv(H, 256 / TW);
+    a.g = g; a.x = x; a.gscale = gscale; a.xscale = xscale; a.dw = dw;
+    a.N = N; a.GH = OH; a.GW = OW; a.XH = H; a.XW = W; a.A = A; a.B = B; a.KK = KH * KW; a.S = stride;
+    const int TW = OW >= 32 ? 32 : 16;
+    a.tiles_x = (int)cdiv(OW, TW);
+    a.tiles_y = (int)cdiv(OH, 256 / TW);
     a.tiles = N * a.tiles_x * a.tiles_y;
     const int cb = (int)(cdiv(A, BC) * cdiv(B, BC));
-    // ~512 workgroups (2 per CU over the launch), at least 4 tiles each
+    // ~512 workgroups per launch, at least 4 tiles each
     int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(512, cb), a.tiles / 4));
     a.tiles_per_block = (int)cdiv(a.tiles, splits);
     splits = (int)cdiv(a.tiles, a.tiles_per_block);
     dim3 grid((unsigned)cdiv(A, BC), (unsigned)cdiv(B, BC), (unsigned)splits);
-    if (dtype == SG2_F16) {
-        if (TW == 32) wgrad3x3_kernel<f16_t, 32><<<grid, 256, 0, s>>>(a);
-        else wgrad3x3_kernel<f16_t, 16><<<grid, 256, 0, s>>>(a);
-    } else {
-        if (TW == 32) wgrad3x3_kernel<bf16_t, 32><<<grid, 256, 0, s>>>(a);
-        else wgrad3x3_kernel<bf16_t, 16><<<grid, 256, 0, s>>>(a);
-    }
-    return launch_status("sg2_conv2d_wgrad (3x3 halo)");
+    for (int py = 0; py < stride; ++py)
+        for (int px = 0; px < stride; ++px) {
+            int nt = 0;
+            for (int ky = 0; ky < KH; ++ky) {
+                const int ry = ky - pad_y;
+                if (((ry % stride) + stride) % stride != py) continue;
+                for (int kx = 0; kx < KW; ++kx) {
+                    const int rx = kx - pad_x;
+                    if (((rx % stride) + stride) % stride != px) continue;
+                    a.taps[nt++] = PTap{(int8_t)floordiv_w(ry, stride), (int8_t)floordiv_w(rx, stride),
+                                        (int8_t)(ky * KW + kx), 0};
+                }
+            }
+            if (nt == 0) continue;
+            a.PY = py; a.PX = px;
+            int rc;
+            if (dtype == SG2_F16) rc = TW == 32 ? dispatch_nt<f16_t, 32>(a, grid, nt, s) : dispatch_nt<f16_t, 16>(a, grid, nt, s);
+            else rc = TW == 32 ? dispatch_nt<bf16_t, 32>(a, grid, nt, s) : dispatch_nt<bf16_t, 16>(a, grid, nt, s);
+            if (rc) return rc;
+            rc = launch_status("sg2_conv2d_wgrad (halo)");
+            if (rc) return rc;
+        }
+    return 0;
 }
 
 }  // namespace sg2

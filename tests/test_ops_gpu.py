@@ -636,3 +636,40 @@ def test_conv_fused_dot_and_scale(dtype, geom):
     tol = 1e-5 if dtype == torch.float32 else 5e-3
     assert rel_err(y.float(), ref * s.double()[:, :, None, None]) < tol
     assert rel_err(dot, (ref.to(dtype).double() * src.double()).sum([2, 3])) < (1e-5 if dtype == torch.float32 else 5e-3)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('case', ['conv_s2', 'convT_s2', 'conv_1x1'])
+def test_wgrad_halo_phases(dtype, case):
+    """Halo weight gradient split by output phase: stride-2 conv (D down layers), the transposed
+    stride-2 conv of the up layers (with the modulation on the g operand) and 1x1, vs autograd in f64."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(31)
+    N, Ci, Co = 2, 64, 72
+    if case == 'conv_s2':
+        x = torch.randn(N, Ci, 33, 41, device=DEV)
+        w = torch.randn(Co, Ci, 3, 3, device=DEV, dtype=torch.float64, requires_grad=True)
+        y = F.conv2d(x.to(dtype).double(), w, stride=2)
+        g = torch.randn_like(y)
+        ref, = torch.autograd.grad((y * g.to(dtype).double()).sum(), [w])
+        dw = cg._wgrad_raw(g.to(dtype).contiguous(memory_format=torch.channels_last),
+                           x.to(dtype).contiguous(memory_format=torch.channels_last), 3, 3, 2, (0, 0))
+    elif case == 'convT_s2':
+        x = torch.randn(N, Ci, 16, 20, device=DEV)
+        s = torch.rand(N, Ci, device=DEV) + 0.5
+        wt = torch.randn(Ci, Co, 3, 3, device=DEV, dtype=torch.float64, requires_grad=True)
+        xs = (x.to(dtype).float() * s[:, :, None, None]).to(dtype).double()
+        y = F.conv_transpose2d(xs, wt, stride=2)
+        dt = torch.randn_like(y)
+        ref, = torch.autograd.grad((y * dt.to(dtype).double()).sum(), [wt])
+        dw = cg._wgrad_raw(x.to(dtype).contiguous(memory_format=torch.channels_last),
+                           dt.to(dtype).contiguous(memory_format=torch.channels_last), 3, 3, 2, (0, 0), g_scale=s)
+    else:
+        x = torch.randn(N, Ci, 24, 20, device=DEV)
+        w = torch.randn(Co, Ci, 1, 1, device=DEV, dtype=torch.float64, requires_grad=True)
+        y = F.conv2d(x.to(dtype).double(), w)
+        g = torch.randn_like(y)
+        ref, = torch.autograd.grad((y * g.to(dtype).double()).sum(), [w])
+        dw = cg._wgrad_raw(g.to(dtype).contiguous(memory_format=torch.channels_last),
+                           x.to(dtype).contiguous(memory_format=torch.channels_last), 1, 1, 1, (0, 0))
+    assert rel_err(dw, ref) < (2e-3 if dtype == torch.float16 else 1e-2)

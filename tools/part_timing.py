@@ -33,12 +33,17 @@ def t(name, fn, reps=5):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     h0 = time.perf_counter()
     e0.record()
+    issue = 0.0
     for _ in range(reps):
+        torch.cuda.synchronize()           # empty queue: the host time of fn() is its pure issue cost
+        t0 = time.perf_counter()
         fn()
+        issue += time.perf_counter() - t0
     e1.record()
     e1.synchronize()
     h1 = time.perf_counter()
-    print(f'{name:28s} gpu {e0.elapsed_time(e1) / reps:8.2f} ms   wall {(h1 - h0) / reps * 1e3:8.2f} ms', flush=True)
+    print(f'{name:28s} gpu {e0.elapsed_time(e1) / reps:8.2f} ms   wall {(h1 - h0) / reps * 1e3:8.2f} ms   '
+          f'host issue {issue / reps * 1e3:8.2f} ms', flush=True)
 
 
 with torch.no_grad():
