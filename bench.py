@@ -55,6 +55,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--phase-timing', action='store_true')
+    ap.add_argument('--no-graphs', action='store_true', help='eager PyTorch dispatch instead of HIP-graph replay')
     return ap.parse_args()
 
 
@@ -206,6 +207,12 @@ def main():
     tr = build(args, device, rank, num_gpus)
     real, real_c = make_inputs(args, device, rank)
     for _ in range(args.warmup):
+        one_step(tr, args, device, real, real_c)
+    if not args.no_graphs:
+        # capture: one untimed step at batch_idx 0 runs (and captures) all four phases; afterwards every
+        # phase is a single HIP-graph replay (trainer.py Trainer.graphs)
+        tr.graphs = True
+        tr.batch_idx = 0
         one_step(tr, args, device, real, real_c)
     torch.cuda.synchronize(device)
     tr.batch_idx = 0                                    # timed region starts a full 16-step cycle

@@ -19,6 +19,7 @@ struct GSParams {
     int N, C, Hi, Wi, Ho, Wo;
     int64_t is_n, is_c, is_h, is_w;
     int64_t os_n, os_c, os_h, os_w;
+    const int* dyn_hw;   // optional device [2]: logical input height / width (<= Hi, Wi of the buffer)
 };
 
 struct Corners {
@@ -26,10 +27,10 @@ struct Corners {
     float w00, w01, w10, w11;  // w[yy][xx]
 };
 
-__device__ __forceinline__ Corners corners(const GSParams& p, int n, int oy, int ox) {
+__device__ __forceinline__ Corners corners(const GSParams& p, int n, int oy, int ox, int Hi, int Wi) {
     const float* g = p.grid + (((int64_t)n * p.Ho + oy) * p.Wo + ox) * 2;
-    const float ix = ((g[0] + 1.f) * p.Wi - 1.f) * 0.5f;
-    const float iy = ((g[1] + 1.f) * p.Hi - 1.f) * 0.5f;
+    const float ix = ((g[0] + 1.f) * Wi - 1.f) * 0.5f;
+    const float iy = ((g[1] + 1.f) * Hi - 1.f) * 0.5f;
     Corners c;
     const float fx = floorf(ix), fy = floorf(iy);
     c.x0 = (int)fx;
@@ -48,14 +49,15 @@ __global__ __launch_bounds__(256) void grid_sample_fwd_kernel(GSParams p) {
     const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
     const T* in = (const T*)p.in;
     T* out = (T*)p.out;
+    const int Hi = p.dyn_hw ? p.dyn_hw[0] : p.Hi, Wi = p.dyn_hw ? p.dyn_hw[1] : p.Wi;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += (int64_t)gridDim.x * blockDim.x) {
         const int ox = (int)(idx % p.Wo);
         const int oy = (int)((idx / p.Wo) % p.Ho);
         const int n = (int)(idx / ((int64_t)p.Wo * p.Ho));
-        const Corners k = corners(p, n, oy, ox);
-        const bool vx0 = k.x0 >= 0 && k.x0 < p.Wi, vx1 = k.x0 + 1 >= 0 && k.x0 + 1 < p.Wi;
-        const bool vy0 = k.y0 >= 0 && k.y0 < p.Hi, vy1 = k.y0 + 1 >= 0 && k.y0 + 1 < p.Hi;
+        const Corners k = corners(p, n, oy, ox, Hi, Wi);
+        const bool vx0 = k.x0 >= 0 && k.x0 < Wi, vx1 = k.x0 + 1 >= 0 && k.x0 + 1 < Wi;
+        const bool vy0 = k.y0 >= 0 && k.y0 < Hi, vy1 = k.y0 + 1 >= 0 && k.y0 + 1 < Hi;
         for (int c = 0; c < p.C; ++c) {
             const T* b = in + n * p.is_n + c * p.is_c;
             float acc = 0.f;
@@ -73,14 +75,15 @@ __global__ __launch_bounds__(256) void grid_sample_bwd_kernel(GSParams p) {
     const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
     const T* gout = (const T*)p.in;   // gradient w.r.t. output (layout os_*)
     float* gin = (float*)p.out;       // gradient w.r.t. input  (layout is_*)
+    const int Hi = p.dyn_hw ? p.dyn_hw[0] : p.Hi, Wi = p.dyn_hw ? p.dyn_hw[1] : p.Wi;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += (int64_t)gridDim.x * blockDim.x) {
         const int ox = (int)(idx % p.Wo);
         const int oy = (int)((idx / p.Wo) % p.Ho);
         const int n = (int)(idx / ((int64_t)p.Wo * p.Ho));
-        const Corners k = corners(p, n, oy, ox);
-        const bool vx0 = k.x0 >= 0 && k.x0 < p.Wi, vx1 = k.x0 + 1 >= 0 && k.x0 + 1 < p.Wi;
-        const bool vy0 = k.y0 >= 0 && k.y0 < p.Hi, vy1 = k.y0 + 1 >= 0 && k.y0 + 1 < p.Hi;
+        const Corners k = corners(p, n, oy, ox, Hi, Wi);
+        const bool vx0 = k.x0 >= 0 && k.x0 < Wi, vx1 = k.x0 + 1 >= 0 && k.x0 + 1 < Wi;
+        const bool vy0 = k.y0 >= 0 && k.y0 < Hi, vy1 = k.y0 + 1 >= 0 && k.y0 + 1 < Hi;
         for (int c = 0; c < p.C; ++c) {
             const float g = (float)gout[n * p.os_n + c * p.os_c + (int64_t)oy * p.os_h + (int64_t)ox * p.os_w];
             float* b = gin + n * p.is_n + c * p.is_c;
@@ -89,6 +92,52 @@ __global__ __launch_bounds__(256) void grid_sample_bwd_kernel(GSParams p) {
             if (vy1 && vx0) atomicAdd(b + (k.y0 + 1) * p.is_h + k.x0 * p.is_w, g * k.w10);
             if (vy1 && vx1) atomicAdd(b + (k.y0 + 1) * p.is_h + (k.x0 + 1) * p.is_w, g * k.w11);
         }
+    }
+}
+
+// Reflect padding with margins held in device memory (so the ADA pipe needs no host sync): the
+// padded image of logical size (H + my0 + my1) x (W + mx0 + mx1) is written at the origin of a static
+// [N, C, Hs, Ws] buffer, zeros elsewhere (exactly what upfirdn2d's implicit zero padding sees).
+// Margins never exceed the image size minus one (augment_mi.py:295-296), so one reflection suffices.
+__device__ __forceinline__ int reflect1(int k, int L) { return k < 0 ? -k : (k >= L ? 2 * (L - 1) - k : k); }
+
+__global__ __launch_bounds__(256) void reflect_pad_kernel(float* y, const float* x, const int* m, int N, int C, int H,
+                                                          int W, int Hs, int Ws) {
+    const int mx0 = m[0], my0 = m[1], mx1 = m[2], my1 = m[3];
+    const int Hd = H + my0 + my1, Wd = W + mx0 + mx1;
+    const int64_t total = (int64_t)N * C * Hs * Ws;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int px = (int)(i % Ws);
+        const int py = (int)((i / Ws) % Hs);
+        const int64_t nc = i / ((int64_t)Ws * Hs);
+        float v = 0.f;
+        if (py < Hd && px < Wd) v = x[(nc * H + reflect1(py - my0, H)) * W + reflect1(px - mx0, W)];
+        y[i] = v;
+    }
+}
+
+// Adjoint of reflect_pad_kernel: every source pixel gathers the (up to 3 x 3) padded positions that
+// reflect onto it.
+__global__ __launch_bounds__(256) void reflect_pad_adj_kernel(float* gx, const float* gy, const int* m, int N, int C,
+                                                              int H, int W, int Hs, int Ws) {
+    const int mx0 = m[0], my0 = m[1], mx1 = m[2], my1 = m[3];
+    const int64_t total = (int64_t)N * C * H * W;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int ix = (int)(i % W);
+        const int iy = (int)((i / W) % H);
+        const int64_t nc = i / ((int64_t)W * H);
+        int ys[3], xs[3], ny = 0, nx = 0;
+        ys[ny++] = my0 + iy;
+        if (iy >= 1 && iy <= my0) ys[ny++] = my0 - iy;
+        if (iy <= H - 2 && iy >= H - 1 - my1) ys[ny++] = my0 + 2 * (H - 1) - iy;
+        xs[nx++] = mx0 + ix;
+        if (ix >= 1 && ix <= mx0) xs[nx++] = mx0 - ix;
+        if (ix <= W - 2 && ix >= W - 1 - mx1) xs[nx++] = mx0 + 2 * (W - 1) - ix;
+        const float* b = gy + nc * Hs * Ws;
+        float acc = 0.f;
+        for (int a = 0; a < ny; ++a)
+            for (int c = 0; c < nx; ++c) acc += b[(int64_t)ys[a] * Ws + xs[c]];
+        gx[i] = acc;
     }
 }
 
@@ -108,11 +157,11 @@ int fill(GSParams& p, const int64_t* in_size, const int64_t* in_stride, const in
 
 extern "C" int sg2_grid_sample_fwd(void* out, const void* in, const float* grid, int dtype, const int64_t* in_size,
                                    const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
-                                   void* stream) {
+                                   const int* dyn_hw, void* stream) {
     using namespace sg2;
     SG2_CHECK(out && in && grid, "sg2_grid_sample_fwd: null pointer");
     GSParams p;
-    p.in = in; p.out = out; p.grid = grid;
+    p.in = in; p.out = out; p.grid = grid; p.dyn_hw = dyn_hw;
     if (fill(p, in_size, in_stride, out_size, out_stride)) return -1;
     const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
     if (total == 0 || p.C == 0) return 0;
@@ -123,13 +172,12 @@ extern "C" int sg2_grid_sample_fwd(void* out, const void* in, const float* grid,
 
 extern "C" int sg2_grid_sample_bwd(float* gin, const void* gout, const float* grid, int dtype, const int64_t* in_size,
                                    const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
-                                   void* stream) {
+                                   const int* dyn_hw, void* stream) {
     using namespace sg2;
     SG2_CHECK(gin && gout && grid, "sg2_grid_sample_bwd: null pointer");
     GSParams p;
-    p.in = gout; p.out = gin; p.grid = grid;
+    p.in = gout; p.out = gin; p.grid = grid; p.dyn_hw = dyn_hw;
     if (fill(p, in_size, in_stride, out_size, out_stride)) return -1;
-    SG2_CHECK(p.is_w == 1 || p.C == 1 || true, "");
     // zero the float32 input-gradient buffer (dense over the strided extent)
     const int64_t extent = (p.N - 1) * p.is_n + (p.C - 1) * p.is_c + (p.Hi - 1) * p.is_h + (p.Wi - 1) * p.is_w + 1;
     hipStream_t s = as_stream(stream);
@@ -140,4 +188,18 @@ extern "C" int sg2_grid_sample_bwd(float* gin, const void* gout, const float* gr
     const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 32);
     SG2_DISPATCH(dtype, T, { grid_sample_bwd_kernel<T><<<g, 256, 0, s>>>(p); });
     return launch_status("sg2_grid_sample_bwd");
+}
+
+extern "C" int sg2_reflect_pad_dyn(float* y, const float* x, const int* margins, int N, int C, int H, int W, int Hs,
+                                   int Ws, int adjoint, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(y && x && margins, "sg2_reflect_pad_dyn: null pointer");
+    SG2_CHECK(N >= 0 && C >= 0 && H > 0 && W > 0 && Hs >= 3 * H - 2 && Ws >= 3 * W - 2,
+              "sg2_reflect_pad_dyn: the static buffer must hold the largest padded image (3H-2 x 3W-2)");
+    const int64_t total = adjoint ? (int64_t)N * C * H * W : (int64_t)N * C * Hs * Ws;
+    if (total == 0) return 0;
+    const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 64);
+    if (adjoint) reflect_pad_adj_kernel<<<g, 256, 0, as_stream(stream)>>>(y, x, margins, N, C, H, W, Hs, Ws);
+    else reflect_pad_kernel<<<g, 256, 0, as_stream(stream)>>>(y, x, margins, N, C, H, W, Hs, Ws);
+    return launch_status("sg2_reflect_pad_dyn");
 }

@@ -46,8 +46,9 @@ SIGNATURES = {
     'sg2_upfirdn2d_fused': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _i, _i, _i, _i, _i, _i, _i, _i, _i,
                             _i, _i, _f, ctypes.POINTER(Epilogue), _vp],
     'sg2_layer_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _f, _vp],
-    'sg2_grid_sample_fwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp],
-    'sg2_grid_sample_bwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp],
+    'sg2_grid_sample_fwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
+    'sg2_grid_sample_bwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
+    'sg2_reflect_pad_dyn': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp],
     'sg2_demod_coefs': [_vp, _vp, _vp, _i, _i, _i, _i, _f, _vp],
     'sg2_adam_step': [_vp, _vp, _vp, _vp, _i64, _f, _f, _f, _f, _f, _i64, _vp],
     'sg2_lerp': [_vp, _vp, _i64, _f, _vp],

@@ -17,6 +17,7 @@ from torch_utils import misc
 from torch_utils import persistence
 from torch_utils.ops import conv2d_gradfix
 from torch_utils.ops import grid_sample_gradfix
+from torch_utils.ops import reflect_pad
 from torch_utils.ops import upfirdn2d
 
 wavelets = {
@@ -195,18 +196,23 @@ class AugmentPipe(torch.nn.Module):
         m = m + misc.constant([hz_pad * 2 - cx, hz_pad * 2 - cy] * 2, device=dev)
         m = m.max(misc.constant([0, 0] * 2, device=dev))
         m = m.min(misc.constant([w - 1, h - 1] * 2, device=dev))
-        mx0, my0, mx1, my1 = [int(v) for v in m.ceil().to(torch.int32).tolist()]
+        mi = m.ceil().to(torch.int32)                     # (mx0, my0, mx1, my1), kept on the device
+        mf = mi.float()
+        mx0, my0, mx1, my1 = mf[0], mf[1], mf[2], mf[3]
 
-        images = torch.nn.functional.pad(input=images, pad=[mx0, mx1, my0, my1], mode='reflect')
-        G = translate2d((mx0 - mx1) / 2, (my0 - my1) / 2, device=dev) @ G
+        # Reflect pad into a static buffer (logical size h+my0+my1 x w+mx0+mx1 at its origin): no host
+        # sync, so the step can be graph-captured (torch_utils/ops/reflect_pad.py).
+        images = reflect_pad.reflect_pad_dyn(images, mi)
+        G = translate2d((mx0 - mx1) / 2, (my0 - my1) / 2) @ G
         images = upfirdn2d.upsample2d(x=images, f=self.Hz_geom, up=2)
         G = scale2d(2, 2, device=dev) @ G @ scale2d_inv(2, 2, device=dev)
         G = translate2d(-0.5, -0.5, device=dev) @ G @ translate2d_inv(-0.5, -0.5, device=dev)
         shape = [n, c, (h + hz_pad * 2) * 2, (w + hz_pad * 2) * 2]
-        G = scale2d(2 / images.shape[3], 2 / images.shape[2], device=dev) @ G @ \
-            scale2d_inv(2 / shape[3], 2 / shape[2], device=dev)
+        dyn_h, dyn_w = (h + my0 + my1) * 2, (w + mx0 + mx1) * 2     # logical size of the upsampled image
+        G = scale2d(2 / dyn_w, 2 / dyn_h) @ G @ scale2d_inv(2 / shape[3], 2 / shape[2], device=dev)
         grid = torch.nn.functional.affine_grid(theta=G[:, :2, :], size=shape, align_corners=False)
-        images = grid_sample_gradfix.grid_sample(images, grid)
+        dyn_hw = torch.stack([dyn_h, dyn_w]).to(torch.int32)
+        images = grid_sample_gradfix.grid_sample(images, grid, dyn_hw=dyn_hw)
         return upfirdn2d.downsample2d(x=images, f=self.Hz_geom, down=2, padding=-hz_pad * 2, flip_filter=True)
 
     # ------------------------------------------------------------------ colour

@@ -41,7 +41,11 @@ class StyleGAN2Loss(Loss):
                 cutoff = torch.empty([], dtype=torch.int64, device=ws.device).random_(1, ws.shape[1])
                 cutoff = torch.where(torch.rand([], device=ws.device) < self.style_mixing_prob, cutoff,
                                      torch.full_like(cutoff, ws.shape[1]))
-                ws[:, cutoff:] = self.G.mapping(torch.randn_like(z), c, update_emas=False)[:, cutoff:]
+                # ws[:, cutoff:] = mapping(z2)[:, cutoff:] as a device-side select: slicing by a device
+                # tensor would read it back to the host (a sync per call, and no HIP-graph capture)
+                ws2 = self.G.mapping(torch.randn_like(z), c, update_emas=False)
+                mix = (torch.arange(ws.shape[1], device=ws.device) >= cutoff).reshape(1, -1, 1)
+                ws = torch.where(mix, ws2, ws)
         img = self.G.synthesis(ws, update_emas=update_emas)
         return img, ws
 

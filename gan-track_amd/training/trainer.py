@@ -118,7 +118,7 @@ class Trainer:
     def __init__(self, G, D, G_ema, loss, G_opt_kwargs, D_opt_kwargs, G_reg_interval=4, D_reg_interval=16,
                  batch_size=32, batch_gpu=32, num_gpus=1, rank=0, device=None, ema_kimg=10, ema_rampup=0.05,
                  augment_pipe=None, ada_target=None, ada_interval=4, ada_kimg=500, bucket_mb=32, overlap=True,
-                 phase_timing=False):
+                 phase_timing=False, graphs=False):
         self.G, self.D, self.G_ema, self.loss = G, D, G_ema, loss
         self.batch_size, self.batch_gpu, self.num_gpus, self.rank = batch_size, batch_gpu, num_gpus, rank
         self.device = device
@@ -153,6 +153,43 @@ class Trainer:
         self.cur_nimg = 0
         self.batch_idx = 0
         self.on_grads = None   # optional callback(phase_name, module) after the gradient exchange
+        # HIP-graph mode: each phase's forward + backward (all micro-batches) is captured once and
+        # replayed; the gradient exchange, the optimiser, EMA and ADA stay eager.  Capture the first
+        # time a phase runs in graph mode -- run at least one eager step first so every lazily created
+        # state (kernel attributes, statistics counters, cached constants) exists before capture.
+        self.graphs = graphs
+        self._graphs = {}
+
+    def _accumulate(self, phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c, arm):
+        chunks = list(zip(phase_real_img, phase_real_c, phase_gen_z, phase_gen_c))
+        for ci, (real_img, real_c, gen_z, gen_c) in enumerate(chunks):
+            if arm and ci == len(chunks) - 1:
+                phase.reducer.arm(expected=2 if phase.name in ('Dmain', 'Dboth') else 1)
+            self.loss.accumulate_gradients(phase=phase.name, real_img=real_img, real_c=real_c, gen_z=gen_z,
+                                           gen_c=gen_c, gain=phase.interval, cur_nimg=self.cur_nimg)
+
+    def _graph_phase(self, phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c):
+        st = self._graphs.get(phase.name)
+        if st is None:
+            st = dnnlib.EasyDict()
+            st.inputs = [[t.clone() for t in lst] for lst in (phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)]
+            st.params = list(phase.module.parameters())
+            phase.opt.zero_grad(set_to_none=True)
+            torch.cuda.synchronize(self.device)
+            st.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(st.graph):
+                phase.module.requires_grad_(True)
+                self._accumulate(phase, *st.inputs, arm=False)
+                phase.module.requires_grad_(False)
+            st.grads = [p.grad for p in st.params]      # the graph writes these buffers on every replay
+            self._graphs[phase.name] = st
+        else:
+            for dst, src in zip(st.inputs, (phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)):
+                for d, s_ in zip(dst, src):
+                    d.copy_(s_)
+        for p, g in zip(st.params, st.grads):
+            p.grad = g
+        st.graph.replay()
 
     def step(self, phase_real_img, phase_real_c, all_gen_z, all_gen_c):
         """One iteration.  phase_real_img/c: lists of batch_gpu chunks; all_gen_z/c: per phase, lists
@@ -162,15 +199,13 @@ class Trainer:
                 continue
             if phase.start_event is not None:
                 phase.start_event.record(torch.cuda.current_stream(self.device))
-            phase.opt.zero_grad(set_to_none=True)
-            phase.module.requires_grad_(True)
-            chunks = list(zip(phase_real_img, phase_real_c, phase_gen_z, phase_gen_c))
-            for ci, (real_img, real_c, gen_z, gen_c) in enumerate(chunks):
-                if ci == len(chunks) - 1:
-                    phase.reducer.arm(expected=2 if phase.name in ('Dmain', 'Dboth') else 1)
-                self.loss.accumulate_gradients(phase=phase.name, real_img=real_img, real_c=real_c, gen_z=gen_z,
-                                               gen_c=gen_c, gain=phase.interval, cur_nimg=self.cur_nimg)
-            phase.module.requires_grad_(False)
+            if self.graphs:
+                self._graph_phase(phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)
+            else:
+                phase.opt.zero_grad(set_to_none=True)
+                phase.module.requires_grad_(True)
+                self._accumulate(phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c, arm=True)
+                phase.module.requires_grad_(False)
             with torch.autograd.profiler.record_function(phase.name + '_opt'):
                 phase.reducer.finish()
                 if self.on_grads is not None:

@@ -156,13 +156,24 @@ int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, const void* dy,
  * out [N,C,Ho,Wo] any strides. */
 int sg2_grid_sample_fwd(void* out, const void* in, const float* grid, int dtype, const int64_t* in_size,
                         const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
-                        void* stream);
+                        const int* dyn_hw, void* stream);
 
 /* Gradient of sg2_grid_sample_fwd w.r.t. its input: gin (float32, [N,C,Hi,Wi] with in_stride) is
  * zero-filled then accumulated. */
 int sg2_grid_sample_bwd(float* gin, const void* gout, const float* grid, int dtype, const int64_t* in_size,
                         const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
-                        void* stream);
+                        const int* dyn_hw, void* stream);
+
+/* dyn_hw (both grid-sample calls; may be NULL): device int[2], the logical input height / width when
+ * `in` is a larger static buffer whose valid region starts at the origin -- the ADA pipe's padded image
+ * whose size depends on device-side margins (augment_mi.py:288-318), sampled without a host sync. */
+
+/* Reflect padding with device-side margins (augment_mi.py:301): margins = device int[4] {mx0, my0,
+ * mx1, my1} (each <= size - 1).  adjoint = 0: y [N,C,Hs,Ws] (NCHW, f32) = reflect-padded x [N,C,H,W]
+ * at the origin, zeros elsewhere; Hs >= 3H-2, Ws >= 3W-2.  adjoint = 1: y [N,C,H,W] = the adjoint
+ * (gather of the reflected positions) of x [N,C,Hs,Ws]. */
+int sg2_reflect_pad_dyn(float* y, const float* x, const int* margins, int N, int C, int H, int W, int Hs, int Ws,
+                        int adjoint, void* stream);
 
 /* Demodulation coefficients d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps), wsq[o,i] = sum_k w[o,i,k]^2
  * (SG3/training/networks_stylegan2.py:59-63, summation regrouped).  s [N,I] f32, w [O,I*KK] f32. */
