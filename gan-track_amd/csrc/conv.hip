@@ -20,6 +20,15 @@
 // Weight gradient: dw[a][tap][b] = sum_m g[m][a] * x[in(m,tap)][b]; GEMM over K = pixels with both
 // operands pixel-major in LDS; the 16-bit fragments are read with ds_read_b64_tr_b16 (hardware
 // transpose), f32 fragments with plain ds_read_b32.  Split over pixels, f32 atomic reduction.
+//
+// f32 layers (the 4^2..16^2 blocks, num_fp16_res=4) run by default as a three-way bf16 split ("S3"):
+// each f32 operand is staged into LDS as x = h + m + l (three bf16 planes, exact for normal
+// numbers), and the GEMM takes the six products h*h, h*m, m*h, h*l, l*h, m*m on the bf16 MFMA with
+// f32 accumulation.  The dropped terms (m*l, l*m, l*l) are O(2^-24) of each product, the size of
+// one f32 rounding, so the result has f32 accuracy (the reference disables TF32,
+// training_loop_mi_multimodal.py:169-170, and this keeps that contract) at 6 x 16 = 96 cycles per
+// 32-deep K step instead of 8 x 32 = 256 for v_mfma_f32_16x16x4_f32.  SG2_F32_EXACT=1 selects the
+// f32-input MFMA path instead.
 #include "sg2_common.h"
 
 #include <algorithm>
@@ -72,6 +81,39 @@ template <typename T> struct Traits;
 template <> struct Traits<float> {
     static constexpr int BK = 16, V = 4;
 };
+// K-stage of a kernel instance: 32 (one bf16 MFMA K) for the split-f32 form
+template <typename T, bool S3> struct KStage { static constexpr int BK = Traits<T>::BK; };
+template <> struct KStage<float, true> { static constexpr int BK = 32; };
+
+constexpr int S3LD = 32 + 8;          // bf16 plane row pitch (elements, 80 B: conflict-free b128 reads)
+
+// x = h + m + l, three bf16 pieces (exact for normal f32; round-to-nearest at each step)
+__device__ __forceinline__ void split3(float x, bf16_t& h, bf16_t& m, bf16_t& l) {
+    h = (bf16_t)x;
+    float r = x - (float)h;
+    m = (bf16_t)r;
+    r -= (float)m;
+    l = (bf16_t)r;
+}
+
+// acc += a * b over the six significant products of the split operands (small terms first)
+__device__ __forceinline__ f32x4 mfma_s3(const bf16x8* a, const bf16x8* b, f32x4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+}
+
+// f32 exact mode (SG2_F32_EXACT=1): the f32-input MFMA kernels instead of the bf16 split
+inline bool f32_exact() {
+    static const bool v = [] {
+        const char* e = getenv("SG2_F32_EXACT");
+        return e != nullptr && e[0] == '1';
+    }();
+    return v;
+}
 template <> struct Traits<f16_t> {
     static constexpr int BK = 32, V = 8;
 };
@@ -139,9 +181,10 @@ __device__ __forceinline__ float epi_full(const Epi& e, float c, int n, int o, i
 }
 
 // Implicit-GEMM convolution.  grid = (M tiles, Cout tiles, phases * splits).
-template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI>
-__global__ __launch_bounds__(256, 3) void conv_fwd_kernel(ConvArgs a) {
-    constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
+template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI, bool S3>
+__global__ __launch_bounds__(256, S3 ? 1 : 3) void conv_fwd_kernel(ConvArgs a) {
+    static_assert(!S3 || std::is_same<T, float>::value, "the split form is for f32 operands");
+    constexpr int BK = KStage<T, S3>::BK, V = Traits<T>::V;
     constexpr int LPR = BK / V;          // lanes per tile row
     constexpr int RPP = 256 / LPR;       // rows per load pass
     constexpr int PA = BM / RPP, PB = BN / RPP;
@@ -152,6 +195,9 @@ __global__ __launch_bounds__(256, 3) void conv_fwd_kernel(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     T* lds = (T*)smem_raw;               // [2][(BM + BN) * LDK], reused by the epilogue
     constexpr int BUF = (BM + BN) * LDK;
+    // split form: [2][3 planes][(BM + BN) rows][S3LD] bf16
+    bf16_t* lds3 = (bf16_t*)smem_raw;
+    constexpr int PLANE = (BM + BN) * S3LD, BUF3 = 3 * PLANE;
 
     const int phase = blockIdx.z / a.splits, split = blockIdx.z - phase * a.splits;
     const int QH = a.ph[phase].QH, QW = a.ph[phase].QW, M = a.ph[phase].M;
@@ -216,6 +262,21 @@ __global__ __launch_bounds__(256, 3) void conv_fwd_kernel(ConvArgs a) {
             rb[i] = Loader<T, VEC>::load(row, c, a.Cin);
         }
     };
+    typedef bf16_t bf16x4_t __attribute__((ext_vector_type(4)));
+    // split-f32 staging: row r of the buffer (A rows first, then B) gets the three planes of v
+    auto store3 = [&](int buf, int r, const vecT& v) {
+        bf16x4_t h, m, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bf16_t a_, b_, c_;
+            split3((float)v[j], a_, b_, c_);
+            h[j] = a_; m[j] = b_; l[j] = c_;
+        }
+        bf16_t* p = lds3 + buf * BUF3 + r * S3LD + lcol;
+        *(bf16x4_t*)p = h;
+        *(bf16x4_t*)(p + PLANE) = m;
+        *(bf16x4_t*)(p + 2 * PLANE) = l;
+    };
     auto sstore = [&](int buf) {
         T* As = lds + buf * BUF;
         T* Bs = As + BM * LDK;
@@ -226,11 +287,15 @@ __global__ __launch_bounds__(256, 3) void conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
                 for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * rsc[i][j]);
             }
-            *(vecT*)(As + (lrow + i * RPP) * LDK + lcol) = v;
+            if constexpr (S3) store3(buf, lrow + i * RPP, v);
+            else *(vecT*)(As + (lrow + i * RPP) * LDK + lcol) = v;
         }
 #pragma unroll
-        for (int i = 0; i < PB; ++i)
-            *(vecT*)(Bs + (lrow + i * RPP) * LDK + lcol) = Loader<T, VEC>::mask(rb[i], cur_c, a.Cin, rb_ok[i]);
+        for (int i = 0; i < PB; ++i) {
+            const vecT v = Loader<T, VEC>::mask(rb[i], cur_c, a.Cin, rb_ok[i]);
+            if constexpr (S3) store3(buf, BM + lrow + i * RPP, v);
+            else *(vecT*)(Bs + (lrow + i * RPP) * LDK + lcol) = v;
+        }
     };
 
     f32x4 acc[TM][TN];
@@ -249,7 +314,24 @@ __global__ __launch_bounds__(256, 3) void conv_fwd_kernel(ConvArgs a) {
             if (more) gload(kc + 1);
             const T* As = lds + cur * BUF + (wm * WM) * LDK;
             const T* Bs = lds + cur * BUF + BM * LDK + (wn * WN) * LDK;
-            if constexpr (std::is_same<T, float>::value) {
+            if constexpr (S3) {
+                const bf16_t* P = lds3 + cur * BUF3;
+                const int ko = 8 * (lane >> 4);
+                bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+                        af[i][q] = *(const bf16x8*)(P + q * PLANE + (wm * WM + i * 16 + (lane & 15)) * S3LD + ko);
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        bfr[j][q] = *(const bf16x8*)(P + q * PLANE + (BM + wn * WN + j * 16 + (lane & 15)) * S3LD + ko);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma_s3(af[i], bfr[j], acc[i][j]);
+            } else if constexpr (std::is_same<T, float>::value) {
 #pragma unroll
                 for (int kk = 0; kk < BK; kk += 4) {
                     float af[TM], bfr[TN];
@@ -450,18 +532,19 @@ __global__ void conv_finalize_kernel(T* y, const float* src, Epi e, int64_t n_el
     }
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool S3>
 size_t fwd_lds_bytes() {
     constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
+    if (S3) return 2 * 3 * (size_t)(BM + BN) * S3LD * sizeof(bf16_t);
     const size_t main = 2 * (size_t)(BM + BN) * (BK + V) * sizeof(T);
     const size_t epi = std::is_same<T, float>::value ? 0 : 2 * (size_t)BM * (64 + 8) * sizeof(T) + 64 * sizeof(float);
     return std::max(main, epi);
 }
 
-template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI>
+template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI, bool S3>
 int launch_fwd_k(ConvArgs& a, dim3 grid, hipStream_t s) {
-    auto kern = conv_fwd_kernel<T, BM, BN, VEC, SPLIT, SI>;
-    const size_t lds = fwd_lds_bytes<T, BM, BN>();
+    auto kern = conv_fwd_kernel<T, BM, BN, VEC, SPLIT, SI, S3>;
+    const size_t lds = fwd_lds_bytes<T, BM, BN, S3>();
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -478,8 +561,16 @@ int launch_fwd(ConvArgs& a, bool vec, hipStream_t s) {
     for (int i = 0; i < kMaxPhases; ++i)
         if (a.ph[i].M > 0) { maxM = std::max(maxM, a.ph[i].M); nph = i + 1; }
     dim3 grid((unsigned)cdiv(maxM, BM), (unsigned)cdiv(a.Cout, BN), (unsigned)(nph * a.splits));
-#define LF(V_, S_) return a.in_scale ? launch_fwd_k<T, BM, BN, V_, S_, true>(a, grid, s) \
-                                     : launch_fwd_k<T, BM, BN, V_, S_, false>(a, grid, s)
+    constexpr bool F32 = std::is_same<T, float>::value;
+    if (F32 && !f32_exact()) {
+#define LF(V_, S_) return a.in_scale ? launch_fwd_k<T, BM, BN, V_, S_, true, F32>(a, grid, s) \
+                                     : launch_fwd_k<T, BM, BN, V_, S_, false, F32>(a, grid, s)
+        if (a.splits > 1) { if (vec) LF(true, true); else LF(false, true); }
+        if (vec) LF(true, false); else LF(false, false);
+#undef LF
+    }
+#define LF(V_, S_) return a.in_scale ? launch_fwd_k<T, BM, BN, V_, S_, true, false>(a, grid, s) \
+                                     : launch_fwd_k<T, BM, BN, V_, S_, false, false>(a, grid, s)
     if (a.splits > 1) { if (vec) LF(true, true); else LF(false, true); }
     if (vec) LF(true, false); else LF(false, false);
 #undef LF
@@ -511,17 +602,38 @@ __device__ __forceinline__ v8_t<T> frag_tr(const T* base, int ld, int k0, int c0
     return __builtin_bit_cast(v8_t<T>, r);
 }
 
-template <typename T, int BM, int BN, bool VEC>
+template <typename T, int BM, int BN, bool VEC, bool S3>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
-    constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
+    static_assert(!S3 || std::is_same<T, float>::value, "the split form is for f32 operands");
+    constexpr int BK = KStage<T, S3>::BK, V = Traits<T>::V;
     constexpr int LDA = BM + V, LDB = BN + V;   // padded pixel-major rows
     constexpr int LPA = BM / V, LPB = BN / V;   // lanes per row
     constexpr int RPA = 256 / LPA, RPB = 256 / LPB;
     constexpr int PA = (BK + RPA - 1) / RPA, PB = (BK + RPB - 1) / RPB;
     constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
     typedef typename Loader<T, VEC>::vecT vecT;
+    // split form: [2][3 planes][BK][LDA3 + LDB3] bf16, pixel-major, read with ds_read_b64_tr_b16
+    constexpr int LDA3 = BM + 8, LDB3 = BN + 8, PL3 = BK * (LDA3 + LDB3);
+    constexpr size_t BYTES = S3 ? 2 * 3 * (size_t)PL3 * 2 : 2 * (size_t)BK * (LDA + LDB) * sizeof(T);
 
-    __shared__ __attribute__((aligned(16))) T lds[2][BK * (LDA + LDB)];
+    __shared__ __attribute__((aligned(16))) char lds_raw[BYTES];
+    typedef T Row[BK * (LDA + LDB)];
+    Row* lds = (Row*)lds_raw;
+    bf16_t* lds3 = (bf16_t*)lds_raw;
+    typedef bf16_t bf16x4_t __attribute__((ext_vector_type(4)));
+    auto store3 = [&](int buf, int off, const vecT& v) {
+        bf16x4_t h, m, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bf16_t a_, b_, c_;
+            split3((float)v[j], a_, b_, c_);
+            h[j] = a_; m[j] = b_; l[j] = c_;
+        }
+        bf16_t* p = lds3 + buf * 3 * PL3 + off;
+        *(bf16x4_t*)p = h;
+        *(bf16x4_t*)(p + PL3) = m;
+        *(bf16x4_t*)(p + 2 * PL3) = l;
+    };
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -597,7 +709,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
                 for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * asc[i][j]);
             }
-            if (r < BK) *(vecT*)(As + r * LDA + ga_col) = v;
+            if constexpr (S3) {
+                if (r < BK) store3(buf, r * LDA3 + ga_col, v);
+            } else {
+                if (r < BK) *(vecT*)(As + r * LDA + ga_col) = v;
+            }
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
@@ -607,7 +723,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
                 for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * rsc[i][j]);
             }
-            if (r < BK) *(vecT*)(Bs + r * LDB + xb_col) = v;
+            if constexpr (S3) {
+                if (r < BK) store3(buf, BK * LDA3 + r * LDB3 + xb_col, v);
+            } else {
+                if (r < BK) *(vecT*)(Bs + r * LDB + xb_col) = v;
+            }
         }
     };
 
@@ -628,7 +748,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
             if (more) gload(p0 + BK);
             const T* As = lds[cur];
             const T* Bs = lds[cur] + BK * LDA;
-            if constexpr (std::is_same<T, float>::value) {
+            if constexpr (S3) {
+                const bf16_t* P = lds3 + cur * 3 * PL3;
+                bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) af[i][q] = frag_tr<bf16_t>(P + q * PL3, LDA3, 0, wm * WM + i * 16, lane);
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        bfr[j][q] = frag_tr<bf16_t>(P + q * PL3 + BK * LDA3, LDB3, 0, wn * WN + j * 16, lane);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma_s3(af[i], bfr[j], acc[i][j]);
+            } else if constexpr (std::is_same<T, float>::value) {
 #pragma unroll
                 for (int kk = 0; kk < BK; kk += 4) {
                     float af[TM], bfr[TN];
@@ -675,7 +810,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 
 template <typename T, int BM, int BN>
 int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
-    constexpr int BK = Traits<T>::BK;
+    constexpr bool F32 = std::is_same<T, float>::value;
+    const bool s3 = F32 && !f32_exact();
+    const int BK = s3 ? KStage<float, true>::BK : Traits<T>::BK;
     const int mt = (int)cdiv(a.A, BM), nt = (int)cdiv(a.B, BN);
     const int KK = a.KH * a.KW;
     const int chunks = (int)cdiv(a.M, BK);
@@ -683,8 +820,13 @@ int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
     a.kper = (int)cdiv(chunks, splits) * BK;
     a.splits = (int)cdiv(a.M, a.kper);
     dim3 grid(mt, nt, KK * a.splits);
-    if (vec) conv_wgrad_kernel<T, BM, BN, true><<<grid, 256, 0, s>>>(a);
-    else conv_wgrad_kernel<T, BM, BN, false><<<grid, 256, 0, s>>>(a);
+    if (s3) {
+        if (vec) conv_wgrad_kernel<T, BM, BN, true, F32><<<grid, 256, 0, s>>>(a);
+        else conv_wgrad_kernel<T, BM, BN, false, F32><<<grid, 256, 0, s>>>(a);
+    } else {
+        if (vec) conv_wgrad_kernel<T, BM, BN, true, false><<<grid, 256, 0, s>>>(a);
+        else conv_wgrad_kernel<T, BM, BN, false, false><<<grid, 256, 0, s>>>(a);
+    }
     return launch_status("sg2_conv2d_wgrad");
 }
 
@@ -777,7 +919,8 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
 
     int rc = 0;
     SG2_DISPATCH(dtype, T, {
-        constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
+        constexpr int V = Traits<T>::V;
+        const int BK = (std::is_same<T, float>::value && !f32_exact()) ? KStage<float, true>::BK : Traits<T>::BK;
         const bool vec = (Cin % V == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)w % 16 == 0);
         const bool wide = Cout > 64;
         const int BN_ = wide ? 128 : 64;

@@ -1,0 +1,70 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench line, rocprofv3 kernel-trace summary of the bench command,
+# and the HBM-traffic PMC passes of the roofline kernel.  Every GPU step has its own time limit and
+# the first failure ends the script.
+#   gpurun --timeout 1100 -- 'bash tools/gpu_round.sh <tag> [steps...]'   (steps: test smoke bench prof pmc)
+TAG=${1:-run}
+shift
+STEPS=${*:-"test bench prof pmc"}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=/tmp
+cd /tmp || exit 1
+
+step() { case " $STEPS " in *" $1 "*) return 0 ;; esac; return 1; }
+
+if step test; then
+    echo "== pytest -m gpu"
+    (cd "$R" && timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+        > "$O/pytest_gpu.log" 2>&1)
+    rc=$?; tail -3 "$O/pytest_gpu.log"; [ $rc -eq 0 ] || exit $rc
+fi
+if step smoke; then
+    echo "== smoke"
+    (cd "$R" && timeout -k 10 300 python -u __graft_entry__.py smoke > "$O/smoke.log" 2>&1)
+    rc=$?; tail -2 "$O/smoke.log"; [ $rc -eq 0 ] || exit $rc
+fi
+if step bench; then
+    echo "== bench"
+    (cd "$R" && timeout -k 10 400 python -u bench.py > "$O/bench.log" 2>&1)
+    rc=$?; tail -1 "$O/bench.log"; [ $rc -eq 0 ] || exit $rc
+fi
+if step parts; then
+    echo "== part timing"
+    (cd "$R" && timeout -k 10 300 python -u tools/part_timing.py > "$O/parts.log" 2>&1)
+    rc=$?; cat "$O/parts.log" | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc
+fi
+if step prof; then
+    echo "== rocprofv3 kernel trace of the bench command"
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv \
+        -- python3 "$R/bench.py" --no-cpu-baseline > "$O/prof_bench.log" 2>&1
+    rc=$?; tail -1 "$O/prof_bench.log"; [ $rc -eq 0 ] || exit $rc
+    f=$(find "$O/prof" -name 'run_kernel_stats.csv' | head -1)
+    python3 "$R/profiles/prof_summary.py" "$(dirname "$f")" 45 > "$O/prof_summary.txt" 2>&1
+    head -50 "$O/prof_summary.txt"
+fi
+if step pmc; then
+    # HBM bytes of the roofline kernel: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots).
+    for c in FETCH_SIZE WRITE_SIZE; do
+        echo "== pmc $c"
+        timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex conv3x3_halo -d "$O/pmc_$c" -o run \
+            --output-format csv -- python3 "$R/tools/roofline_only.py" > "$O/pmc_$c.log" 2>&1
+        rc=$?; tail -1 "$O/pmc_$c.log"; [ $rc -eq 0 ] || exit $rc
+    done
+    python3 "$R/tools/pmc_traffic.py" "$O" > "$O/pmc_traffic.txt" 2>&1; cat "$O/pmc_traffic.txt"
+fi
+if step diag; then
+    # where the halo conv waves wait (one pass, 8 SQ counters; MI355X_MICROARCH.md rocprofv3 PMC slots)
+    echo "== pmc diag halo"
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-include-regex 'conv3x3_halo|conv_fwd|wgrad' \
+        -d "$O/diag" -o run --output-format csv -- python3 "$R/tools/conv_micro.py" --reps 3 > "$O/diag.log" 2>&1
+    rc=$?; tail -5 "$O/diag.log"; [ $rc -eq 0 ] || exit $rc
+fi
+if step micro; then
+    echo "== conv micro"
+    (cd "$R" && timeout -k 10 300 python -u tools/conv_micro.py > "$O/micro.log" 2>&1)
+    rc=$?; grep -v amdgpu.ids "$O/micro.log"; [ $rc -eq 0 ] || exit $rc
+fi
+echo "== done"
