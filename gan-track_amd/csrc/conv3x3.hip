@@ -321,7 +321,11 @@ int dispatch(Conv3Args& a, hipStream_t s) {
     const int TW = a.W >= 32 ? 32 : 16;
     a.tiles_x = (a.W + TW - 1) / TW;
     a.tiles_y = (a.H + (256 / TW) - 1) / (256 / TW);
-    const int nbuf = (a.Cin <= 2 * CK) ? 1 : 2;
+    static const int force_nbuf = [] { const char* e = getenv("SG2_HALO_NBUF"); return e ? atoi(e) : 0; }();
+    // one LDS buffer per workgroup: two workgroups per CU (2 waves / SIMD) hide each other's staging and
+    // load latency; measured 1.3-1.4x faster than a double-buffered single workgroup per CU at C >= 128
+    // (gpurun_out/nbuf.log; SG2_HALO_NBUF=2 selects the double-buffered form)
+    const int nbuf = force_nbuf ? force_nbuf : 1;
 #define L3(TWV, SIV, EPIV) return nbuf == 1 ? launch3<T, TWV, SIV, EPIV, 1>(a, s) : launch3<T, TWV, SIV, EPIV, 2>(a, s)
     if (TW == 32) {
         if (si) { if (epi) L3(32, true, true); else L3(32, true, false); }

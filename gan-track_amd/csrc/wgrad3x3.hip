@@ -31,7 +31,16 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x8w __attribute__((ext_vector_type(8)));
 
 constexpr int BC = 64;          // channels per block in a and in b
-constexpr int LD = BC + 8;      // LDS row pitch (elements) of both tiles
+constexpr int LDP = BC + 8;     // padded LDS row pitch (elements), SWZ = false
+// SWZ = true: 128-B unpadded rows whose 32-channel halves swap when bit 1 of the row is set, so the four
+// rows of a ds_read_b64_tr_b16 block hit disjoint banks (rows r and r + 2 share a bank half and always
+// differ in that bit); 75.5 KB of LDS instead of 86 KB
+template <bool SWZ> struct Lay {
+    static constexpr int LD = SWZ ? BC : LDP;
+    static __device__ __forceinline__ int off(int row, int col) {
+        return row * LD + (SWZ ? (col ^ (((row >> 1) & 1) << 5)) : col);
+    }
+};
 
 struct PTap { int8_t dy, dx, out, pad_; };   // shift on the phase grid, output tap index
 
@@ -62,19 +71,20 @@ __device__ __forceinline__ f32x16 mma32(v8w<T> a, v8w<T> b, f32x16 c) {
 // 32x32x16 operand fragment from a row-major (pixel-major) LDS tile: lane l gets column c0 + (l & 31)
 // at rows row0 + j, j = 0..7, where row0 already includes the 8 * (l >> 5) half offset.
 // ds_read_b64_tr_b16 transposes a 4-row x 16-column block inside each 16-lane group.
-template <typename T>
+template <typename T, bool SWZ>
 __device__ __forceinline__ v8w<T> frag32(const T* tile, int row0, int c0, int lane) {
     const int G = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-    const T* p0 = tile + (row0 + q) * LD + c0 + 16 * (G & 1) + 4 * p;
-    const T* p1 = p0 + 4 * LD;
+    const T* p0 = tile + Lay<SWZ>::off(row0 + q, c0 + 16 * (G & 1) + 4 * p);
+    const T* p1 = p0 + 4 * Lay<SWZ>::LD;       // row + 4 keeps the swizzle bit
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p0);
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p1);
     s16x8w r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(v8w<T>, r);
 }
 
-template <typename T, int TW, int NT>
+template <typename T, int TW, int NT, bool SWZ>
 __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
+    constexpr int LD = Lay<SWZ>::LD;
     constexpr int TH = 256 / TW;
     constexpr int HWD = TW + 2, HP = HWD * (TH + 2);     // halo width / pixels (g-grid coordinates)
     constexpr int GCH = 8;                               // g: 256 px x 8 chunks / 256 threads
@@ -138,7 +148,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
                 if (a.gscale) f *= gsc[j];
                 v[j] = (T)f;
             }
-            *(vec8*)(gs + ((tid >> 3) + i * 32) * LD + cc) = v;
+            *(vec8*)(gs + Lay<SWZ>::off((tid >> 3) + i * 32, cc)) = v;
         }
 #pragma unroll
         for (int i = 0; i < XCH; ++i) {
@@ -150,7 +160,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
                 if (a.xscale) f *= xsc[j];
                 v[j] = (T)f;
             }
-            if (hp < HP) *(vec8*)(xs + hp * LD + cc) = v;
+            if (hp < HP) *(vec8*)(xs + Lay<SWZ>::off(hp, cc)) = v;
         }
     };
 
@@ -176,11 +186,11 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
                 // this lane's 8 pixels: k0 + 8 * (lane >> 5) + j, all in one tile row
                 const int pr = k0 + 8 * ((lane >> 4) >> 1);
                 const int py = pr / TW, px = pr % TW;
-                const v8w<T> fa = frag32<T>(gs, pr, wa * 32, lane);
+                const v8w<T> fa = frag32<T, SWZ>(gs, pr, wa * 32, lane);
                 const int hb = py * HWD + px;
 #pragma unroll
                 for (int tp = 0; tp < NT; ++tp) {
-                    const v8w<T> fb = frag32<T>(xs, hb + toff[tp], wb * 32, lane);
+                    const v8w<T> fb = frag32<T, SWZ>(xs, hb + toff[tp], wb * 32, lane);
                     acc[tp] = mma32<T>(fa, fb, acc[tp]);
                 }
             }
@@ -208,7 +218,9 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
 
 template <typename T, int TW, int NT>
 void launch_w3(const W3Args& a, dim3 grid, hipStream_t s) {
-    wgrad3x3_kernel<T, TW, NT><<<grid, 256, 0, s>>>(a);
+    static const bool swz = [] { const char* e = getenv("SG2_WGRAD_SWZ"); return e != nullptr && e[0] == '1'; }();
+    if (swz) wgrad3x3_kernel<T, TW, NT, true><<<grid, 256, 0, s>>>(a);
+    else wgrad3x3_kernel<T, TW, NT, false><<<grid, 256, 0, s>>>(a);
 }
 
 template <typename T, int TW>

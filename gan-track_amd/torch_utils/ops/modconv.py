@@ -157,9 +157,13 @@ def _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c
     dt = x.dtype
     dz = _ba.bias_act_grad(dy, zsrc, act=_ACT[act], alpha=alpha, gain=gain, clamp=clamp)
     dx = ds = dw = dd = dnoise = db = None
-    if need[5] and bias is not None:
+    # Under no_weight_gradients() (the path-length pass, loss.py pl_no_weight_grad) the caller asks for
+    # input gradients only (autograd.grad(..., inputs=[ws])): the parameter gradients db / dnoise would
+    # be computed and discarded, and -- being differentiable -- add their own double-backward nodes.
+    param_grads = not _cg.weight_gradients_disabled
+    if need[5] and bias is not None and param_grads:
         db = dz.sum([0, 2, 3], dtype=torch.float32).to(bias.dtype)
-    if need[4] and noise is not None:
+    if need[4] and noise is not None and param_grads:
         dnoise = dz.sum(1, keepdim=True, dtype=torch.float32).to(noise.dtype)
     s_ = styles.to(dt).reshape(n, -1, 1, 1) if styles is not None else None
     if need[3] and dcoefs is not None:
@@ -272,9 +276,10 @@ class UpModConv(torch.autograd.Function):
                 dw = _cg._wgrad_raw(x, dt_, kh, kw, 2, tpad, g_scale=s32).transpose(0, 1).to(weight.dtype)
         else:
             dz = _ba.bias_act_grad(dy, y, act='lrelu', alpha=alpha, gain=gain, clamp=clamp)
-            if need[5] and bias is not None:
+            param_grads = not _cg.weight_gradients_disabled      # see _composed_backward
+            if need[5] and bias is not None and param_grads:
                 db = dz.sum([0, 2, 3], dtype=torch.float32)
-            if need[4] and noise is not None:
+            if need[4] and noise is not None and param_grads:
                 dn = dz.sum(1, keepdim=True, dtype=torch.float32)
             s_ = styles.to(dt).reshape(n, -1, 1, 1)
             xs = x * s_
