@@ -110,6 +110,7 @@ __global__ __launch_bounds__(256) void reflect_pad_kernel(float* y, const float*
         const int px = (int)(i % Ws);
         const int py = (int)((i / Ws) % Hs);
         const int64_t nc = i / ((int64_t)Ws * Hs);
+        if (py >= Hd + 64 || px >= Wd + 64) continue;      // never read (upfirdn2d.hip UpfParams::lim)
         float v = 0.f;
         if (py < Hd && px < Wd) v = x[(nc * H + reflect1(py - my0, H)) * W + reflect1(px - mx0, W)];
         y[i] = v;
@@ -138,6 +139,20 @@ __global__ __launch_bounds__(256) void reflect_pad_adj_kernel(float* gx, const f
         for (int a = 0; a < ny; ++a)
             for (int c = 0; c < nx; ++c) acc += b[(int64_t)ys[a] * Ws + xs[c]];
         gx[i] = acc;
+    }
+}
+
+// Zero rows < dyn_h + band and cols < dyn_w + band of the [N, C, Hi, Wi] gradient buffer (strides is_*).
+__global__ __launch_bounds__(256) void zero_region_kernel(float* g, GSParams p, const int* dyn_hw, int band) {
+    const int hl = min(p.Hi, dyn_hw[0] + band), wl = min(p.Wi, dyn_hw[1] + band);
+    const int64_t total = (int64_t)p.N * p.C * p.Hi * p.Wi;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int x = (int)(i % p.Wi);
+        const int y = (int)((i / p.Wi) % p.Hi);
+        const int64_t nc = i / ((int64_t)p.Wi * p.Hi);
+        if (y >= hl || x >= wl) continue;
+        const int c = (int)(nc % p.C), n = (int)(nc / p.C);
+        g[n * p.is_n + c * p.is_c + y * p.is_h + x * p.is_w] = 0.f;
     }
 }
 
@@ -181,8 +196,18 @@ extern "C" int sg2_grid_sample_bwd(float* gin, const void* gout, const float* gr
     // zero the float32 input-gradient buffer (dense over the strided extent)
     const int64_t extent = (p.N - 1) * p.is_n + (p.C - 1) * p.is_c + (p.Hi - 1) * p.is_h + (p.Wi - 1) * p.is_w + 1;
     hipStream_t s = as_stream(stream);
-    hipError_t e = hipMemsetAsync(gin, 0, extent * sizeof(float), s);
-    if (e != hipSuccess) { set_error("sg2_grid_sample_bwd: memset failed"); return (int)e; }
+    if (dyn_hw) {
+        // only the region a consumer of the dynamically sized gradient reads: the logical image plus a
+        // band (upfirdn2d.hip kZeroBand and the adjoint FIR's reach)
+        const int64_t tot = (int64_t)p.N * p.C * p.Hi * p.Wi;
+        const int g = (int)std::min<int64_t>(cdiv(tot, 256), 256 * 64);
+        zero_region_kernel<<<g, 256, 0, s>>>(gin, p, dyn_hw, 96);
+        int rc = launch_status("sg2_grid_sample_bwd zero");
+        if (rc) return rc;
+    } else {
+        hipError_t e = hipMemsetAsync(gin, 0, extent * sizeof(float), s);
+        if (e != hipSuccess) { set_error("sg2_grid_sample_bwd: memset failed"); return (int)e; }
+    }
     const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
     if (total == 0 || p.C == 0) return 0;
     const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 32);

@@ -38,7 +38,14 @@ struct UpfParams {
     void* aux;                // like y
     float noise_gain, alpha, egain, clamp;
     int act, aux_mode, epi;
+    // optional device int[2] output extent (rows, cols) of a dynamically sized image in a static buffer
+    // (the ADA pipe): outputs below it are computed, outputs in the kZeroBand rows/cols beyond it are
+    // written as zeros (their exact value: the image's support ends inside the extent), the rest of the
+    // static buffer is left untouched -- no consumer reads it.  Generic kernel only.
+    const int* lim;
 };
+
+constexpr int kZeroBand = 32;
 
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 
@@ -77,6 +84,14 @@ __global__ __launch_bounds__(256) void upfirdn_generic(UpfParams p) {
         const int oy = (int)(r % p.OH); r /= p.OH;
         const int c = (int)(r % p.C); r /= p.C;
         const int n = (int)r;
+        if (p.lim) {
+            const int ly = p.lim[0], lx = p.lim[1];
+            if (oy >= ly + kZeroBand || ox >= lx + kZeroBand) continue;
+            if (oy >= ly || ox >= lx) {
+                y[n * p.ys_n + c * p.ys_c + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w] = (T)0.f;
+                continue;
+            }
+        }
         int ty0, iy0, tx0, ix0;
         axis_taps(oy, p.downy, p.pady0, p.upy, ty0, iy0);
         axis_taps(ox, p.downx, p.padx0, p.upx, tx0, ix0);
@@ -295,7 +310,7 @@ extern "C" int sg2_upfirdn2d_fused(void* y, const void* x, const float* f, int d
     p.xs_n = in_stride[0]; p.xs_c = in_stride[1]; p.xs_h = in_stride[2]; p.xs_w = in_stride[3];
     p.ys_n = out_stride[0]; p.ys_c = out_stride[1]; p.ys_h = out_stride[2]; p.ys_w = out_stride[3];
     p.fw = fw; p.fh = fh; p.upx = upx; p.upy = upy; p.downx = downx; p.downy = downy;
-    p.padx0 = padx0; p.pady0 = pady0; p.flip = flip; p.gain = gain;
+    p.padx0 = padx0; p.pady0 = pady0; p.flip = flip; p.gain = gain; p.lim = nullptr;
     p.out_scale = nullptr; p.noise = nullptr; p.bias = nullptr; p.residual = nullptr; p.aux = nullptr;
     p.noise_gain = 0.f; p.alpha = 0.f; p.egain = 1.f; p.clamp = -1.f; p.act = 0; p.aux_mode = 0; p.epi = 0;
     if (epi) {
@@ -317,6 +332,32 @@ extern "C" int sg2_upfirdn2d_fused(void* y, const void* x, const float* f, int d
         SG2_CHECK(vec || !p.epi, "sg2_upfirdn2d: the fused epilogue needs NHWC activations with C % 8 == 0");
         return launch<T>(p, vec, s);
     });
+    return 0;
+}
+
+extern "C" int sg2_upfirdn2d_lim(void* y, const void* x, const float* f, int dtype, const int64_t* in_size,
+                                 const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride, int fw,
+                                 int fh, int upx, int upy, int downx, int downy, int padx0, int padx1, int pady0,
+                                 int pady1, int flip, float gain, const int* lim, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(x && y && f && in_size && in_stride && out_size && out_stride, "sg2_upfirdn2d: null argument");
+    SG2_CHECK(upx >= 1 && upy >= 1 && downx >= 1 && downy >= 1, "sg2_upfirdn2d: up/down must be >= 1");
+    SG2_CHECK(fw >= 1 && fh >= 1 && fw * fh <= kMaxTaps, "sg2_upfirdn2d: filter too large");
+    UpfParams p{};
+    p.x = x; p.y = y; p.f = f; p.lim = lim;
+    p.N = (int)in_size[0]; p.C = (int)in_size[1]; p.H = (int)in_size[2]; p.W = (int)in_size[3];
+    p.OH = (int)out_size[2]; p.OW = (int)out_size[3];
+    SG2_CHECK(out_size[0] == p.N && out_size[1] == p.C, "sg2_upfirdn2d: batch/channel mismatch");
+    const int64_t eh = ((int64_t)p.H * upy + pady0 + pady1 - fh + downy) / downy;
+    const int64_t ew = ((int64_t)p.W * upx + padx0 + padx1 - fw + downx) / downx;
+    SG2_CHECK(eh == p.OH && ew == p.OW, "sg2_upfirdn2d: output size mismatch");
+    p.xs_n = in_stride[0]; p.xs_c = in_stride[1]; p.xs_h = in_stride[2]; p.xs_w = in_stride[3];
+    p.ys_n = out_stride[0]; p.ys_c = out_stride[1]; p.ys_h = out_stride[2]; p.ys_w = out_stride[3];
+    p.fw = fw; p.fh = fh; p.upx = upx; p.upy = upy; p.downx = downx; p.downy = downy;
+    p.padx0 = padx0; p.pady0 = pady0; p.flip = flip; p.gain = gain; p.egain = 1.f; p.clamp = -1.f;
+    if ((int64_t)p.N * p.C * p.OH * p.OW == 0) return 0;
+    hipStream_t s = as_stream(stream);
+    SG2_DISPATCH(dtype, T, { return launch<T>(p, false, s); });
     return 0;
 }
 

@@ -81,6 +81,60 @@ def _raw(x, f2, upx, upy, downx, downy, px0, px1, py0, py1, flip, gain):
     return y
 
 
+def _raw_lim(x, f2, upx, upy, downx, downy, px0, px1, py0, py1, flip, gain, lim):
+    """sg2_upfirdn2d_lim: outputs beyond the device extent `lim` (int32 [2]) are zero-banded / skipped."""
+    n, c, h, w = x.shape
+    fh, fw = f2.shape
+    oh = (h * upy + py0 + py1 - fh + downy) // downy
+    ow = (w * upx + px0 + px1 - fw + downx) // downx
+    y = torch.empty([n, c, oh, ow], dtype=x.dtype, device=x.device)
+    _hip.check(_hip.lib().sg2_upfirdn2d_lim(
+        _hip.ptr(y), _hip.ptr(x), _hip.ptr(f2), _hip.dtype_code(x), _hip.i64arr(x.shape), _hip.i64arr(x.stride()),
+        _hip.i64arr(y.shape), _hip.i64arr(y.stride()), fw, fh, upx, upy, downx, downy, px0, px1, py0, py1,
+        int(bool(flip)), float(gain), _hip.ptr(lim), _hip.stream_ptr(x.device)), 'sg2_upfirdn2d_lim')
+    return y
+
+
+class _SepLimited(torch.autograd.Function):
+    """Separable upfirdn2d of a dynamically sized image held in a static buffer (the ADA pipe,
+    augment_mi.py): the horizontal pass computes outputs inside extent lims[0], the vertical pass inside
+    lims[1]; the backward (the adjoint, again separable) uses lims[2], lims[3], and its own backward the
+    forward's.  Exact wherever a consumer reads (see UpfParams::lim in upfirdn2d.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, f, up, down, padding, flip_filter, gain, lims):
+        upx, upy = up
+        downx, downy = down
+        px0, px1, py0, py1 = padding
+        x = x.contiguous()
+        y = _raw_lim(x, f.unsqueeze(0), upx, 1, downx, 1, px0, px1, 0, 0, flip_filter, 1.0, lims[0])
+        y = _raw_lim(y, f.unsqueeze(1), 1, upy, 1, downy, 0, 0, py0, py1, flip_filter, gain, lims[1])
+        ctx.save_for_backward(f)
+        ctx.cfg = (up, down, padding, flip_filter, gain, lims, x.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        f, = ctx.saved_tensors
+        up, down, padding, flip_filter, gain, lims, xs = ctx.cfg
+        aup, adown, p, aflip = adjoint_params(f, (xs[2], xs[3]), (dy.shape[2], dy.shape[3]), list(up), list(down),
+                                              list(padding), flip_filter)
+        dx = _SepLimited.apply(dy, f, tuple(aup), tuple(adown), tuple(p), aflip, gain,
+                               (lims[2], lims[3], lims[0], lims[1]))
+        return dx, None, None, None, None, None, None, None
+
+
+def upsample2d_limited(x, f, lims, up=2, gain=1):
+    """upsample2d (1-D separable filter, f32 NCHW) computing only inside device extents `lims` (four
+    int32 [2] tensors: forward horizontal / vertical pass, backward horizontal / vertical pass)."""
+    _hip.require_device(x)
+    assert f.ndim == 1 and x.dtype == torch.float32
+    fw = f.shape[0]
+    p = [(fw + up - 1) // 2, (fw - up) // 2] * 2
+    return _SepLimited.apply(x, f.to(device=x.device, dtype=torch.float32).contiguous(), (up, up), (1, 1),
+                             tuple(p), False, float(gain * up * up), tuple(lims))
+
+
 def fir_fused(x, f2, padding, gain=1.0, flip_filter=False, out_scale=None, noise=None, noise_gain=1.0, bias=None,
               act=0, alpha=0.2, act_gain=1.0, clamp=-1.0, aux_mode=0):
     """2-D FIR (up = down = 1) with the fused layer epilogue (sg2_upfirdn2d_fused):

@@ -204,7 +204,12 @@ class AugmentPipe(torch.nn.Module):
         # sync, so the step can be graph-captured (torch_utils/ops/reflect_pad.py).
         images = reflect_pad.reflect_pad_dyn(images, mi)
         G = translate2d((mx0 - mx1) / 2, (my0 - my1) / 2) @ G
-        images = upfirdn2d.upsample2d(x=images, f=self.Hz_geom, up=2)
+        # extents (rows, cols) the up-sampling passes and their adjoints compute: the logical image plus
+        # the filter reach (upfirdn2d.upsample2d_limited; the rest of the static buffer is never read)
+        hd, wd = mi[1] + mi[3] + h, mi[0] + mi[2] + w
+        lims = torch.stack([hd + 32, 2 * wd + 32, 2 * hd + 32, 2 * wd + 32,
+                            2 * hd + 96, wd + 32, hd + 32, wd + 32]).to(torch.int32).reshape(4, 2)
+        images = upfirdn2d.upsample2d_limited(images, self.Hz_geom, lims.unbind(0), up=2)
         G = scale2d(2, 2, device=dev) @ G @ scale2d_inv(2, 2, device=dev)
         G = translate2d(-0.5, -0.5, device=dev) @ G @ translate2d_inv(-0.5, -0.5, device=dev)
         shape = [n, c, (h + hz_pad * 2) * 2, (w + hz_pad * 2) * 2]

@@ -71,6 +71,16 @@ int sg2_upfirdn2d(void* y, const void* x, const float* f, int dtype, const int64
                   int upx, int upy, int downx, int downy, int padx0, int padx1, int pady0, int pady1, int flip,
                   float gain, void* stream);
 
+/* sg2_upfirdn2d of a dynamically sized image held at the origin of a static buffer (the ADA pipe's padded
+ * image, augment_mi.py:288-321, whose size is data dependent): lim = device int[2] output extent (rows,
+ * cols).  Outputs inside it are computed, outputs within 32 rows / cols beyond it are written as zeros
+ * (exact when the image's support ends inside the extent), the rest of y is left unwritten.  Generic
+ * (any-stride) kernel. */
+int sg2_upfirdn2d_lim(void* y, const void* x, const float* f, int dtype, const int64_t* in_size,
+                      const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride, int fw, int fh,
+                      int upx, int upy, int downx, int downy, int padx0, int padx1, int pady0, int pady1, int flip,
+                      float gain, const int* lim, void* stream);
+
 /* sg2_upfirdn2d followed by the fused layer epilogue (sg2_epilogue, defined below) -- the FIR of
  * an up-2 synthesis layer with its demodulation, noise, bias, lrelu and clamp
  * (networks_stylegan2.py:68-76 + :325-327).  epi may be NULL; with an epilogue the activations
