@@ -673,3 +673,26 @@ def test_wgrad_halo_phases(dtype, case):
         dw = cg._wgrad_raw(g.to(dtype).contiguous(memory_format=torch.channels_last),
                            x.to(dtype).contiguous(memory_format=torch.channels_last), 1, 1, 1, (0, 0))
     assert rel_err(dw, ref) < (2e-3 if dtype == torch.float16 else 1e-2)
+
+
+@pytest.mark.parametrize('dp', [0.02, 0.5, 0.97])
+def test_augment_dynamic_extent(dp):
+    """ADA geometric pipe at 128^2, 2 channels: the padded image is dynamically sized inside static buffers
+    and the up-sampling passes / their adjoints / the grid-sample gradient only touch its extent
+    (upfirdn2d.upsample2d_limited, sg2_upfirdn2d_lim).  Forward, input gradient and the R1-style double
+    backward vs the CPU oracle (debug_percentile: deterministic transforms, small and large margins)."""
+    from training import augment_mi
+    cfg = dict(xflip=1, rotate90=1, xint=1, scale=1, rotate=1, aniso=1, xfrac=1)
+    torch.manual_seed(5)
+    x = torch.randn(3, 2, 128, 128)
+    dy = torch.randn(3, 2, 128, 128)
+    res = []
+    for dev, pipe in [(DEV, augment_mi.AugmentPipe(run_dir=None, batch_size=3, **cfg).to(DEV)),
+                      (torch.device('cpu'), O.AugmentPipe(**cfg))]:
+        xd = x.to(dev).requires_grad_(True)
+        y = pipe(xd, False, debug_percentile=dp)
+        g, = torch.autograd.grad((y * y).sum(), [xd], create_graph=True)       # 2 A^T A x
+        gg, = torch.autograd.grad((g * dy.to(dev)).sum(), [xd])                 # 2 A^T A dy
+        res.append([t.detach().double().cpu() for t in (y, g, gg)])
+    for a, b in zip(*res):
+        assert rel_err(a, b) < 2e-5
