@@ -173,7 +173,7 @@ __device__ __forceinline__ float epi_full(const Epi& e, float c, int n, int o, i
     float v = c;
     if (e.out_scale) v *= e.out_scale[(int64_t)n * Cout + o];
     if (e.noise) v += (float)((const T*)e.noise)[pix] * e.noise_gain;
-    if (e.bias) v += e.bias[o];
+    if (e.bias) v += (float)(T)e.bias[o];        // bias rounded to the activation dtype, as the reference
     if (e.act == 1) v = v > 0.f ? v : v * e.alpha;
     v *= e.gain;
     if (e.clamp >= 0.f) v = fminf(fmaxf(v, -e.clamp), e.clamp);
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(256, S3 ? 1 : 3) void conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int o = min(n0 + wn * WN + j * 16 + (lane & 15), a.Cout - 1);
-        bj[j] = (a.e.on && a.e.bias) ? a.e.bias[o] : 0.f;
+        bj[j] = (a.e.on && a.e.bias) ? (float)(T)a.e.bias[o] : 0.f;
     }
     typedef T vec8o __attribute__((ext_vector_type(8)));
     const bool cvec = (a.Cout % 8) == 0;

@@ -214,7 +214,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
         const int o = o0 + j * 16 + (lane & 15);
         const int oc = o < a.Cout ? o : 0;
         dsc[j] = (EPI && a.out_scale) ? a.out_scale[(int64_t)n * a.Cout + oc] : 1.f;
-        bsc[j] = (EPI && a.bias) ? a.bias[oc] : 0.f;
+        bsc[j] = (EPI && a.bias) ? (float)(T)a.bias[oc] : 0.f;   // the reference adds the bias rounded to x.dtype
     }
     constexpr int OS = BN + 8;                 // LDS row stride (elements) of the output tile
     T* ot = smem;                              // y tile  [256][OS]

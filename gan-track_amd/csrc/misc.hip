@@ -33,6 +33,75 @@ __global__ __launch_bounds__(256) void demod_kernel(float* d, const float* s, co
     }
 }
 
+// Demodulation with the per-(o, i) weight energy kept for the backward: wsq[o,i] = sum_k w^2 (written when
+// wsq_out != null), d[n,o] = rsqrt(sum_i s[n,i]^2 wsq[o,i] + eps).  One workgroup per o.
+__global__ __launch_bounds__(256) void demod_fwd_kernel(float* d, float* wsq_out, const float* s, const float* w,
+                                                        int N, int O, int I, int KK, float eps) {
+    __shared__ float wsq[1024];
+    __shared__ float red[4];
+    const int o = blockIdx.x;
+    for (int i = threadIdx.x; i < I; i += 256) {
+        const float* wr = w + ((int64_t)o * I + i) * KK;
+        float acc = 0.f;
+        for (int k = 0; k < KK; ++k) acc += wr[k] * wr[k];
+        wsq[i] = acc;
+        if (wsq_out) wsq_out[(int64_t)o * I + i] = acc;
+    }
+    __syncthreads();
+    for (int n = 0; n < N; ++n) {
+        float acc = 0.f;
+        for (int i = threadIdx.x; i < I; i += 256) {
+            const float v = s[(int64_t)n * I + i];
+            acc += v * v * wsq[i];
+        }
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) d[(int64_t)n * O + o] = rsqrtf(red[0] + red[1] + red[2] + red[3] + eps);
+        __syncthreads();
+    }
+}
+
+// Backward of demod_fwd: with gu[n,o] = -1/2 dd[n,o] d[n,o]^3,
+//   gw[o,i,k] = 2 w[o,i,k] sum_n gu[n,o] s[n,i]^2     (workgroup per o)
+//   gs[n,i]   = 2 s[n,i]   sum_o gu[n,o] wsq[o,i]      (workgroup per n)
+__global__ __launch_bounds__(256) void demod_bwd_w_kernel(float* gw, const float* dd, const float* d, const float* s,
+                                                          const float* w, int N, int O, int I, int KK) {
+    __shared__ float gu[1024];
+    const int o = blockIdx.x;
+    for (int n = threadIdx.x; n < N; n += 256) {
+        const float dv = d[(int64_t)n * O + o];
+        gu[n] = -0.5f * dd[(int64_t)n * O + o] * dv * dv * dv;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < I; i += 256) {
+        float acc = 0.f;
+        for (int n = 0; n < N; ++n) {
+            const float v = s[(int64_t)n * I + i];
+            acc += gu[n] * v * v;
+        }
+        const float* wr = w + ((int64_t)o * I + i) * KK;
+        float* gr = gw + ((int64_t)o * I + i) * KK;
+        for (int k = 0; k < KK; ++k) gr[k] = 2.f * wr[k] * acc;
+    }
+}
+
+__global__ __launch_bounds__(256) void demod_bwd_s_kernel(float* gs, const float* dd, const float* d, const float* s,
+                                                          const float* wsq, int N, int O, int I) {
+    __shared__ float gu[1024];
+    const int n = blockIdx.x;
+    for (int o = threadIdx.x; o < O; o += 256) {
+        const float dv = d[(int64_t)n * O + o];
+        gu[o] = -0.5f * dd[(int64_t)n * O + o] * dv * dv * dv;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < I; i += 256) {
+        float acc = 0.f;
+        for (int o = 0; o < O; ++o) acc += gu[o] * wsq[(int64_t)o * I + i];
+        gs[(int64_t)n * I + i] = 2.f * s[(int64_t)n * I + i] * acc;
+    }
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                                    const float* __restrict__ g, int64_t n, float lr, float b1, float b2,
                                                    float eps, float gscale, float bc1, float bc2_sqrt) {
@@ -68,6 +137,35 @@ extern "C" int sg2_demod_coefs(float* d, const float* s, const float* w, int N, 
     dim3 grid(O, std::min(N, 64));
     demod_kernel<<<grid, 256, 0, as_stream(stream)>>>(d, s, w, N, O, I, KK, eps);
     return launch_status("sg2_demod_coefs");
+}
+
+extern "C" int sg2_demod_fwd(float* d, float* wsq, const float* s, const float* w, int N, int O, int I, int KK,
+                             float eps, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(d && s && w, "sg2_demod_fwd: null pointer");
+    SG2_CHECK(I <= 1024 && I > 0 && O > 0 && N > 0 && KK > 0, "sg2_demod_fwd: unsupported shape");
+    demod_fwd_kernel<<<O, 256, 0, as_stream(stream)>>>(d, wsq, s, w, N, O, I, KK, eps);
+    return launch_status("sg2_demod_fwd");
+}
+
+extern "C" int sg2_demod_bwd(float* gs, float* gw, const float* dd, const float* d, const float* s, const float* w,
+                             const float* wsq, int N, int O, int I, int KK, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(dd && d && s && w, "sg2_demod_bwd: null pointer");
+    SG2_CHECK(!gs || wsq, "sg2_demod_bwd: gs needs wsq");
+    SG2_CHECK(I <= 1024 && O <= 1024 && N <= 1024 && I > 0 && O > 0 && N > 0 && KK > 0,
+              "sg2_demod_bwd: unsupported shape");
+    hipStream_t st = as_stream(stream);
+    if (gw) {
+        demod_bwd_w_kernel<<<O, 256, 0, st>>>(gw, dd, d, s, w, N, O, I, KK);
+        int rc = launch_status("sg2_demod_bwd");
+        if (rc) return rc;
+    }
+    if (gs) {
+        demod_bwd_s_kernel<<<N, 256, 0, st>>>(gs, dd, d, s, wsq, N, O, I);
+        return launch_status("sg2_demod_bwd");
+    }
+    return 0;
 }
 
 extern "C" int sg2_adam_step(float* param, float* exp_avg, float* exp_avg_sq, const float* grad, int64_t n, float lr,

@@ -128,7 +128,7 @@ __device__ __forceinline__ void store_out(const UpfParams& p, T* y, const float*
             float v = acc[j];
             if (p.out_scale) v *= p.out_scale[(int64_t)n * p.C + c];
             v += nv;
-            if (p.bias) v += p.bias[c];
+            if (p.bias) v += (float)(T)p.bias[c];     // bias rounded to the activation dtype
             if (p.act == 1) v = v > 0.f ? v : v * p.alpha;
             v *= p.egain;
             if (p.clamp >= 0.f) v = fminf(fmaxf(v, -p.clamp), p.clamp);

@@ -112,12 +112,14 @@ def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None):
     return dw.permute(0, 3, 1, 2)
 
 
-def _pack_conv(w):          # [O, I, kh, kw] -> [O][kh][kw][I]
-    return w.permute(0, 2, 3, 1).contiguous()
+def _pack_conv(w, dtype=None):      # [O, I, kh, kw] -> [O][kh][kw][I], cast to dtype in the same copy
+    out = torch.empty([w.shape[0], w.shape[2], w.shape[3], w.shape[1]], dtype=dtype or w.dtype, device=w.device)
+    return out.copy_(w.permute(0, 2, 3, 1))
 
 
-def _pack_convT(w):         # [I, O, kh, kw] -> [O][kh][kw][I]
-    return w.permute(1, 2, 3, 0).contiguous()
+def _pack_convT(w, dtype=None):     # [I, O, kh, kw] -> [O][kh][kw][I]
+    out = torch.empty([w.shape[1], w.shape[2], w.shape[3], w.shape[0]], dtype=dtype or w.dtype, device=w.device)
+    return out.copy_(w.permute(1, 2, 3, 0))
 
 
 def _halo_ok(x, kh, kw, stride, pad, out_hw):

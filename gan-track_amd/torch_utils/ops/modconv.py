@@ -67,19 +67,18 @@ class FusedConv(torch.autograd.Function):
         oh = (h + 2 * pad - kh) // stride + 1
         ow = (w + 2 * pad - kw) // stride + 1
         dt = x.dtype
-        wT = weight.to(dt)
         nz = noise.to(dt).reshape(n, oh, ow).contiguous() if noise is not None else None
         any_grad = any(ctx.needs_input_grad[:7])
         want_c = any_grad and dcoefs is not None          # c feeds dL/dd
         want_z = any_grad and residual is not None        # z = y - residual feeds the activation grad
         assert not (want_c and want_z), 'demodulation and a residual in one layer are not supported'
-        b32 = _f32(bias.to(dt)) if bias is not None else None   # the reference adds the bias rounded to x.dtype
+        b32 = _f32(bias) if bias is not None else None   # the kernels add it rounded to x.dtype, as the reference
         if _halo(x, kh, kw, stride, pad) and residual is None:
-            y, aux = _cg.conv3x3_fused(x, _cg._pack_conv(wT), cout, in_scale=_f32(styles), out_scale=_f32(dcoefs),
+            y, aux = _cg.conv3x3_fused(x, _cg._pack_conv(weight, dt), cout, in_scale=_f32(styles), out_scale=_f32(dcoefs),
                                        noise=nz, noise_gain=1.0, bias=b32, act=act, alpha=alpha, gain=gain,
                                        clamp=clamp, want_raw=want_c)
         else:
-            y, aux = _cg.conv_fused(x, _cg._pack_conv(wT), cout, oh, ow, kh, kw, stride, (pad, pad),
+            y, aux = _cg.conv_fused(x, _cg._pack_conv(weight, dt), cout, oh, ow, kh, kw, stride, (pad, pad),
                                     in_scale=_f32(styles), out_scale=_f32(dcoefs), noise=nz, noise_gain=1.0,
                                     bias=b32, act=act, alpha=alpha, gain=gain, clamp=clamp, residual=residual,
                                     aux_mode=1 if want_c else (2 if want_z else 0))
@@ -126,17 +125,17 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
     want_ds = need[1] and styles is not None
     if need[0] or want_ds:
         if _halo(dc, kh, kw, stride, pad):
-            wT = _cg._pack_convT(weight.to(dt).flip([2, 3]))
+            wT = _cg._pack_convT(weight.flip([2, 3]), dt)
             if want_ds:
                 dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
             else:
                 dx, _ = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32)
         else:
             if want_ds:
-                dx, _, ds = _cg.conv_fused(dc, _cg._pack_convT(weight.to(dt)), cin, h, w, kh, kw, stride, (pad, pad),
+                dx, _, ds = _cg.conv_fused(dc, _cg._pack_convT(weight, dt), cin, h, w, kh, kw, stride, (pad, pad),
                                            transpose=True, out_scale=s32, dot_src=x)
             else:
-                dx, _ = _cg.conv_fused(dc, _cg._pack_convT(weight.to(dt)), cin, h, w, kh, kw, stride, (pad, pad),
+                dx, _ = _cg.conv_fused(dc, _cg._pack_convT(weight, dt), cin, h, w, kh, kw, stride, (pad, pad),
                                        transpose=True, out_scale=s32)
         ds = ds.to(styles.dtype) if want_ds else None
         dx = dx if need[0] else None
@@ -234,12 +233,12 @@ class UpModConv(torch.autograd.Function):
         cout, _, kh, kw = weight.shape
         dt = x.dtype
         tpad, (th, tw), fpad = _up_geometry(h, w, kh, kw, f)
-        t, _ = _cg.conv_fused(x, _cg._pack_conv(weight.to(dt)), cout, th, tw, kh, kw, 2, tpad, transpose=True,
+        t, _ = _cg.conv_fused(x, _cg._pack_conv(weight, dt), cout, th, tw, kh, kw, 2, tpad, transpose=True,
                               in_scale=_f32(styles))
         oh, ow = th + fpad[2] + fpad[3] - f.shape[0] + 1, tw + fpad[0] + fpad[1] - f.shape[1] + 1
         nz = noise.to(dt).reshape(n, oh, ow).contiguous() if noise is not None else None
         want_c = any(ctx.needs_input_grad[:6]) and dcoefs is not None
-        b32 = _f32(bias.to(dt)) if bias is not None else None
+        b32 = _f32(bias) if bias is not None else None       # rounded to x.dtype in the kernel
         y, c = _up.fir_fused(t, f, fpad, gain=4.0, out_scale=_f32(dcoefs), noise=nz, bias=b32, act=1, alpha=alpha,
                              act_gain=gain, clamp=clamp, aux_mode=1 if want_c else 0)
         ctx.save_for_backward(x, styles, weight, dcoefs, noise, bias, f, y, c)
@@ -256,7 +255,6 @@ class UpModConv(torch.autograd.Function):
         dt = x.dtype
         oh, ow = y.shape[2], y.shape[3]
         aup, adown, apad, aflip = _up.adjoint_params(f, (th, tw), (oh, ow), 1, 1, fpad, False)
-        wt = weight.to(dt).transpose(0, 1)                    # conv_transpose2d weight [Cin, Cout, kh, kw]
         dx = ds = dw = dd = dn = db = None
         if not torch.is_grad_enabled() and fast_backward:
             d32, s32 = _f32(dcoefs), _f32(styles)
@@ -267,14 +265,15 @@ class UpModConv(torch.autograd.Function):
             dt_ = _up.upfirdn2d(dc, f, up=aup, down=adown, padding=apad, flip_filter=aflip, gain=4)
             if need[0] or need[1]:
                 if need[1]:
-                    dx, _, ds = _cg.conv_fused(dt_, _cg._pack_conv(wt), cin, h, w, kh, kw, 2, tpad, out_scale=s32,
+                    dx, _, ds = _cg.conv_fused(dt_, _cg._pack_conv(weight.transpose(0, 1), dt), cin, h, w, kh, kw, 2, tpad, out_scale=s32,
                                                dot_src=x)
                 else:
-                    dx, _ = _cg.conv_fused(dt_, _cg._pack_conv(wt), cin, h, w, kh, kw, 2, tpad, out_scale=s32)
+                    dx, _ = _cg.conv_fused(dt_, _cg._pack_conv(weight.transpose(0, 1), dt), cin, h, w, kh, kw, 2, tpad, out_scale=s32)
                 dx = dx if need[0] else None
             if need[2] and not _cg.weight_gradients_disabled:
                 dw = _cg._wgrad_raw(x, dt_, kh, kw, 2, tpad, g_scale=s32).transpose(0, 1).to(weight.dtype)
         else:
+            wt = weight.to(dt).transpose(0, 1)                # conv_transpose2d weight [Cin, Cout, kh, kw]
             dz = _ba.bias_act_grad(dy, y, act='lrelu', alpha=alpha, gain=gain, clamp=clamp)
             param_grads = not _cg.weight_gradients_disabled      # see _composed_backward
             if need[5] and bias is not None and param_grads:

@@ -17,6 +17,7 @@ MI355X-specific execution choices (numerically equivalent to the reference up to
 import numpy as np
 import torch
 
+import sg2hip as _hip
 from torch_utils import misc
 from torch_utils import persistence
 from torch_utils.ops import bias_act
@@ -33,8 +34,47 @@ def normalize_2nd_moment(x, dim=1, eps=1e-8):
     return x * (x.square().mean(dim=dim, keepdim=True) + eps).rsqrt()
 
 
+class _Demod(torch.autograd.Function):
+    """d[n,o] = rsqrt(sum_i s[n,i]^2 sum_k w[o,i,k]^2 + 1e-8) in one kernel (sg2_demod_fwd) where autograd
+    of the reference's expression (:59-63) runs six elementwise / reduction / GEMM launches, and the
+    first-order gradient in two (sg2_demod_bwd).  Under create_graph (the path-length pass) the gradient
+    is composed of differentiable torch ops."""
+
+    @staticmethod
+    def forward(ctx, weight, styles):
+        w = weight.float().contiguous()
+        s = styles.float().contiguous()
+        n, o, i, kk = s.shape[0], w.shape[0], w.shape[1], w.shape[2] * w.shape[3]
+        d = torch.empty([n, o], dtype=torch.float32, device=s.device)
+        wsq = torch.empty([o, i], dtype=torch.float32, device=s.device)
+        _hip.check(_hip.lib().sg2_demod_fwd(_hip.ptr(d), _hip.ptr(wsq), _hip.ptr(s), _hip.ptr(w), n, o, i, kk, 1e-8,
+                                            _hip.stream_ptr(s.device)), 'sg2_demod_fwd')
+        ctx.save_for_backward(w, s, d, wsq)
+        return d
+
+    @staticmethod
+    def backward(ctx, dd):
+        w, s, d, wsq = ctx.saved_tensors
+        need_w, need_s = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if torch.is_grad_enabled():
+            gu = dd * d.pow(3) * -0.5
+            gs = 2 * s * (gu @ w.square().sum([2, 3])) if need_s else None
+            gw = 2 * w * (gu.t() @ s.square())[:, :, None, None] if need_w else None
+            return gw, gs
+        dd = dd.float().contiguous()
+        n, o, i, kk = s.shape[0], w.shape[0], w.shape[1], w.shape[2] * w.shape[3]
+        gw = torch.empty_like(w) if need_w else None
+        gs = torch.empty_like(s) if need_s else None
+        _hip.check(_hip.lib().sg2_demod_bwd(_hip.ptr(gs), _hip.ptr(gw), _hip.ptr(dd), _hip.ptr(d), _hip.ptr(s),
+                                            _hip.ptr(w), _hip.ptr(wsq), n, o, i, kk, _hip.stream_ptr(s.device)),
+                   'sg2_demod_bwd')
+        return gw, gs
+
+
 def _demod(weight, styles):
     """d[n,o] = rsqrt(sum_i s[n,i]^2 sum_k w[o,i,k]^2 + 1e-8)   (:59-63, regrouped)."""
+    if weight.shape[1] <= 1024 and weight.shape[0] <= 1024 and styles.shape[0] <= 1024:
+        return _Demod.apply(weight, styles)
     wsq = weight.float().square().sum(dim=[2, 3])                 # [O, I]
     return (styles.float().square() @ wsq.t() + 1e-8).rsqrt()     # [N, O]
 
@@ -75,16 +115,20 @@ class FullyConnectedLayer(torch.nn.Module):
         self.weight_gain = lr_multiplier / np.sqrt(in_features)
         self.bias_gain = lr_multiplier
 
-    def forward(self, x):
-        w = self.weight.to(x.dtype) * self.weight_gain
+    def forward(self, x, out_gain=1):
+        """y = act(x @ (W * weight_gain)^T + b * bias_gain) (* out_gain for a linear layer).  The weight and
+        bias gains (reference :111-125: two elementwise multiplies per call, and their backward) are the
+        alpha / beta scalars of ONE addmm; `out_gain` folds ToRGBLayer's styles * weight_gain (:352)."""
+        w = self.weight if self.weight.dtype == x.dtype else self.weight.to(x.dtype)
         b = self.bias
         if b is not None:
-            b = b.to(x.dtype)
-            if self.bias_gain != 1:
-                b = b * self.bias_gain
-        if self.activation == 'linear' and b is not None:
-            return torch.addmm(b.unsqueeze(0), x, w.t())
-        return bias_act.bias_act(x.matmul(w.t()), b, act=self.activation)
+            b = b if b.dtype == x.dtype else b.to(x.dtype)
+            if self.activation == 'linear':
+                return torch.addmm(b, x, w.t(), beta=self.bias_gain * out_gain, alpha=self.weight_gain * out_gain)
+            y = torch.addmm(b, x, w.t(), beta=self.bias_gain, alpha=self.weight_gain)
+            return bias_act.bias_act(y, None, act=self.activation)
+        y = x.matmul((w * (self.weight_gain * out_gain)).t())
+        return bias_act.bias_act(y, None, act=self.activation) if self.activation != 'linear' else y
 
     def extra_repr(self):
         return f'in_features={self.in_features:d}, out_features={self.out_features:d}, activation={self.activation:s}'
@@ -270,7 +314,7 @@ class ToRGBLayer(torch.nn.Module):
         self.weight_gain = 1 / np.sqrt(in_channels * (kernel_size ** 2))
 
     def forward(self, x, w, fused_modconv=True):
-        styles = self.affine(w) * self.weight_gain
+        styles = self.affine(w, out_gain=self.weight_gain)
         if modconv.supported_generic(x, self.weight):
             # modulation folded into the conv's operand staging, bias + clamp into its epilogue
             return modconv.fused_conv(x, self.weight, styles=styles, bias=self.bias,

@@ -112,7 +112,7 @@ int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int N, int Cin,
 struct sg2_epilogue {
     const float* out_scale;  /* [N, Cout] float32 */
     const void* noise;       /* [N, OH, OW], activation dtype */
-    const float* bias;       /* [Cout] float32 */
+    const float* bias;       /* [Cout] float32, added rounded to the activation dtype (the reference's b.to(x.dtype)) */
     const void* residual;    /* [N, OH, OW, Cout] NHWC, activation dtype */
     void* aux;               /* [N, OH, OW, Cout] NHWC, activation dtype */
     float noise_gain, alpha, gain, clamp;   /* clamp < 0: off */
@@ -189,6 +189,17 @@ int sg2_reflect_pad_dyn(float* y, const float* x, const int* margins, int N, int
  * (SG3/training/networks_stylegan2.py:59-63, summation regrouped).  s [N,I] f32, w [O,I*KK] f32. */
 int sg2_demod_coefs(float* d, const float* s, const float* w, int N, int O, int I, int KK, float eps,
                     void* stream);
+
+/* sg2_demod_coefs that also writes wsq [O, I] (may be NULL) for the backward. */
+int sg2_demod_fwd(float* d, float* wsq, const float* s, const float* w, int N, int O, int I, int KK, float eps,
+                  void* stream);
+
+/* Gradient of sg2_demod_fwd (first order): with gu = -dd * d^3 / 2,
+ *   gw[o,i,k] = 2 w[o,i,k] sum_n gu[n,o] s[n,i]^2,   gs[n,i] = 2 s[n,i] sum_o gu[n,o] wsq[o,i].
+ * gs / gw may be NULL (gs needs wsq).  The reference gets these from autograd of
+ * networks_stylegan2.py:59-63. */
+int sg2_demod_bwd(float* gs, float* gw, const float* dd, const float* d, const float* s, const float* w,
+                  const float* wsq, int N, int O, int I, int KK, void* stream);
 
 /* Adam step on a flat float32 parameter vector (torch.optim.Adam semantics, no weight decay,
  * amsgrad off) with the reference's gradient sanitation fused in front:

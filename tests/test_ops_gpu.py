@@ -696,3 +696,27 @@ def test_augment_dynamic_extent(dp):
         res.append([t.detach().double().cpu() for t in (y, g, gg)])
     for a, b in zip(*res):
         assert rel_err(a, b) < 2e-5
+
+
+def test_demod_kernel():
+    """sg2_demod_fwd / sg2_demod_bwd (networks_stylegan2._Demod) vs autograd of the reference expression
+    (networks_stylegan2.py:59-63) in fp64: value, first-order gradients and a create_graph second order."""
+    from training import networks_stylegan2 as net
+    torch.manual_seed(41)
+    w = torch.randn(96, 80, 3, 3, device=DEV)
+    s = torch.rand(5, 80, device=DEV) + 0.2
+    dd = torch.randn(5, 96, device=DEV)
+    ref = []
+    for dev, fn in [(DEV, net._Demod.apply),
+                    (torch.device('cpu'), lambda w_, s_: ((w_[None] * s_[:, None, :, None, None]).square()
+                                                          .sum([2, 3, 4]) + 1e-8).rsqrt())]:
+        dt = torch.float32 if dev.type == 'cuda' else torch.float64
+        wd = w.to(dev, dt).requires_grad_(True)
+        sd = s.to(dev, dt).requires_grad_(True)
+        d = fn(wd, sd)
+        gw, gs = torch.autograd.grad((d * dd.to(dev, dt)).sum(), [wd, sd], create_graph=True)
+        gw2, = torch.autograd.grad((gs.square().sum() + gw.square().sum()), [wd])
+        gwf, gsf = torch.autograd.grad((fn(wd, sd) * dd.to(dev, dt)).sum(), [wd, sd])   # first-order kernel path
+        ref.append([t.detach().double().cpu() for t in (d, gw, gs, gw2, gwf, gsf)])
+    for a, b in zip(*ref):
+        assert rel_err(a, b) < 1e-5
