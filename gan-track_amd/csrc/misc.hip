@@ -34,12 +34,12 @@ __global__ __launch_bounds__(256) void demod_kernel(float* d, const float* s, co
 }
 
 // Demodulation with the per-(o, i) weight energy kept for the backward: wsq[o,i] = sum_k w^2 (written when
-// wsq_out != null), d[n,o] = rsqrt(sum_i s[n,i]^2 wsq[o,i] + eps).  One workgroup per o.
+// wsq_out != null), d[n,o] = rsqrt(sum_i s[n,i]^2 wsq[o,i] + eps).  One workgroup per o; after wsq is in
+// LDS each wave takes every fourth sample and reduces over i with shuffles (no block barrier per sample).
 __global__ __launch_bounds__(256) void demod_fwd_kernel(float* d, float* wsq_out, const float* s, const float* w,
                                                         int N, int O, int I, int KK, float eps) {
     __shared__ float wsq[1024];
-    __shared__ float red[4];
-    const int o = blockIdx.x;
+    const int o = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < I; i += 256) {
         const float* wr = w + ((int64_t)o * I + i) * KK;
         float acc = 0.f;
@@ -48,23 +48,20 @@ __global__ __launch_bounds__(256) void demod_fwd_kernel(float* d, float* wsq_out
         if (wsq_out) wsq_out[(int64_t)o * I + i] = acc;
     }
     __syncthreads();
-    for (int n = 0; n < N; ++n) {
+    for (int n = wave; n < N; n += 4) {
         float acc = 0.f;
-        for (int i = threadIdx.x; i < I; i += 256) {
+        for (int i = lane; i < I; i += 64) {
             const float v = s[(int64_t)n * I + i];
             acc += v * v * wsq[i];
         }
-        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-        __syncthreads();
-        if (threadIdx.x == 0) d[(int64_t)n * O + o] = rsqrtf(red[0] + red[1] + red[2] + red[3] + eps);
-        __syncthreads();
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+        if (lane == 0) d[(int64_t)n * O + o] = rsqrtf(acc + eps);
     }
 }
 
 // Backward of demod_fwd: with gu[n,o] = -1/2 dd[n,o] d[n,o]^3,
 //   gw[o,i,k] = 2 w[o,i,k] sum_n gu[n,o] s[n,i]^2     (workgroup per o)
-//   gs[n,i]   = 2 s[n,i]   sum_o gu[n,o] wsq[o,i]      (workgroup per n)
+//   gs[n,i]   = 2 s[n,i]   sum_o gu[n,o] wsq[o,i]      (workgroup per (n, 64 i); four o-quarters reduced in LDS)
 __global__ __launch_bounds__(256) void demod_bwd_w_kernel(float* gw, const float* dd, const float* d, const float* s,
                                                           const float* w, int N, int O, int I, int KK) {
     __shared__ float gu[1024];
@@ -89,17 +86,21 @@ __global__ __launch_bounds__(256) void demod_bwd_w_kernel(float* gw, const float
 __global__ __launch_bounds__(256) void demod_bwd_s_kernel(float* gs, const float* dd, const float* d, const float* s,
                                                           const float* wsq, int N, int O, int I) {
     __shared__ float gu[1024];
-    const int n = blockIdx.x;
+    __shared__ float part[4][64];
+    const int n = blockIdx.x, i = blockIdx.y * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
     for (int o = threadIdx.x; o < O; o += 256) {
         const float dv = d[(int64_t)n * O + o];
         gu[o] = -0.5f * dd[(int64_t)n * O + o] * dv * dv * dv;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < I; i += 256) {
-        float acc = 0.f;
-        for (int o = 0; o < O; ++o) acc += gu[o] * wsq[(int64_t)o * I + i];
-        gs[(int64_t)n * I + i] = 2.f * s[(int64_t)n * I + i] * acc;
-    }
+    float acc = 0.f;
+    if (i < I)
+        for (int o = q; o < O; o += 4) acc += gu[o] * wsq[(int64_t)o * I + i];
+    part[q][threadIdx.x & 63] = acc;
+    __syncthreads();
+    if (q == 0 && i < I)
+        gs[(int64_t)n * I + i] = 2.f * s[(int64_t)n * I + i] * (part[0][threadIdx.x] + part[1][threadIdx.x] +
+                                                                 part[2][threadIdx.x] + part[3][threadIdx.x]);
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
@@ -162,7 +163,7 @@ extern "C" int sg2_demod_bwd(float* gs, float* gw, const float* dd, const float*
         if (rc) return rc;
     }
     if (gs) {
-        demod_bwd_s_kernel<<<N, 256, 0, st>>>(gs, dd, d, s, wsq, N, O, I);
+        demod_bwd_s_kernel<<<dim3(N, (I + 63) / 64), 256, 0, st>>>(gs, dd, d, s, wsq, N, O, I);
         return launch_status("sg2_demod_bwd");
     }
     return 0;
