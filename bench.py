@@ -114,13 +114,10 @@ def one_step(tr, args, device, real, real_c):
     tr.step([real], [real_c], [[z[i]] for i in range(n_ph)], [[c[i]] for i in range(n_ph)])
 
 
-def roofline(device, res, cbase, dtype):
-    """Average duration of the dominant kernel -- the LDS-halo MFMA 3x3 conv (sg2_conv3x3) of the
-    top-resolution layer, [32, C, res, res] -> [32, C, res, res] with the fused modulation/demod/noise/
-    bias/lrelu/clamp epilogue -- measured with HIP events on its launch stream."""
+def _layer_launch(device, res, C, dtype, N=32):
+    """One launch of the fused modulated 3x3 synthesis-layer conv (sg2_conv3x3: modulation in the operand
+    staging, demod + noise + bias + lrelu + clamp epilogue) on [N, C, res, res] -> [N, C, res, res]."""
     from torch_utils.ops import conv2d_gradfix as cg
-    C = min(cbase // res, 512)
-    N = 32
     x = torch.randn([N, C, res, res], device=device, dtype=dtype).contiguous(memory_format=torch.channels_last)
     w = (torch.randn([C, C, 3, 3], device=device) / np.sqrt(C * 9)).to(dtype)
     wp = cg._pack_conv(w)
@@ -135,7 +132,7 @@ def roofline(device, res, cbase, dtype):
     for _ in range(3):
         launch()
     reps = 20
-    stream = torch.cuda.current_stream(device)
+    stream = torch.cuda.current_stream(device)       # the stream sg2_conv3x3 is launched on
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(reps):
@@ -143,15 +140,52 @@ def roofline(device, res, cbase, dtype):
     e1.record(stream)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    flops = 2.0 * N * C * C * 9 * res * res
-    ach = flops / (ms * 1e-3) / 1e12
-    byts = (2 * N * C * res * res + N * res * res) * x.element_size() + C * C * 9 * x.element_size()
-    return {'kernel': f'conv3x3_halo_kernel<{str(dtype).split(".")[-1]},TW=32,scale,epilogue> '
-                      f'(G {res}^2 modulated 3x3 conv, C={C}, N={N})',
-            'bound': 'mfma', 'achieved': round(ach, 2), 'peak': MFMA_PEAK_FP16, 'unit': 'TFLOP/s',
-            'frac': round(ach / MFMA_PEAK_FP16, 4), 'traffic': None, 'ms_per_launch': round(ms, 4),
-            'algorithmic_flops_per_launch': flops, 'algorithmic_hbm_bytes_per_launch': byts,
-            'achieved_hbm_GBps': round(byts / (ms * 1e-3) / 1e9, 1)}
+    flops = 2.0 * N * C * C * 9 * res * res                             # 2 N Cout Cin 9 H W
+    esz = x.element_size()
+    byts = (2 * N * C * res * res + N * res * res + C * C * 9) * esz + (2 * N * C + C) * 4   # x, y, noise, w, s, d, b
+    return ms, flops, byts
+
+
+def _measured_traffic(key):
+    """HBM bytes per launch of the roofline launch from the committed PMC passes (tools/pmc_traffic.py ->
+    profiles/roofline_traffic.json), if they were taken on this exact launch configuration."""
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'roofline_traffic.json')) as f:
+            t = json.load(f)
+        return t['hbm_bytes_per_launch'] if t.get('config') == key else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def roofline(device, res, cbase, dtype):
+    """Roofline of the dominant kernel, the LDS-halo MFMA 3x3 conv (sg2_conv3x3 = conv3x3_halo_kernel,
+    ~the largest kernel family of the step), on the 256^2 synthesis layer the north star names.  Its
+    arithmetic intensity (~286 FLOP/B at C = 64, 16-bit) is below the MI355X ridge (2500 TFLOP/s / 8 TB/s
+    = 312 FLOP/B), so the bound is HBM: achieved = algorithmic bytes / measured launch time.  The MFMA
+    view of the same launch and of the MFMA-bound 32^2 / C = 512 layer are reported beside it."""
+    C = min(cbase // res, 512)
+    ms, flops, byts = _layer_launch(device, res, C, dtype)
+    ai = flops / byts
+    ridge = MFMA_PEAK_FP16 * 1e12 / (HBM_PEAK * 1e9)
+    key = f'sg2_conv3x3 fused {res}^2 C={C} N=32 {str(dtype).split(".")[-1]}'
+    gbps = byts / (ms * 1e-3) / 1e9
+    tflops = flops / (ms * 1e-3) / 1e12
+    out = {'kernel': f'conv3x3_halo_kernel ({key}: modulation + demod/noise/bias/lrelu/clamp epilogue)'}
+    if ai < ridge:
+        out.update({'bound': 'hbm', 'achieved': round(gbps, 1), 'peak': HBM_PEAK, 'unit': 'GB/s',
+                    'frac': round(gbps / HBM_PEAK, 4)})
+    else:
+        out.update({'bound': 'mfma', 'achieved': round(tflops, 2), 'peak': MFMA_PEAK_FP16, 'unit': 'TFLOP/s',
+                    'frac': round(tflops / MFMA_PEAK_FP16, 4)})
+    out.update({'traffic': _measured_traffic(key), 'ms_per_launch': round(ms, 4),
+                'algorithmic_flops_per_launch': flops, 'algorithmic_hbm_bytes_per_launch': byts,
+                'arithmetic_intensity': round(ai, 1), 'ridge': round(ridge, 1),
+                'mfma_tflops': round(tflops, 1), 'mfma_frac': round(tflops / MFMA_PEAK_FP16, 4)})
+    ms2, fl2, _ = _layer_launch(device, 32, 512, dtype)
+    out['mfma_bound_layer'] = {'kernel': 'conv3x3_halo_kernel, 32^2 C=512 N=32 (AI ~2300 FLOP/B)',
+                               'ms_per_launch': round(ms2, 4), 'achieved': round(fl2 / (ms2 * 1e-3) / 1e12, 1),
+                               'unit': 'TFLOP/s', 'frac': round(fl2 / (ms2 * 1e-3) / 1e12 / MFMA_PEAK_FP16, 4)}
+    return out
 
 
 def cpu_baseline(args):

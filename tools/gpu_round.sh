@@ -52,7 +52,7 @@ if step pmc; then
             --output-format csv -- python3 "$R/tools/roofline_only.py" > "$O/pmc_$c.log" 2>&1
         rc=$?; tail -1 "$O/pmc_$c.log"; [ $rc -eq 0 ] || exit $rc
     done
-    python3 "$R/tools/pmc_traffic.py" "$O" > "$O/pmc_traffic.txt" 2>&1; cat "$O/pmc_traffic.txt"
+    python3 "$R/tools/pmc_traffic.py" "$O" "$O/roofline_traffic.json" > "$O/pmc_traffic.txt" 2>&1; cat "$O/pmc_traffic.txt"
 fi
 if step diag; then
     # where the halo conv waves wait (one pass, 8 SQ counters; MI355X_MICROARCH.md rocprofv3 PMC slots)
