@@ -11,6 +11,8 @@
 //    each lane owns one 16-byte channel vector of one output pixel, so every tap read is a
 //    coalesced 16-byte load and neighbouring taps hit L1/L2.
 //  * upfirdn_generic : any 4-D strides (images, NCHW tensors, odd channel counts).
+#include <cstdlib>
+
 #include "sg2_common.h"
 
 namespace sg2 {
@@ -252,8 +254,149 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_f4(UpfParams p) {
     }
 }
 
+// One lane's column strip of the f4s kernel: every input row is read from LDS once and feeds the
+// up-to-4 output rows that use it; an output row is stored as soon as its last input row is in.  The
+// layer epilogue (store_out's semantics) is resolved to per-lane constants once, so the per-row store
+// is branch-free apart from the uniform noise/residual/aux pointer tests.
+template <typename T, int V, typename vecT, int TW, int TH, int CG>
+__device__ __forceinline__ void fir4_strip(const UpfParams& p, const vecT* base, const float* wf, int n, int ty0,
+                                           int ox, int cv) {
+    constexpr int F = 4, IW = TW + F - 1, IH = TH + F - 1;
+    float os[V], bj[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        const int c = cv * V + j;
+        os[j] = (p.epi && p.out_scale) ? p.out_scale[(int64_t)n * p.C + c] : 1.f;
+        bj[j] = (p.epi && p.bias) ? (float)(T)p.bias[c] : 0.f;   // bias rounded to the activation dtype
+    }
+    const float slope = (p.epi && p.act == 1) ? p.alpha : 1.f;
+    const float eg = p.epi ? p.egain : 1.f;
+    const float cl = (p.epi && p.clamp >= 0.f) ? p.clamp : __builtin_inff();
+    const bool noise = p.epi && p.noise, resid = p.epi && p.residual;
+    const int aux_mode = p.epi ? p.aux_mode : 0;
+    float acc[TH][V];
+#pragma unroll
+    for (int o = 0; o < TH; ++o)
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[o][j] = 0.f;
+#pragma unroll
+    for (int ry = 0; ry < IH; ++ry) {
+        vecT v[F];
+#pragma unroll
+        for (int kx = 0; kx < F; ++kx) v[kx] = base[(ry * IW + kx) * CG];
+#pragma unroll
+        for (int ky = 0; ky < F; ++ky) {
+            const int o = ry - ky;                    // output row fed by input row ry through tap row ky
+            if (o < 0 || o >= TH) continue;
+#pragma unroll
+            for (int kx = 0; kx < F; ++kx)
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[o][j] += (float)v[kx][j] * wf[ky * F + kx];
+        }
+        const int od = ry - (F - 1);                  // output row completed by input row ry
+        if (od < 0) continue;
+        const int oy = ty0 + od;
+        const int64_t dst = n * p.ys_n + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w + cv * V;
+        const float nv = noise ? (float)((const T*)p.noise)[((int64_t)n * p.OH + oy) * p.OW + ox] * p.noise_gain : 0.f;
+        vecT o, ax;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            float z = acc[od][j] * os[j] + nv + bj[j];
+            z = (z > 0.f ? z : z * slope) * eg;
+            z = fminf(fmaxf(z, -cl), cl);
+            o[j] = (T)z;
+            ax[j] = (T)(aux_mode == 1 ? acc[od][j] : z);
+        }
+        if (resid) {
+            const vecT rv = *(const vecT*)((const T*)p.residual + dst);
+#pragma unroll
+            for (int j = 0; j < V; ++j) o[j] = (T)((float)o[j] + (float)rv[j]);
+        }
+        if (aux_mode) *(vecT*)((T*)p.aux + dst) = ax;
+        *(vecT*)((T*)p.y + dst) = o;
+        __builtin_amdgcn_sched_barrier(0);            // keeps the next rows' LDS reads below this store
+    }
+}
+
+// 4x4 filter, up = down = 1, channels-last: the FIR of every G up-layer and D down-layer pad-FIR.
+// A workgroup owns a TW x TH output tile x CG = 8 channel vectors (a whole 128-byte line of each
+// pixel, so no line is split between workgroups on different XCDs).  All loads of the
+// (TH+3) x (TW+3) input patch are issued before the first LDS write (one latency per tile, ~13
+// 16-byte loads in flight per lane).  Each lane then owns one column x one channel vector and slides
+// down the strip: every input row is read from LDS once (4 ds_read_b128) and feeds the up-to-4 output
+// rows that use it, 5.5 LDS reads per output instead of 16.  Blocks are renumbered so each XCD walks a
+// contiguous run of tiles (neighbouring tiles share halo rows in that XCD's L2).
+template <typename T, int TW, int TH>
+__global__ __launch_bounds__(256, 2) void upfirdn_nhwc_f4s(UpfParams p) {
+    constexpr int V = VecN<T>::N, F = 4, CG = 8;
+    constexpr int IW = TW + F - 1, IH = TH + F - 1, NIN = IW * IH * CG;
+    constexpr int NL = (NIN + 255) / 256;
+    static_assert(TW * CG == 256, "one lane per (column, channel vector)");
+    typedef T vecT __attribute__((ext_vector_type(V)));
+    extern __shared__ __attribute__((aligned(16))) char tile_raw[];
+    vecT* tile = (vecT*)tile_raw;                     // [IH][IW][CG]
+    const int tid = threadIdx.x;
+    float wf[F * F];
+#pragma unroll
+    for (int t = 0; t < F * F; ++t) {
+        const int ty = t / F, tx = t % F;
+        wf[t] = p.f[(p.flip ? ty : F - 1 - ty) * F + (p.flip ? tx : F - 1 - tx)] * p.gain;
+    }
+    const int CV = p.C / V;
+    const int ngroups = (CV + CG - 1) / CG;
+    const int tiles_x = (p.OW + TW - 1) / TW, tiles_y = (p.OH + TH - 1) / TH;
+    int64_t b = blockIdx.x;
+    const int64_t nb = gridDim.x;
+    if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);   // XCD-contiguous tile runs
+    // the last tile of a row/column is shifted back inside the image (host guarantees OH >= TH,
+    // OW >= TW): every strip is whole and branch-free; the overlap is written twice with equal values
+    const int tx0 = min((int)(b % tiles_x) * TW, p.OW - TW); b /= tiles_x;
+    const int ty0 = min((int)(b % tiles_y) * TH, p.OH - TH); b /= tiles_y;
+    const int cg = (int)(b % ngroups); b /= ngroups;
+    const int n = (int)b;
+    const int cv0 = cg * CG;
+    const T* xb = (const T*)p.x + n * p.xs_n;
+    const int iy0 = ty0 - p.pady0, ix0 = tx0 - p.padx0;
+    vecT r[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        const int i = tid + l * 256;
+        const int c = i % CG, px = i / CG;
+        const int ry = px / IW, rx = px - ry * IW;
+        const int iy = iy0 + ry, ix = ix0 + rx;
+        const bool ok = i < NIN && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W && cv0 + c < CV;
+        r[l] = *(const vecT*)(xb + (int64_t)(ok ? iy : 0) * p.xs_h + (int64_t)(ok ? ix : 0) * p.xs_w +
+                              (ok ? cv0 + c : 0) * V);
+#pragma unroll
+        for (int j = 0; j < V; ++j) r[l][j] = ok ? r[l][j] : (T)0.f;
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+        if (l < NL - 1 || tid + l * 256 < NIN) tile[tid + l * 256] = r[l];
+    __syncthreads();
+    const int c = tid % CG, col = tid / CG;
+    if (cv0 + c >= CV) return;
+    fir4_strip<T, V, vecT, TW, TH, CG>(p, tile + col * CG + c, wf, n, ty0, tx0 + col, cv0 + c);
+}
+
 template <typename T>
 int launch(const UpfParams& p, bool vec, hipStream_t s) {
+    static const bool fir_old = getenv("SG2_FIR_OLD") != nullptr;
+    if (!fir_old && vec && p.upx == 1 && p.upy == 1 && p.downx == 1 && p.downy == 1 && p.fw == 4 && p.fh == 4 &&
+        p.OH >= 8 && (p.OW % 32 == 0 || p.OW >= 224) && !(p.residual && p.residual == p.y)) {
+        // (narrow ragged widths, e.g. the 65- and 33-wide pad-FIR of D, waste up to half the shifted last
+        // column tile: they stay on upfirdn_nhwc_f4)
+        constexpr int TW = 32, TH = 8;
+        const int64_t blocks = (int64_t)p.N * cdiv(p.OH, TH) * cdiv(p.OW, TW) * cdiv(p.C / VecN<T>::N, 8);
+        if (blocks < INT32_MAX) {
+            const size_t lds = (size_t)(TH + 3) * (TW + 3) * 8 * 16;
+            auto k = upfirdn_nhwc_f4s<T, TW, TH>;
+            static bool set = false;
+            if (!set) { (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); set = true; }
+            k<<<(unsigned)blocks, 256, lds, s>>>(p);
+            return launch_status("sg2_upfirdn2d");
+        }
+    }
     if (vec && p.upx == 1 && p.upy == 1 && p.downx == p.downy && (p.downy == 1 || p.downy == 2) && p.fw == 4 &&
         p.fh == 4) {
         constexpr int CG = 4;

@@ -111,6 +111,35 @@ def test_upfirdn2d_vec_path(dtype):
         assert rel_err(y.float(), r) < tol, kw
 
 
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
+def test_fir_strip_ragged(dtype):
+    """Column-strip FIR kernel (upfirdn_nhwc_f4s): image sizes that are not tile multiples (the last
+    tile row/column is shifted back inside the image), partial channel groups (C = 72), plain and
+    with the full layer epilogue (out_scale, noise, bias, lrelu, gain, clamp, aux), vs the oracle."""
+    from torch_utils.ops import upfirdn2d
+    torch.manual_seed(3)
+    f = upfirdn2d.setup_filter([1, 3, 3, 1])
+    tol = {torch.float32: 1e-5, torch.float16: 2e-3, torch.bfloat16: 1e-2}[dtype]
+    for (n, c, h, w, pad) in [(2, 64, 45, 250, 1), (1, 128, 33, 40, 2), (2, 72, 20, 33, 1), (1, 64, 257, 257, 1)]:
+        x = torch.randn(n, c, h, w).to(dtype).float()
+        xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+        ref = O.upfirdn2d(x, f, padding=pad, gain=4)
+        y = upfirdn2d.upfirdn2d(xd, f.to(DEV), padding=pad, gain=4)
+        assert rel_err(y.float(), ref) < tol, (n, c, h, w, pad)
+        oh, ow = ref.shape[2:]
+        os_ = torch.rand(n, c) + 0.5
+        noise = torch.randn(n, 1, oh, ow).to(dtype).float()
+        bias = torch.randn(c).to(dtype).float()
+        for aux_mode in (1, 2):
+            yd, aux = upfirdn2d.fir_fused(xd, f.to(DEV), pad, gain=4, out_scale=os_.to(DEV), noise=noise.to(DEV, dtype),
+                                          noise_gain=0.3, bias=bias.to(DEV), act=1, alpha=0.2, act_gain=1.4,
+                                          clamp=2.5, aux_mode=aux_mode)
+            z = ref * os_[:, :, None, None] + noise * 0.3 + bias[None, :, None, None]
+            z = (torch.where(z > 0, z, z * 0.2) * 1.4).clamp(-2.5, 2.5)
+            assert rel_err(yd.float(), z) < tol, (n, c, h, w, pad, aux_mode)
+            assert rel_err(aux.float(), ref if aux_mode == 1 else z) < tol, (n, c, h, w, pad, aux_mode)
+
+
 # ------------------------------------------------------------------ convolutions (torch fp32 reference)
 CONV_CASES = [
     # N, Cin, H, W, Cout, k, stride, pad
