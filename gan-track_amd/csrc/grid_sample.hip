@@ -16,6 +16,7 @@ struct GSParams {
     const void* in;
     void* out;
     const float* grid;
+    const float* theta;  // optional [N, 2, 3]: the grid is affine_grid(theta, align_corners=False), built inline
     int N, C, Hi, Wi, Ho, Wo;
     int64_t is_n, is_c, is_h, is_w;
     int64_t os_n, os_c, os_h, os_w;
@@ -28,9 +29,20 @@ struct Corners {
 };
 
 __device__ __forceinline__ Corners corners(const GSParams& p, int n, int oy, int ox, int Hi, int Wi) {
-    const float* g = p.grid + (((int64_t)n * p.Ho + oy) * p.Wo + ox) * 2;
-    const float ix = ((g[0] + 1.f) * Wi - 1.f) * 0.5f;
-    const float iy = ((g[1] + 1.f) * Hi - 1.f) * 0.5f;
+    float gx, gy;
+    if (p.theta) {
+        // affine_grid, align_corners = False: base coordinates at pixel centres, (2j + 1) / W - 1
+        const float* t = p.theta + n * 6;
+        const float bx = (float)(2 * ox + 1) / (float)p.Wo - 1.f, by = (float)(2 * oy + 1) / (float)p.Ho - 1.f;
+        gx = t[0] * bx + t[1] * by + t[2];
+        gy = t[3] * bx + t[4] * by + t[5];
+    } else {
+        const float* g = p.grid + (((int64_t)n * p.Ho + oy) * p.Wo + ox) * 2;
+        gx = g[0];
+        gy = g[1];
+    }
+    const float ix = ((gx + 1.f) * Wi - 1.f) * 0.5f;
+    const float iy = ((gy + 1.f) * Hi - 1.f) * 0.5f;
     Corners c;
     const float fx = floorf(ix), fy = floorf(iy);
     c.x0 = (int)fx;
@@ -170,13 +182,14 @@ int fill(GSParams& p, const int64_t* in_size, const int64_t* in_stride, const in
 }  // namespace
 }  // namespace sg2
 
-extern "C" int sg2_grid_sample_fwd(void* out, const void* in, const float* grid, int dtype, const int64_t* in_size,
-                                   const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
-                                   const int* dyn_hw, void* stream) {
-    using namespace sg2;
-    SG2_CHECK(out && in && grid, "sg2_grid_sample_fwd: null pointer");
+namespace sg2 {
+namespace {
+int gs_fwd(void* out, const void* in, const float* grid, const float* theta, int dtype, const int64_t* in_size,
+           const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride, const int* dyn_hw,
+           void* stream) {
+    SG2_CHECK(out && in && (grid || theta), "sg2_grid_sample_fwd: null pointer");
     GSParams p;
-    p.in = in; p.out = out; p.grid = grid; p.dyn_hw = dyn_hw;
+    p.in = in; p.out = out; p.grid = grid; p.theta = theta; p.dyn_hw = dyn_hw;
     if (fill(p, in_size, in_stride, out_size, out_stride)) return -1;
     const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
     if (total == 0 || p.C == 0) return 0;
@@ -185,13 +198,12 @@ extern "C" int sg2_grid_sample_fwd(void* out, const void* in, const float* grid,
     return launch_status("sg2_grid_sample_fwd");
 }
 
-extern "C" int sg2_grid_sample_bwd(float* gin, const void* gout, const float* grid, int dtype, const int64_t* in_size,
-                                   const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
-                                   const int* dyn_hw, void* stream) {
-    using namespace sg2;
-    SG2_CHECK(gin && gout && grid, "sg2_grid_sample_bwd: null pointer");
+int gs_bwd(float* gin, const void* gout, const float* grid, const float* theta, int dtype, const int64_t* in_size,
+           const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride, const int* dyn_hw,
+           void* stream) {
+    SG2_CHECK(gin && gout && (grid || theta), "sg2_grid_sample_bwd: null pointer");
     GSParams p;
-    p.in = gout; p.out = gin; p.grid = grid; p.dyn_hw = dyn_hw;
+    p.in = gout; p.out = gin; p.grid = grid; p.theta = theta; p.dyn_hw = dyn_hw;
     if (fill(p, in_size, in_stride, out_size, out_stride)) return -1;
     // zero the float32 input-gradient buffer (dense over the strided extent)
     const int64_t extent = (p.N - 1) * p.is_n + (p.C - 1) * p.is_c + (p.Hi - 1) * p.is_h + (p.Wi - 1) * p.is_w + 1;
@@ -213,6 +225,32 @@ extern "C" int sg2_grid_sample_bwd(float* gin, const void* gout, const float* gr
     const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 32);
     SG2_DISPATCH(dtype, T, { grid_sample_bwd_kernel<T><<<g, 256, 0, s>>>(p); });
     return launch_status("sg2_grid_sample_bwd");
+}
+}  // namespace
+}  // namespace sg2
+
+extern "C" int sg2_grid_sample_fwd(void* out, const void* in, const float* grid, int dtype, const int64_t* in_size,
+                                   const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
+                                   const int* dyn_hw, void* stream) {
+    return sg2::gs_fwd(out, in, grid, nullptr, dtype, in_size, in_stride, out_size, out_stride, dyn_hw, stream);
+}
+
+extern "C" int sg2_grid_sample_bwd(float* gin, const void* gout, const float* grid, int dtype, const int64_t* in_size,
+                                   const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
+                                   const int* dyn_hw, void* stream) {
+    return sg2::gs_bwd(gin, gout, grid, nullptr, dtype, in_size, in_stride, out_size, out_stride, dyn_hw, stream);
+}
+
+extern "C" int sg2_affine_grid_sample_fwd(void* out, const void* in, const float* theta, int dtype,
+                                          const int64_t* in_size, const int64_t* in_stride, const int64_t* out_size,
+                                          const int64_t* out_stride, const int* dyn_hw, void* stream) {
+    return sg2::gs_fwd(out, in, nullptr, theta, dtype, in_size, in_stride, out_size, out_stride, dyn_hw, stream);
+}
+
+extern "C" int sg2_affine_grid_sample_bwd(float* gin, const void* gout, const float* theta, int dtype,
+                                          const int64_t* in_size, const int64_t* in_stride, const int64_t* out_size,
+                                          const int64_t* out_stride, const int* dyn_hw, void* stream) {
+    return sg2::gs_bwd(gin, gout, nullptr, theta, dtype, in_size, in_stride, out_size, out_stride, dyn_hw, stream);
 }
 
 extern "C" int sg2_reflect_pad_dyn(float* y, const float* x, const int* margins, int N, int C, int H, int W, int Hs,

@@ -111,6 +111,47 @@ __global__ __launch_bounds__(256) void upfirdn_generic(UpfParams p) {
     }
 }
 
+// One separable pass (filter along x only, or along y only; the other axis is the identity): the two
+// launches of every 1-D-filter upfirdn2d (upfirdn2d.py:190-193), e.g. the ADA pipe's 12-tap sym6
+// up/down-sampling of single-channel images.  A workgroup owns 256 consecutive outputs of one output
+// row, so all index math is 32-bit and per-row terms (the vertical tap window, the lim test) are
+// uniform; reads are coalesced along x and the horizontal pass's neighbouring taps hit L1.
+template <typename T, bool HORIZ>
+__global__ __launch_bounds__(256) void upfirdn_1d(UpfParams p) {
+    __shared__ float sf[64];
+    const int F = HORIZ ? p.fw : p.fh;
+    for (int t = threadIdx.x; t < F; t += 256) sf[t] = p.f[p.flip ? t : F - 1 - t] * p.gain;
+    __syncthreads();
+    const int tiles = (p.OW + 255) / 256;
+    const int row = blockIdx.x / tiles;
+    const int ox = (blockIdx.x - row * tiles) * 256 + threadIdx.x;
+    const int oy = row % p.OH, nc = row / p.OH;
+    const int c = nc % p.C, n = nc / p.C;
+    if (ox >= p.OW) return;
+    T* yp = (T*)p.y + n * p.ys_n + c * p.ys_c + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w;
+    if (p.lim) {
+        const int ly = p.lim[0], lx = p.lim[1];
+        if (oy >= ly + kZeroBand || ox >= lx + kZeroBand) return;
+        if (oy >= ly || ox >= lx) { *yp = (T)0.f; return; }
+    }
+    const T* xb = (const T*)p.x + n * p.xs_n + c * p.xs_c;
+    float acc = 0.f;
+    if (HORIZ) {
+        int t0, i0;
+        axis_taps(ox, p.downx, p.padx0, p.upx, t0, i0);
+        const T* xr = xb + (int64_t)oy * p.xs_h;
+        for (int t = t0, ix = i0; t < F; t += p.upx, ++ix)
+            if (ix >= 0 && ix < p.W) acc += (float)xr[(int64_t)ix * p.xs_w] * sf[t];
+    } else {
+        int t0, i0;
+        axis_taps(oy, p.downy, p.pady0, p.upy, t0, i0);
+        const T* xc = xb + (int64_t)ox * p.xs_w;
+        for (int t = t0, iy = i0; t < F; t += p.upy, ++iy)
+            if (iy >= 0 && iy < p.H) acc += (float)xc[(int64_t)iy * p.xs_h] * sf[t];
+    }
+    *yp = (T)acc;
+}
+
 template <typename T> struct VecN { static constexpr int N = 8; };
 template <> struct VecN<float> { static constexpr int N = 4; };
 
@@ -416,6 +457,16 @@ int launch(const UpfParams& p, bool vec, hipStream_t s) {
                 if (!set2) { (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); set2 = true; }
                 k<<<(unsigned)blocks, 256, lds, s>>>(p);
             }
+            return launch_status("sg2_upfirdn2d");
+        }
+    }
+    if (!vec && !p.epi) {
+        const bool horiz = p.fh == 1 && p.upy == 1 && p.downy == 1 && p.pady0 == 0 && p.OH == p.H && p.fw <= 64;
+        const bool vert = p.fw == 1 && p.upx == 1 && p.downx == 1 && p.padx0 == 0 && p.OW == p.W && p.fh <= 64;
+        const int64_t blocks = (int64_t)p.N * p.C * p.OH * cdiv(p.OW, 256);
+        if ((horiz || vert) && blocks < INT32_MAX && (int64_t)p.N * p.C < INT32_MAX / 2) {
+            if (horiz) upfirdn_1d<T, true><<<(unsigned)blocks, 256, 0, s>>>(p);
+            else upfirdn_1d<T, false><<<(unsigned)blocks, 256, 0, s>>>(p);
             return launch_status("sg2_upfirdn2d");
         }
     }

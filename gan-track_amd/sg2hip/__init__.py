@@ -50,6 +50,8 @@ SIGNATURES = {
     'sg2_layer_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _f, _vp],
     'sg2_grid_sample_fwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
     'sg2_grid_sample_bwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
+    'sg2_affine_grid_sample_fwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
+    'sg2_affine_grid_sample_bwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
     'sg2_reflect_pad_dyn': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp],
     'sg2_demod_coefs': [_vp, _vp, _vp, _i, _i, _i, _i, _f, _vp],
     'sg2_demod_fwd': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp],

@@ -215,9 +215,9 @@ class AugmentPipe(torch.nn.Module):
         shape = [n, c, (h + hz_pad * 2) * 2, (w + hz_pad * 2) * 2]
         dyn_h, dyn_w = (h + my0 + my1) * 2, (w + mx0 + mx1) * 2     # logical size of the upsampled image
         G = scale2d(2 / dyn_w, 2 / dyn_h) @ G @ scale2d_inv(2 / shape[3], 2 / shape[2], device=dev)
-        grid = torch.nn.functional.affine_grid(theta=G[:, :2, :], size=shape, align_corners=False)
         dyn_hw = torch.stack([dyn_h, dyn_w]).to(torch.int32)
-        images = grid_sample_gradfix.grid_sample(images, grid, dyn_hw=dyn_hw)
+        # affine_grid + grid_sample (augment_mi.py:317-318) with the grid built inside the sampling kernel
+        images = grid_sample_gradfix.affine_grid_sample(images, G[:, :2, :], shape, dyn_hw=dyn_hw)
         return upfirdn2d.downsample2d(x=images, f=self.Hz_geom, down=2, padding=-hz_pad * 2, flip_filter=True)
 
     # ------------------------------------------------------------------ colour

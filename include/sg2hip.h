@@ -174,7 +174,18 @@ int sg2_grid_sample_bwd(float* gin, const void* gout, const float* grid, int dty
                         const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
                         const int* dyn_hw, void* stream);
 
-/* dyn_hw (both grid-sample calls; may be NULL): device int[2], the logical input height / width when
+/* The same two ops with the sampling grid built inline from theta (float32 [N,2,3] contiguous) as
+ * torch.nn.functional.affine_grid(theta, [N,C,Ho,Wo], align_corners=False) would build it: the fusion of
+ * SG3/training/augment_mi.py:317-318 (affine_grid + grid_sample_gradfix.grid_sample), which never
+ * materialises the [N,Ho,Wo,2] grid in HBM. */
+int sg2_affine_grid_sample_fwd(void* out, const void* in, const float* theta, int dtype, const int64_t* in_size,
+                               const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
+                               const int* dyn_hw, void* stream);
+int sg2_affine_grid_sample_bwd(float* gin, const void* gout, const float* theta, int dtype, const int64_t* in_size,
+                               const int64_t* in_stride, const int64_t* out_size, const int64_t* out_stride,
+                               const int* dyn_hw, void* stream);
+
+/* dyn_hw (all grid-sample calls; may be NULL): device int[2], the logical input height / width when
  * `in` is a larger static buffer whose valid region starts at the origin -- the ADA pipe's padded image
  * whose size depends on device-side margins (augment_mi.py:288-318), sampled without a host sync. */
 

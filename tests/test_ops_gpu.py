@@ -259,6 +259,33 @@ def test_grid_sample():
     assert rel_err(ggo, F.grid_sample(v.double(), grid.double(), align_corners=False)) < 1e-5
 
 
+
+def test_affine_grid_sample():
+    """Grid built inside the kernel (sg2_affine_grid_sample_*) vs affine_grid + grid_sample in fp64:
+    forward, input gradient, backward-of-backward; also with a static buffer + dyn_hw."""
+    from torch_utils.ops import grid_sample_gradfix as gs
+    torch.manual_seed(4)
+    x = torch.randn(2, 1, 40, 36)
+    theta = torch.tensor([[[1.05, 0.1, 0.03], [-0.08, 0.95, -0.02]], [[0.9, -0.2, 0.1], [0.15, 1.1, 0.05]]])
+    size = [2, 1, 50, 46]
+    grid = F.affine_grid(theta.double(), size, align_corners=False)
+    xd = x.to(DEV).requires_grad_(True)
+    y = gs.affine_grid_sample(xd, theta.to(DEV), size)
+    assert rel_err(y, F.grid_sample(x.double(), grid, align_corners=False)) < 1e-5
+    dy = torch.randn(y.shape)
+    dyd = dy.to(DEV).requires_grad_(True)
+    gx, = torch.autograd.grad(y, [xd], dyd, create_graph=True)
+    xr = x.double().requires_grad_(True)
+    gxr, = torch.autograd.grad(F.grid_sample(xr, grid, align_corners=False), [xr], dy.double())
+    assert rel_err(gx, gxr) < 1e-5
+    v = torch.randn(gx.shape)
+    ggo, = torch.autograd.grad((gx * v.to(DEV)).sum(), [dyd])
+    assert rel_err(ggo, F.grid_sample(v.double(), grid, align_corners=False)) < 1e-5
+    # logical 30 x 28 image at the origin of the 40 x 36 buffer
+    dyn = torch.tensor([30, 28], dtype=torch.int32, device=DEV)
+    y2 = gs.affine_grid_sample(xd, theta.to(DEV), size, dyn_hw=dyn)
+    assert rel_err(y2, F.grid_sample(x[:, :, :30, :28].double(), grid, align_corners=False)) < 1e-5
+
 # ------------------------------------------------------------------ modulated conv + conv layers (golden)
 CV = load('conv.npz')
 
