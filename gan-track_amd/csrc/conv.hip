@@ -182,7 +182,7 @@ __device__ __forceinline__ float epi_full(const Epi& e, float c, int n, int o, i
 
 // Implicit-GEMM convolution.  grid = (M tiles, Cout tiles, phases * splits).
 template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI, bool S3>
-__global__ __launch_bounds__(256, S3 ? 1 : 3) void conv_fwd_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
     static_assert(!S3 || std::is_same<T, float>::value, "the split form is for f32 operands");
     constexpr int BK = KStage<T, S3>::BK, V = Traits<T>::V;
     constexpr int LPR = BK / V;          // lanes per tile row
@@ -212,8 +212,10 @@ __global__ __launch_bounds__(256, S3 ? 1 : 3) void conv_fwd_kernel(ConvArgs a) {
 
     // --- per-thread load geometry (fixed across K) ---
     const int lrow = tid / LPR, lcol = (tid % LPR) * V;
-    int a_n[PA], a_qy[PA], a_qx[PA];
-    bool a_ok[PA];
+    // 32-bit element offsets (the host checks numel < 2^31): the row base is computed once, each K step
+    // adds a uniform tap offset, so the per-row cost of a prefetch is a bounds test and one add
+    int a_n[PA], a_qy[PA], a_qx[PA], a_base[PA], b_base[PB];
+    bool a_ok[PA], b_ok[PB];
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
         const int m = m0 + lrow + i * RPP;
@@ -224,8 +226,15 @@ __global__ __launch_bounds__(256, S3 ? 1 : 3) void conv_fwd_kernel(ConvArgs a) {
         const int r = mm - a_n[i] * per;
         a_qy[i] = (r / QW) * a.isy;
         a_qx[i] = (r % QW) * a.isx;
+        a_base[i] = ((a_n[i] * a.H + a_qy[i]) * a.W + a_qx[i]) * a.Cin;
     }
-    const int64_t wrow = (int64_t)a.wtaps * a.Cin;
+    const int wrow = a.wtaps * a.Cin;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+        const int o = n0 + lrow + i * RPP;
+        b_ok[i] = o < a.Cout;
+        b_base[i] = (b_ok[i] ? o : 0) * wrow;
+    }
 
     const int k_begin = split * a.kper;
     const int k_end = min(nk, k_begin + a.kper);
@@ -240,26 +249,24 @@ __global__ __launch_bounds__(256, S3 ? 1 : 3) void conv_fwd_kernel(ConvArgs a) {
         cur_c = c;
         const Tap tp = a.taps[tap0 + t];
         const int dy = tp.dy, dx = tp.dx, wt = tp.w;
+        const int tapoff = (dy * a.W + dx) * a.Cin;
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             const int iy = a_qy[i] + dy, ix = a_qx[i] + dx;
-            const bool ok = a_ok[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            const bool ok = a_ok[i] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
             ra_ok[i] = ok;
-            const T* row = x + (((int64_t)a_n[i] * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.Cin;
-            ra[i] = Loader<T, VEC>::load(row, c, a.Cin);
+            ra[i] = Loader<T, VEC>::load(x + (ok ? a_base[i] + tapoff : 0), c, a.Cin);
             if (SI) {
                 const float* sp = a.in_scale + (int64_t)a_n[i] * a.Cin;
 #pragma unroll
                 for (int j = 0; j < V; ++j) rsc[i][j] = sp[c + j < a.Cin ? c + j : 0];
             }
         }
+        const int woff = wt * a.Cin;
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
-            const int o = n0 + lrow + i * RPP;
-            const bool ok = o < a.Cout;
-            rb_ok[i] = ok;
-            const T* row = w + (ok ? o : 0) * wrow + (int64_t)wt * a.Cin;
-            rb[i] = Loader<T, VEC>::load(row, c, a.Cin);
+            rb_ok[i] = b_ok[i];
+            rb[i] = Loader<T, VEC>::load(w + b_base[i] + woff, c, a.Cin);
         }
     };
     typedef bf16_t bf16x4_t __attribute__((ext_vector_type(4)));
@@ -304,58 +311,75 @@ __global__ __launch_bounds__(256, S3 ? 1 : 3) void conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if (k_begin < k_end) {
-        gload(k_begin);
-        sstore(0);
-        __syncthreads();
-        for (int kc = k_begin; kc < k_end; ++kc) {
-            const int cur = (kc - k_begin) & 1;
-            const bool more = kc + 1 < k_end;
-            if (more) gload(kc + 1);
-            const T* As = lds + cur * BUF + (wm * WM) * LDK;
-            const T* Bs = lds + cur * BUF + BM * LDK + (wn * WN) * LDK;
-            if constexpr (S3) {
-                const bf16_t* P = lds3 + cur * BUF3;
-                const int ko = 8 * (lane >> 4);
-                bf16x8 af[TM][3], bfr[TN][3];
+    auto compute = [&](int cur) {
+        const T* As = lds + cur * BUF + (wm * WM) * LDK;
+        const T* Bs = lds + cur * BUF + BM * LDK + (wn * WN) * LDK;
+        if constexpr (S3) {
+            const bf16_t* P = lds3 + cur * BUF3;
+            const int ko = 8 * (lane >> 4);
+            bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) {
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-                        af[i][q] = *(const bf16x8*)(P + q * PLANE + (wm * WM + i * 16 + (lane & 15)) * S3LD + ko);
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        bfr[j][q] = *(const bf16x8*)(P + q * PLANE + (BM + wn * WN + j * 16 + (lane & 15)) * S3LD + ko);
-                }
+            for (int q = 0; q < 3; ++q) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
+                    af[i][q] = *(const bf16x8*)(P + q * PLANE + (wm * WM + i * 16 + (lane & 15)) * S3LD + ko);
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma_s3(af[i], bfr[j], acc[i][j]);
-            } else if constexpr (std::is_same<T, float>::value) {
-#pragma unroll
-                for (int kk = 0; kk < BK; kk += 4) {
-                    float af[TM], bfr[TN];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) af[i] = As[(i * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) bfr[j] = Bs[(j * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
-                }
-            } else {
-                const int ko = 8 * (lane >> 4);
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = mfma16<T>(As + (i * 16 + (lane & 15)) * LDK + ko,
-                                              Bs + (j * 16 + (lane & 15)) * LDK + ko, acc[i][j]);
+                for (int j = 0; j < TN; ++j)
+                    bfr[j][q] = *(const bf16x8*)(P + q * PLANE + (BM + wn * WN + j * 16 + (lane & 15)) * S3LD + ko);
             }
-            if (more) sstore(cur ^ 1);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma_s3(af[i], bfr[j], acc[i][j]);
+        } else if constexpr (std::is_same<T, float>::value) {
+#pragma unroll
+            for (int kk = 0; kk < BK; kk += 4) {
+                float af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) af[i] = As[(i * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bfr[j] = Bs[(j * 16 + (lane & 15)) * LDK + kk + (lane >> 4)];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        } else {
+            const int ko = 8 * (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = mfma16<T>(As + (i * 16 + (lane & 15)) * LDK + ko,
+                                          Bs + (j * 16 + (lane & 15)) * LDK + ko, acc[i][j]);
+        }
+    };
+    if (k_begin < k_end) {
+        if constexpr (S3) {
+            // one LDS buffer (the three bf16 planes of a K tile are 61 KB): two workgroups per CU, the
+            // next tile's global loads in flight during this tile's MFMAs
+            gload(k_begin);
+            for (int kc = k_begin; kc < k_end; ++kc) {
+                const bool more = kc + 1 < k_end;
+                sstore(0);
+                __syncthreads();
+                if (more) gload(kc + 1);
+                compute(0);
+                __syncthreads();
+            }
+        } else {
+            gload(k_begin);
+            sstore(0);
             __syncthreads();
+            for (int kc = k_begin; kc < k_end; ++kc) {
+                const int cur = (kc - k_begin) & 1;
+                const bool more = kc + 1 < k_end;
+                if (more) gload(kc + 1);
+                compute(cur);
+                if (more) sstore(cur ^ 1);
+                __syncthreads();
+            }
         }
     }
 
@@ -535,7 +559,7 @@ __global__ void conv_finalize_kernel(T* y, const float* src, Epi e, int64_t n_el
 template <typename T, int BM, int BN, bool S3>
 size_t fwd_lds_bytes() {
     constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
-    if (S3) return 2 * 3 * (size_t)(BM + BN) * S3LD * sizeof(bf16_t);
+    if (S3) return 3 * (size_t)(BM + BN) * S3LD * sizeof(bf16_t);   // one buffer (conv_fwd_kernel S3 loop)
     const size_t main = 2 * (size_t)(BM + BN) * (BK + V) * sizeof(T);
     const size_t epi = std::is_same<T, float>::value ? 0 : 2 * (size_t)BM * (64 + 8) * sizeof(T) + 64 * sizeof(float);
     return std::max(main, epi);
@@ -603,7 +627,7 @@ __device__ __forceinline__ v8_t<T> frag_tr(const T* base, int ld, int k0, int c0
 }
 
 template <typename T, int BM, int BN, bool VEC, bool S3>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+__global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a) {
     static_assert(!S3 || std::is_same<T, float>::value, "the split form is for f32 operands");
     constexpr int BK = KStage<T, S3>::BK, V = Traits<T>::V;
     constexpr int LDA = BM + V, LDB = BN + V;   // padded pixel-major rows
@@ -614,7 +638,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
     typedef typename Loader<T, VEC>::vecT vecT;
     // split form: [2][3 planes][BK][LDA3 + LDB3] bf16, pixel-major, read with ds_read_b64_tr_b16
     constexpr int LDA3 = BM + 8, LDB3 = BN + 8, PL3 = BK * (LDA3 + LDB3);
-    constexpr size_t BYTES = S3 ? 2 * 3 * (size_t)PL3 * 2 : 2 * (size_t)BK * (LDA + LDB) * sizeof(T);
+    // S3: one buffer (52 KB of bf16 planes; the loop below is single-buffered), three workgroups per CU
+    constexpr size_t BYTES = S3 ? 3 * (size_t)PL3 * 2 : 2 * (size_t)BK * (LDA + LDB) * sizeof(T);
 
     __shared__ __attribute__((aligned(16))) char lds_raw[BYTES];
     typedef T Row[BK * (LDA + LDB)];
@@ -737,59 +762,74 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if (p_begin < p_end) {
-        gload(p_begin);
-        sstore(0);
-        __syncthreads();
-        int it = 0;
-        for (int p0 = p_begin; p0 < p_end; p0 += BK, ++it) {
-            const int cur = it & 1;
-            const bool more = p0 + BK < p_end;
-            if (more) gload(p0 + BK);
-            const T* As = lds[cur];
-            const T* Bs = lds[cur] + BK * LDA;
-            if constexpr (S3) {
-                const bf16_t* P = lds3 + cur * 3 * PL3;
-                bf16x8 af[TM][3], bfr[TN][3];
+    auto compute = [&](int cur) {
+        const T* As = lds[cur];
+        const T* Bs = lds[cur] + BK * LDA;
+        if constexpr (S3) {
+            const bf16_t* P = lds3 + cur * 3 * PL3;
+            bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
-                for (int q = 0; q < 3; ++q) {
+            for (int q = 0; q < 3; ++q) {
 #pragma unroll
-                    for (int i = 0; i < TM; ++i) af[i][q] = frag_tr<bf16_t>(P + q * PL3, LDA3, 0, wm * WM + i * 16, lane);
+                for (int i = 0; i < TM; ++i) af[i][q] = frag_tr<bf16_t>(P + q * PL3, LDA3, 0, wm * WM + i * 16, lane);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    bfr[j][q] = frag_tr<bf16_t>(P + q * PL3 + BK * LDA3, LDB3, 0, wn * WN + j * 16, lane);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma_s3(af[i], bfr[j], acc[i][j]);
+        } else if constexpr (std::is_same<T, float>::value) {
+#pragma unroll
+            for (int kk = 0; kk < BK; kk += 4) {
+                float af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) af[i] = As[(kk + (lane >> 4)) * LDA + wm * WM + i * 16 + (lane & 15)];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bfr[j] = Bs[(kk + (lane >> 4)) * LDB + wn * WN + j * 16 + (lane & 15)];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        bfr[j][q] = frag_tr<bf16_t>(P + q * PL3 + BK * LDA3, LDB3, 0, wn * WN + j * 16, lane);
-                }
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma_s3(af[i], bfr[j], acc[i][j]);
-            } else if constexpr (std::is_same<T, float>::value) {
-#pragma unroll
-                for (int kk = 0; kk < BK; kk += 4) {
-                    float af[TM], bfr[TN];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) af[i] = As[(kk + (lane >> 4)) * LDA + wm * WM + i * 16 + (lane & 15)];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) bfr[j] = Bs[(kk + (lane >> 4)) * LDB + wn * WN + j * 16 + (lane & 15)];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
-                }
-            } else {
-                v8_t<T> af[TM], bfr[TN];
-#pragma unroll
-                for (int i = 0; i < TM; ++i) af[i] = frag_tr<T>(As, LDA, 0, wm * WM + i * 16, lane);
-#pragma unroll
-                for (int j = 0; j < TN; ++j) bfr[j] = frag_tr<T>(Bs, LDB, 0, wn * WN + j * 16, lane);
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma16v<T>(af[i], bfr[j], acc[i][j]);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
             }
-            if (more) sstore(cur ^ 1);
+        } else {
+            v8_t<T> af[TM], bfr[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = frag_tr<T>(As, LDA, 0, wm * WM + i * 16, lane);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bfr[j] = frag_tr<T>(Bs, LDB, 0, wn * WN + j * 16, lane);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma16v<T>(af[i], bfr[j], acc[i][j]);
+        }
+    };
+    if (p_begin < p_end) {
+        if constexpr (S3) {
+            gload(p_begin);
+            for (int p0 = p_begin; p0 < p_end; p0 += BK) {
+                const bool more = p0 + BK < p_end;
+                sstore(0);
+                __syncthreads();
+                if (more) gload(p0 + BK);
+                compute(0);
+                __syncthreads();
+            }
+        } else {
+            gload(p_begin);
+            sstore(0);
             __syncthreads();
+            int it = 0;
+            for (int p0 = p_begin; p0 < p_end; p0 += BK, ++it) {
+                const int cur = it & 1;
+                const bool more = p0 + BK < p_end;
+                if (more) gload(p0 + BK);
+                compute(cur);
+                if (more) sstore(cur ^ 1);
+                __syncthreads();
+            }
         }
     }
 

@@ -15,9 +15,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument('--which', default='halo,generic,wgrad,convT')
 ap.add_argument('--reps', type=int, default=20)
 ap.add_argument('--shapes', default='256x64,128x128,64x256,32x512')
+ap.add_argument('--dtype', default='float16')
 args = ap.parse_args()
 dev = torch.device('cuda', 0)
-dt = torch.float16
+dt = getattr(torch, args.dtype)
 
 
 def timeit(fn, reps):
