@@ -96,6 +96,32 @@ __device__ __forceinline__ void split3(float x, bf16_t& h, bf16_t& m, bf16_t& l)
     l = (bf16_t)r;
 }
 
+// split3 of four values on packed math: v_cvt_pk_bf16_f32 (round-to-nearest-even, as split3) and
+// v_pk_add_f32 residuals, ~4.5 VALU ops per element instead of ~7.5
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef bf16_t bf16x2_t __attribute__((ext_vector_type(2)));
+typedef bf16_t bf16x4_s3 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x2_t bf16x2_to_f32(unsigned u) {
+    return f32x2_t{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+__device__ __forceinline__ void split3x4(float x0, float x1, float x2, float x3, bf16x4_s3& h, bf16x4_s3& m,
+                                         bf16x4_s3& l) {
+    unsigned hu[2], mu[2], lu[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        f32x2_t r = q ? f32x2_t{x2, x3} : f32x2_t{x0, x1};
+        hu[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2_t));
+        r = r - bf16x2_to_f32(hu[q]);
+        mu[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2_t));
+        r = r - bf16x2_to_f32(mu[q]);
+        lu[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2_t));
+    }
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    h = __builtin_bit_cast(bf16x4_s3, u32x2_t{hu[0], hu[1]});
+    m = __builtin_bit_cast(bf16x4_s3, u32x2_t{mu[0], mu[1]});
+    l = __builtin_bit_cast(bf16x4_s3, u32x2_t{lu[0], lu[1]});
+}
+
 // acc += a * b over the six significant products of the split operands (small terms first)
 __device__ __forceinline__ f32x4 mfma_s3(const bf16x8* a, const bf16x8* b, f32x4 c) {
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
@@ -143,6 +169,17 @@ __device__ __forceinline__ f32x4 mfma16(const T* pa, const T* pb, f32x4 c) {
         f16x8 a = *(const f16x8*)pa, b = *(const f16x8*)pb;
         return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
     }
+}
+
+// Raw buffer loads (stride 0, num_records = the tensor's bytes): an offset past the end (-1 as
+// unsigned) returns zeros, which replaces the bounds select after a conditional load.  gfx9 dword3.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
+                                             (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
+}
+template <typename vecT>
+__device__ __forceinline__ vecT buf_load16(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(vecT, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
 }
 
 template <typename T, bool VEC>
@@ -239,6 +276,8 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
     const int k_begin = split * a.kper;
     const int k_end = min(nk, k_begin + a.kper);
 
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (int64_t)a.N * a.H * a.W * a.Cin * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, (int64_t)a.Cout * wrow * (int64_t)sizeof(T));
     vecT ra[PA], rb[PB];
     bool ra_ok[PA], rb_ok[PB];
     float rsc[SI ? PA : 1][V];
@@ -255,7 +294,10 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
             const int iy = a_qy[i] + dy, ix = a_qx[i] + dx;
             const bool ok = a_ok[i] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
             ra_ok[i] = ok;
-            ra[i] = Loader<T, VEC>::load(x + (ok ? a_base[i] + tapoff : 0), c, a.Cin);
+            if constexpr (VEC)   // out-of-range buffer offset: the hardware returns zeros, no mask
+                ra[i] = buf_load16<vecT>(rx, ok && c < a.Cin ? (a_base[i] + tapoff + c) * (int)sizeof(T) : -1);
+            else
+                ra[i] = Loader<T, VEC>::load(x + (ok ? a_base[i] + tapoff : 0), c, a.Cin);
             if (SI) {
                 const float* sp = a.in_scale + (int64_t)a_n[i] * a.Cin;
 #pragma unroll
@@ -266,19 +308,17 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
             rb_ok[i] = b_ok[i];
-            rb[i] = Loader<T, VEC>::load(w + b_base[i] + woff, c, a.Cin);
+            if constexpr (VEC)
+                rb[i] = buf_load16<vecT>(rw, b_ok[i] && c < a.Cin ? (b_base[i] + woff + c) * (int)sizeof(T) : -1);
+            else
+                rb[i] = Loader<T, VEC>::load(w + b_base[i] + woff, c, a.Cin);
         }
     };
     typedef bf16_t bf16x4_t __attribute__((ext_vector_type(4)));
     // split-f32 staging: row r of the buffer (A rows first, then B) gets the three planes of v
     auto store3 = [&](int buf, int r, const vecT& v) {
         bf16x4_t h, m, l;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            bf16_t a_, b_, c_;
-            split3((float)v[j], a_, b_, c_);
-            h[j] = a_; m[j] = b_; l[j] = c_;
-        }
+        split3x4((float)v[0], (float)v[1], (float)v[2], (float)v[3], h, m, l);
         bf16_t* p = lds3 + buf * BUF3 + r * S3LD + lcol;
         *(bf16x4_t*)p = h;
         *(bf16x4_t*)(p + PLANE) = m;
@@ -289,7 +329,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
         T* Bs = As + BM * LDK;
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
-            vecT v = Loader<T, VEC>::mask(ra[i], cur_c, a.Cin, ra_ok[i]);
+            vecT v = VEC ? ra[i] : Loader<T, VEC>::mask(ra[i], cur_c, a.Cin, ra_ok[i]);
             if (SI) {
 #pragma unroll
                 for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * rsc[i][j]);
@@ -299,7 +339,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
-            const vecT v = Loader<T, VEC>::mask(rb[i], cur_c, a.Cin, rb_ok[i]);
+            const vecT v = VEC ? rb[i] : Loader<T, VEC>::mask(rb[i], cur_c, a.Cin, rb_ok[i]);
             if constexpr (S3) store3(buf, BM + lrow + i * RPP, v);
             else *(vecT*)(Bs + (lrow + i * RPP) * LDK + lcol) = v;
         }
@@ -648,12 +688,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
     typedef bf16_t bf16x4_t __attribute__((ext_vector_type(4)));
     auto store3 = [&](int buf, int off, const vecT& v) {
         bf16x4_t h, m, l;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            bf16_t a_, b_, c_;
-            split3((float)v[j], a_, b_, c_);
-            h[j] = a_; m[j] = b_; l[j] = c_;
-        }
+        split3x4((float)v[0], (float)v[1], (float)v[2], (float)v[3], h, m, l);
         bf16_t* p = lds3 + buf * 3 * PL3 + off;
         *(bf16x4_t*)p = h;
         *(bf16x4_t*)(p + PL3) = m;
@@ -891,8 +926,9 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
     SG2_CHECK(KH >= 1 && KW >= 1 && KH * KW <= kMaxTaps, "sg2_conv2d: kernel too large");
     SG2_CHECK(stride >= 1 && stride <= 4, "sg2_conv2d: unsupported stride");
     SG2_CHECK(pad_y > -64 && pad_y < 64 && pad_x > -64 && pad_x < 64, "sg2_conv2d: padding out of range");
-    SG2_CHECK((int64_t)N * OH * OW * Cout < INT32_MAX && (int64_t)N * H * W * Cin < ((int64_t)1 << 40),
-              "sg2_conv2d: tensor too large");
+    SG2_CHECK((int64_t)N * OH * OW * Cout < INT32_MAX && (int64_t)N * H * W * Cin * 4 < INT32_MAX &&
+                  (int64_t)KH * KW * Cin * Cout * 4 < INT32_MAX,
+              "sg2_conv2d: tensor too large (32-bit byte offsets of the buffer loads)");
     if (epi) {
         SG2_CHECK(epi->act == 0 || epi->act == 1, "sg2_conv2d: epilogue act must be 0 (linear) or 1 (lrelu)");
         SG2_CHECK(epi->aux_mode >= 0 && epi->aux_mode <= 2 && (epi->aux_mode == 0 || epi->aux),
