@@ -171,17 +171,6 @@ __device__ __forceinline__ f32x4 mfma16(const T* pa, const T* pb, f32x4 c) {
     }
 }
 
-// Raw buffer loads (stride 0, num_records = the tensor's bytes): an offset past the end (-1 as
-// unsigned) returns zeros, which replaces the bounds select after a conditional load.  gfx9 dword3.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
-                                             (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
-}
-template <typename vecT>
-__device__ __forceinline__ vecT buf_load16(__amdgpu_buffer_rsrc_t r, int byte_off) {
-    return __builtin_bit_cast(vecT, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
-}
-
 template <typename T, bool VEC>
 struct Loader {
     // A 16-byte chunk of one tile row.  The load itself is unconditional (callers pass a clamped,
@@ -1061,6 +1050,8 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     SG2_CHECK(dw && g && x, "sg2_conv2d_wgrad: null pointer");
     SG2_CHECK(N > 0 && A > 0 && B > 0 && OH > 0 && OW > 0 && H > 0 && W > 0, "sg2_conv2d_wgrad: empty shape");
     SG2_CHECK(KH >= 1 && KW >= 1 && KH * KW <= 64, "sg2_conv2d_wgrad: kernel too large");
+    SG2_CHECK((int64_t)N * OH * OW * A * 4 < INT32_MAX && (int64_t)N * H * W * B * 4 < INT32_MAX,
+              "sg2_conv2d_wgrad: tensor too large (32-bit byte offsets of the buffer loads)");
     hipStream_t s = as_stream(stream);
     hipError_t e = hipMemsetAsync(dw, 0, (int64_t)A * KH * KW * B * sizeof(float), s);
     if (e != hipSuccess) { set_error("sg2_conv2d_wgrad: memset failed"); return (int)e; }

@@ -36,6 +36,17 @@ inline int launch_status(const char* what) {
     return 0;
 }
 
+// Raw buffer loads (stride 0, num_records = the tensor's bytes, < 2 GB): an offset past the end (-1 as
+// unsigned) returns zeros, which replaces the bounds select after a conditional load.  gfx9 dword3.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
+                                             (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL), 0x00020000);
+}
+template <typename vecT>
+__device__ __forceinline__ vecT buf_load16(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    return __builtin_bit_cast(vecT, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
 template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T)v; }
 

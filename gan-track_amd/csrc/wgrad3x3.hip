@@ -105,8 +105,10 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
     const bool a_ok = a0 + cc < a.A, b_ok = b0 + cc < a.B;
 
     vec8 rg[GCH], rx[XCH];
-    bool okg[GCH], okx[XCH];
     float gsc[8], xsc[8];
+    // 32-bit offsets into raw buffer loads (out-of-range pixels read as zeros: no mask in sstore)
+    const __amdgpu_buffer_rsrc_t rgb = make_rsrc(gp, (int64_t)a.N * a.GH * a.GW * a.A * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(xp, (int64_t)a.N * a.XH * a.XW * a.B * (int64_t)sizeof(T));
     auto gload = [&](int t) {
         const int per = a.tiles_x * a.tiles_y;
         const int n = t / per, r = t - n * per;
@@ -116,51 +118,37 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
             const int px = (tid >> 3) + i * 32;          // tile pixel
             const int oy = ty0 + px / TW, ox = tx0 + px % TW;
             const bool ok = a_ok && oy < a.GH && ox < a.GW;
-            okg[i] = ok;
-            const int64_t off = ((int64_t)(n * a.GH + (ok ? oy : 0)) * a.GW + (ok ? ox : 0)) * a.A + (a_ok ? a0 + cc : 0);
-            rg[i] = *(const vec8*)(gp + off);
+            rg[i] = buf_load16<vec8>(rgb, ok ? (((n * a.GH + oy) * a.GW + ox) * a.A + a0 + cc) * (int)sizeof(T) : -1);
         }
 #pragma unroll
         for (int i = 0; i < XCH; ++i) {
             const int hp = (tid >> 3) + i * 32;
             const int iy = (ty0 - 1 + hp / HWD) * a.S + a.PY, ix = (tx0 - 1 + hp % HWD) * a.S + a.PX;
-            const bool ok = b_ok && hp < HP && iy >= 0 && iy < a.XH && ix >= 0 && ix < a.XW;
-            okx[i] = ok;
-            const int64_t off = ((int64_t)(n * a.XH + (ok ? iy : 0)) * a.XW + (ok ? ix : 0)) * a.B + (b_ok ? b0 + cc : 0);
-            rx[i] = *(const vec8*)(xp + off);
+            const bool ok = b_ok && hp < HP && (unsigned)iy < (unsigned)a.XH && (unsigned)ix < (unsigned)a.XW;
+            rx[i] = buf_load16<vec8>(rxb, ok ? (((n * a.XH + iy) * a.XW + ix) * a.B + b0 + cc) * (int)sizeof(T) : -1);
         }
         if (a.gscale) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) gsc[j] = a.gscale[(int64_t)n * a.A + (a_ok ? a0 + cc + j : 0)];
+            for (int j = 0; j < 8; ++j) gsc[j] = a.gscale[n * a.A + (a_ok ? a0 + cc + j : 0)];
         }
         if (a.xscale) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) xsc[j] = a.xscale[(int64_t)n * a.B + (b_ok ? b0 + cc + j : 0)];
+            for (int j = 0; j < 8; ++j) xsc[j] = a.xscale[n * a.B + (b_ok ? b0 + cc + j : 0)];
         }
+    };
+    auto scale8 = [](vec8 v, const float* sc) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (T)((float)v[j] * sc[j]);
+        return v;
     };
     auto sstore = [&]() {
 #pragma unroll
-        for (int i = 0; i < GCH; ++i) {
-            vec8 v = rg[i];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                float f = okg[i] ? (float)v[j] : 0.f;
-                if (a.gscale) f *= gsc[j];
-                v[j] = (T)f;
-            }
-            *(vec8*)(gs + Lay<SWZ>::off((tid >> 3) + i * 32, cc)) = v;
-        }
+        for (int i = 0; i < GCH; ++i)
+            *(vec8*)(gs + Lay<SWZ>::off((tid >> 3) + i * 32, cc)) = a.gscale ? scale8(rg[i], gsc) : rg[i];
 #pragma unroll
         for (int i = 0; i < XCH; ++i) {
             const int hp = (tid >> 3) + i * 32;
-            vec8 v = rx[i];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                float f = okx[i] ? (float)v[j] : 0.f;
-                if (a.xscale) f *= xsc[j];
-                v[j] = (T)f;
-            }
-            if (hp < HP) *(vec8*)(xs + Lay<SWZ>::off(hp, cc)) = v;
+            if (hp < HP) *(vec8*)(xs + Lay<SWZ>::off(hp, cc)) = a.xscale ? scale8(rx[i], xsc) : rx[i];
         }
     };
 

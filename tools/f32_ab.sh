@@ -9,7 +9,7 @@ for v in new old; do
     echo "== $v"
     timeout -k 10 120 python -u tools/conv_micro.py --dtype float32 --which generic,wgrad --shapes 16x512,8x512,4x512 \
         > "$O/$v.log" 2>&1 || exit $?
-    timeout -k 10 120 python -u tools/conv_micro.py --dtype float16 --which generic,convT \
+    timeout -k 10 120 python -u tools/conv_micro.py --dtype float16 --which wgrad,generic \
         >> "$O/$v.log" 2>&1 || exit $?
     grep -v amdgpu.ids "$O/$v.log"
 done
