@@ -113,17 +113,22 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
     // Loads are unconditional (out-of-image / out-of-range lanes read a valid dummy address) and the
     // zero-fill + modulation happen at the LDS write, after the MFMAs: a branch around a load would
     // make hipcc drain vmcnt per load and serialise the prefetch against the math.
+    // Raw buffer loads: an out-of-image pixel, a row past Cout or a channel past Cin gets offset -1,
+    // which reads zeros (sg2_common.h make_rsrc), so the LDS write needs no select.
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(x, (int64_t)a.N * a.H * a.W * a.Cin * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rwb = make_rsrc(w, (int64_t)a.Cout * 9 * a.Cin * (int64_t)sizeof(T));
     vec8 rh[NH], rw[NW];
     float4 sc0, sc1;
-    bool cok = true;
     auto gload = [&](int chunk) {
         const int c = chunk * CK + hq;
-        cok = c < a.Cin;
+        const bool cok = c < a.Cin;
         const int cc = cok ? c : 0;
 #pragma unroll
-        for (int i = 0; i < NH; ++i) rh[i] = *(const vec8*)(x + (int64_t)h_src[i] * a.Cin + cc);
+        for (int i = 0; i < NH; ++i)
+            rh[i] = buf_load16<vec8>(rxb, h_ok[i] && cok ? (h_src[i] * a.Cin + c) * (int)sizeof(T) : -1);
 #pragma unroll
-        for (int i = 0; i < NW; ++i) rw[i] = *(const vec8*)(w + (int64_t)w_src[i] * a.Cin + cc);
+        for (int i = 0; i < NW; ++i)
+            rw[i] = buf_load16<vec8>(rwb, w_ok[i] && cok ? (w_src[i] * a.Cin + c) * (int)sizeof(T) : -1);
         if (SCALE_IN) {
             const float* sc = a.in_scale + (int64_t)n * a.Cin + cc;
             sc0 = *(const float4*)sc;
@@ -137,24 +142,15 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
 #pragma unroll
         for (int i = 0; i < NH; ++i) {
             if (h_dst[i] < 0) continue;
-            const bool ok = h_ok[i] && cok;
-            vec8 v;
+            vec8 v = rh[i];
+            if (SCALE_IN) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                float f = (float)rh[i][j];
-                if (SCALE_IN) f *= scl[j];
-                v[j] = (T)(ok ? f : 0.f);
+                for (int j = 0; j < 8; ++j) v[j] = (T)((float)v[j] * scl[j]);
             }
             *(vec8*)(hb + h_dst[i]) = v;
         }
 #pragma unroll
-        for (int i = 0; i < NW; ++i) {
-            const bool ok = w_ok[i] && cok;
-            vec8 v;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = ok ? rw[i][j] : (T)0.f;
-            *(vec8*)(wb + w_dst[i]) = v;
-        }
+        for (int i = 0; i < NW; ++i) *(vec8*)(wb + w_dst[i]) = rw[i];
     };
 
     // ---- per-lane fragment bases ----
@@ -352,7 +348,8 @@ extern "C" int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, i
     SG2_CHECK(((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0, "sg2_conv3x3: 16-byte alignment required");
     SG2_CHECK(act == 0 || act == 1, "sg2_conv3x3: act must be 0 (linear) or 1 (lrelu)");
     SG2_CHECK((dot_src == nullptr) == (dot_out == nullptr), "sg2_conv3x3: dot_src and dot_out go together");
-    SG2_CHECK((int64_t)N * H * W < INT32_MAX / 2, "sg2_conv3x3: tensor too large");
+    SG2_CHECK((int64_t)N * H * W * Cin * 2 < INT32_MAX && (int64_t)Cout * 9 * Cin * 2 < INT32_MAX,
+              "sg2_conv3x3: tensor too large (32-bit byte offsets of the buffer loads)");
     Conv3Args a{};
     a.x = x; a.w = w; a.y = y; a.y_raw = y_raw; a.in_scale = in_scale; a.out_scale = out_scale; a.noise = noise;
     a.bias = bias; a.dot_src = dot_src; a.dot_out = dot_out; a.noise_gain = noise_gain; a.alpha = alpha; a.gain = gain; a.clamp = clamp; a.act = act;
