@@ -57,32 +57,65 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(LBArgs a) {
         adb[j] = 0.f;
         add[j] = 0.f;
     }
-    const T* dyp = (const T*)a.dy;
-    const T* yp = (const T*)a.y;
-    const T* cp = (const T*)a.c;
     T* dcp = (T*)a.dc;
+    // U pixels per lane per iteration, all loads issued first (raw buffer loads: a pixel past the block
+    // reads zeros); the noise gradient sums the LP lanes of a pixel with xor shuffles when LP is a power
+    // of two <= 64 (C <= 512), else through LDS atomics.
+    constexpr int U = 4;
+    constexpr int V = 16 / sizeof(T) < 8 ? 16 / sizeof(T) : 8;   // elements per 16-byte load
+    constexpr int NL = 8 / V;                                     // 16-byte loads per 8 channels
+    typedef T vecv __attribute__((ext_vector_type(V)));
+    const int64_t bytes = (int64_t)a.N * a.HW * a.C * (int64_t)sizeof(T);
+    const __amdgpu_buffer_rsrc_t rdy = make_rsrc(a.dy, bytes), ry = make_rsrc(a.y, bytes),
+                                 rc = make_rsrc(a.c ? a.c : a.dy, bytes);
+    const bool has_c = a.c != nullptr;
+    const bool shfl = (LP & (LP - 1)) == 0 && LP <= 64;
     if (active) {
-        for (int p = p0 + pl; p < p1; p += PPP) {
-            const int64_t off = ((int64_t)n * a.HW + p) * a.C + c0;
-            const vec8 g = *(const vec8*)(dyp + off);
-            const vec8 yv = *(const vec8*)(yp + off);
-            vec8 cv;
-            if (cp) cv = *(const vec8*)(cp + off);
-            vec8 o;
-            float psum = 0.f;
+        for (int pb = p0 + pl; pb < p1; pb += PPP * U) {
+            vecv g[U][NL], yv[U][NL], cv[U][NL];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float yy = (float)yv[j];
-                float dz = (float)g[j] * a.gain;
-                if (a.act == 1 && !(yy > 0.f)) dz *= a.alpha;
-                if (a.clamp >= 0.f && !(yy > -a.clamp && yy < a.clamp)) dz = 0.f;
-                adb[j] += dz;
-                psum += dz;
-                if (cp) add[j] += dz * (float)cv[j];
-                o[j] = (T)(dz * dv[j]);
+            for (int u = 0; u < U; ++u) {
+                const int p = pb + u * PPP;
+                const int boff = p < p1 ? (int)((((int64_t)n * a.HW + p) * a.C + c0) * (int64_t)sizeof(T)) : -1;
+#pragma unroll
+                for (int l = 0; l < NL; ++l) {
+                    const int o = boff < 0 ? -1 : boff + 16 * l;
+                    g[u][l] = buf_load16<vecv>(rdy, o);
+                    yv[u][l] = buf_load16<vecv>(ry, o);
+                    if (has_c) cv[u][l] = buf_load16<vecv>(rc, o);
+                }
             }
-            *(vec8*)(dcp + off) = o;
-            if (a.dnoise) atomicAdd(&s_dn[p - p0], psum);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int p = pb + u * PPP;
+                float psum = 0.f;
+                vecv o[NL];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int l = j / V, e = j % V;
+                    const float yy = (float)yv[u][l][e];
+                    float dz = (float)g[u][l][e] * a.gain;
+                    if (a.act == 1 && !(yy > 0.f)) dz *= a.alpha;
+                    if (a.clamp >= 0.f && !(yy > -a.clamp && yy < a.clamp)) dz = 0.f;
+                    adb[j] += dz;
+                    psum += dz;
+                    if (has_c) add[j] += dz * (float)cv[u][l][e];
+                    o[l][e] = (T)(dz * dv[j]);
+                }
+                if (p < p1) {
+#pragma unroll
+                    for (int l = 0; l < NL; ++l)
+                        *(vecv*)(dcp + ((int64_t)n * a.HW + p) * a.C + c0 + l * V) = o[l];
+                }
+                if (a.dnoise) {
+                    if (shfl) {
+                        for (int m = 1; m < LP; m <<= 1) psum += __shfl_xor(psum, m);
+                        if (cg == 0 && p < p1) a.dnoise[(int64_t)n * a.HW + p] = psum;
+                    } else if (p < p1) {
+                        atomicAdd(&s_dn[p - p0], psum);
+                    }
+                }
+            }
         }
     }
     if (a.db || a.dd) {
@@ -98,7 +131,7 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(LBArgs a) {
         if (a.db) atomicAdd(&a.db[i], s_db[i]);
         if (a.dd) atomicAdd(&a.dd[(int64_t)n * a.C + i], s_dd[i]);
     }
-    if (a.dnoise)
+    if (a.dnoise && !shfl)
         for (int p = p0 + tid; p < p1; p += 256) a.dnoise[(int64_t)n * a.HW + p] = s_dn[p - p0];
 }
 
@@ -114,6 +147,7 @@ extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, cons
     SG2_CHECK(dtype == SG2_F16 || dtype == SG2_BF16 || dtype == SG2_F32, "sg2_layer_bwd: bad dtype");
     SG2_CHECK(act == 0 || act == 1, "sg2_layer_bwd: act must be linear or lrelu");
     if ((int64_t)N * HW == 0) return 0;
+    SG2_CHECK((int64_t)N * HW * C * 4 < INT32_MAX, "sg2_layer_bwd: tensor too large (32-bit buffer offsets)");
     hipStream_t s = as_stream(stream);
     if (db) { hipError_t e = hipMemsetAsync(db, 0, C * sizeof(float), s); if (e) { set_error("memset"); return e; } }
     if (dd) { hipError_t e = hipMemsetAsync(dd, 0, (int64_t)N * C * sizeof(float), s); if (e) { set_error("memset"); return e; } }
