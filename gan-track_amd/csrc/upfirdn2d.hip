@@ -116,40 +116,44 @@ __global__ __launch_bounds__(256) void upfirdn_generic(UpfParams p) {
 // up/down-sampling of single-channel images.  A workgroup owns 256 consecutive outputs of one output
 // row, so all index math is 32-bit and per-row terms (the vertical tap window, the lim test) are
 // uniform; reads are coalesced along x and the horizontal pass's neighbouring taps hit L1.
-template <typename T, bool HORIZ>
+template <typename T, bool HORIZ, int KT>
 __global__ __launch_bounds__(256) void upfirdn_1d(UpfParams p) {
+    // KT: taps per output (ceil(F / up)), unrolled so all of a lane's loads are in flight together.
+    // The grid strides over (row, 256-column tile) pairs inside the computed extent: with a device-side
+    // lim the skipped part of the static buffer costs no workgroups.
     __shared__ float sf[64];
     const int F = HORIZ ? p.fw : p.fh;
     for (int t = threadIdx.x; t < F; t += 256) sf[t] = p.f[p.flip ? t : F - 1 - t] * p.gain;
     __syncthreads();
-    const int tiles = (p.OW + 255) / 256;
-    const int row = blockIdx.x / tiles;
-    const int ox = (blockIdx.x - row * tiles) * 256 + threadIdx.x;
-    const int oy = row % p.OH, nc = row / p.OH;
-    const int c = nc % p.C, n = nc / p.C;
-    if (ox >= p.OW) return;
-    T* yp = (T*)p.y + n * p.ys_n + c * p.ys_c + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w;
-    if (p.lim) {
-        const int ly = p.lim[0], lx = p.lim[1];
-        if (oy >= ly + kZeroBand || ox >= lx + kZeroBand) return;
-        if (oy >= ly || ox >= lx) { *yp = (T)0.f; return; }
-    }
-    const T* xb = (const T*)p.x + n * p.xs_n + c * p.xs_c;
-    float acc = 0.f;
-    if (HORIZ) {
+    const int rows = p.lim ? min(p.OH, p.lim[0] + kZeroBand) : p.OH;
+    const int cols = p.lim ? min(p.OW, p.lim[1] + kZeroBand) : p.OW;
+    const int tiles = (cols + 255) / 256;
+    const int64_t total = (int64_t)p.N * p.C * rows * tiles;
+    for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
+        const int64_t row = b / tiles;
+        const int ox = (int)(b - row * tiles) * 256 + threadIdx.x;
+        const int oy = (int)(row % rows), nc = (int)(row / rows);
+        const int c = nc % p.C, n = nc / p.C;
+        if (ox >= cols) continue;
+        T* yp = (T*)p.y + n * p.ys_n + c * p.ys_c + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w;
+        if (p.lim && (oy >= p.lim[0] || ox >= p.lim[1])) { *yp = (T)0.f; continue; }
+        const T* xb = (const T*)p.x + n * p.xs_n + c * p.xs_c;
         int t0, i0;
-        axis_taps(ox, p.downx, p.padx0, p.upx, t0, i0);
-        const T* xr = xb + (int64_t)oy * p.xs_h;
-        for (int t = t0, ix = i0; t < F; t += p.upx, ++ix)
-            if (ix >= 0 && ix < p.W) acc += (float)xr[(int64_t)ix * p.xs_w] * sf[t];
-    } else {
-        int t0, i0;
-        axis_taps(oy, p.downy, p.pady0, p.upy, t0, i0);
-        const T* xc = xb + (int64_t)ox * p.xs_w;
-        for (int t = t0, iy = i0; t < F; t += p.upy, ++iy)
-            if (iy >= 0 && iy < p.H) acc += (float)xc[(int64_t)iy * p.xs_h] * sf[t];
+        if (HORIZ) axis_taps(ox, p.downx, p.padx0, p.upx, t0, i0);
+        else axis_taps(oy, p.downy, p.pady0, p.upy, t0, i0);
+        const int up = HORIZ ? p.upx : p.upy, L = HORIZ ? p.W : p.H;
+        const T* xl = HORIZ ? xb + (int64_t)oy * p.xs_h : xb + (int64_t)ox * p.xs_w;
+        const int64_t st = HORIZ ? p.xs_w : p.xs_h;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+            const int t = t0 + k * up, i = i0 + k;
+            const bool ok = t < F && i >= 0 && i < L;
+            const float v = (float)xl[(int64_t)(ok ? i : 0) * st];
+            acc += ok ? v * sf[t < F ? t : 0] : 0.f;
+        }
+        *yp = (T)acc;
     }
-    *yp = (T)acc;
 }
 
 template <typename T> struct VecN { static constexpr int N = 8; };
@@ -464,9 +468,14 @@ int launch(const UpfParams& p, bool vec, hipStream_t s) {
         const bool horiz = p.fh == 1 && p.upy == 1 && p.downy == 1 && p.pady0 == 0 && p.OH == p.H && p.fw <= 64;
         const bool vert = p.fw == 1 && p.upx == 1 && p.downx == 1 && p.padx0 == 0 && p.OW == p.W && p.fh <= 64;
         const int64_t blocks = (int64_t)p.N * p.C * p.OH * cdiv(p.OW, 256);
-        if ((horiz || vert) && blocks < INT32_MAX && (int64_t)p.N * p.C < INT32_MAX / 2) {
-            if (horiz) upfirdn_1d<T, true><<<(unsigned)blocks, 256, 0, s>>>(p);
-            else upfirdn_1d<T, false><<<(unsigned)blocks, 256, 0, s>>>(p);
+        const int up = horiz ? p.upx : p.upy, F = horiz ? p.fw : p.fh;
+        const int kt = (F + up - 1) / up;
+        if ((horiz || vert) && kt <= 16 && (int64_t)p.N * p.C < INT32_MAX / 2) {
+            const unsigned g = (unsigned)std::min<int64_t>(blocks, 256 * 64);
+#define U1D(KT_) { if (horiz) upfirdn_1d<T, true, KT_><<<g, 256, 0, s>>>(p); \
+                   else upfirdn_1d<T, false, KT_><<<g, 256, 0, s>>>(p); }
+            if (kt <= 4) U1D(4) else if (kt <= 8) U1D(8) else U1D(16)
+#undef U1D
             return launch_status("sg2_upfirdn2d");
         }
     }
