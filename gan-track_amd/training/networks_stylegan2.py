@@ -103,6 +103,39 @@ def modulated_conv2d(x, weight, styles, noise=None, up=1, down=1, padding=0, res
     return x
 
 
+class _Addmm(torch.autograd.Function):
+    """y = beta * b + alpha * x @ w^T with the scalars kept inside the GEMMs of the first-order backward too
+    (dx = alpha dy @ w, dw = alpha dy^T x as beta = 0 addmms; autograd of torch.addmm runs a GEMM and a
+    separate scale for each).  Under create_graph (the path-length pass through the affine layers) the
+    backward is built from differentiable ops."""
+
+    @staticmethod
+    def forward(ctx, b, x, w, beta, alpha):
+        ctx.save_for_backward(x, w)
+        ctx.beta, ctx.alpha = beta, alpha
+        return torch.addmm(b, x, w.t(), beta=beta, alpha=alpha)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        beta, alpha = ctx.beta, ctx.alpha
+        nb, nx, nw = ctx.needs_input_grad[:3]
+        if torch.is_grad_enabled():
+            return ((dy.sum(0) * beta) if nb else None, (dy @ w) * alpha if nx else None,
+                    (dy.t() @ x) * alpha if nw else None, None, None)
+        z = _zero_scalar(dy)
+        db = dy.sum(0) if nb else None
+        if db is not None and beta != 1:
+            db = db * beta
+        dx = torch.addmm(z, dy, w, beta=0, alpha=alpha) if nx else None
+        dw = torch.addmm(z, dy.t(), x, beta=0, alpha=alpha) if nw else None
+        return db, dx, dw, None, None
+
+
+def _zero_scalar(t):
+    return torch.empty((), dtype=t.dtype, device=t.device)   # beta = 0: never read
+
+
 @persistence.persistent_class
 class FullyConnectedLayer(torch.nn.Module):
     """:94-125"""
@@ -124,8 +157,8 @@ class FullyConnectedLayer(torch.nn.Module):
         if b is not None:
             b = b if b.dtype == x.dtype else b.to(x.dtype)
             if self.activation == 'linear':
-                return torch.addmm(b, x, w.t(), beta=self.bias_gain * out_gain, alpha=self.weight_gain * out_gain)
-            y = torch.addmm(b, x, w.t(), beta=self.bias_gain, alpha=self.weight_gain)
+                return _Addmm.apply(b, x, w, float(self.bias_gain * out_gain), float(self.weight_gain * out_gain))
+            y = _Addmm.apply(b, x, w, float(self.bias_gain), float(self.weight_gain))
             return bias_act.bias_act(y, None, act=self.activation)
         y = x.matmul((w * (self.weight_gain * out_gain)).t())
         return bias_act.bias_act(y, None, act=self.activation) if self.activation != 'linear' else y
