@@ -207,6 +207,49 @@ __device__ __forceinline__ float epi_full(const Epi& e, float c, int n, int o, i
 }
 
 // Implicit-GEMM convolution.  grid = (M tiles, Cout tiles, phases * splits).
+// 1x1 convolution with a tiny input depth (Cin <= 4: D's fromrgb on 1-channel images): an outer
+// product, HBM-bound on the Cout-wide output, so no GEMM tiling -- a lane owns one pixel x 8 output
+// channels, reads Cin inputs and 8 x Cin weights, applies the fused epilogue and writes 16 / 32 bytes.
+// Same operand rounding as conv_fwd_kernel (x * in_scale rounded to T before the product).
+template <typename T>
+__global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    const int OG = a.Cout / 8, HW = a.H * a.W;
+    const int64_t total = (int64_t)a.N * HW * OG;
+    const T* x = (const T*)a.x;
+    const T* w = (const T*)a.w;
+    for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+        const int64_t pix = idx / OG;
+        const int o0 = (int)(idx - pix * OG) * 8;
+        const int n = (int)(pix / HW);
+        float xv[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float v = c < a.Cin ? (float)x[pix * a.Cin + c] : 0.f;
+            if (a.in_scale && c < a.Cin) v = (float)(T)(v * a.in_scale[(int64_t)n * a.Cin + c]);
+            xv[c] = v;
+        }
+        vec8 yo, ao;
+        const bool resid = a.e.on && a.e.residual;
+        vec8 rv;
+        if (resid) rv = *(const vec8*)((const T*)a.e.residual + pix * a.Cout + o0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int o = o0 + j;
+            float c = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < a.Cin) c += xv[k] * (float)w[(int64_t)o * a.Cin + k];
+            float v = a.e.on ? epi_full<T>(a.e, c, n, o, pix, a.Cout) : c;
+            ao[j] = (T)(a.e.aux_mode == 1 ? c : v);
+            if (resid) v = (float)(T)v + (float)rv[j];
+            yo[j] = (T)v;
+        }
+        if (a.e.on && a.e.aux_mode) *(vec8*)((T*)a.e.aux + pix * a.Cout + o0) = ao;
+        *(vec8*)((T*)a.y + pix * a.Cout + o0) = yo;
+    }
+}
+
 template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI, bool S3>
 __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
     static_assert(!S3 || std::is_same<T, float>::value, "the split form is for f32 operands");
@@ -983,6 +1026,14 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
     }
 
     int rc = 0;
+    if (!transpose && KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W &&
+        Cin <= 4 && Cout % 8 == 0 && !base.e.dot_out && (uintptr_t)y % 32 == 0 &&
+        (!base.e.aux || (uintptr_t)base.e.aux % 32 == 0) && (!base.e.residual || (uintptr_t)base.e.residual % 32 == 0)) {
+        const int64_t total = (int64_t)N * H * W * (Cout / 8);
+        const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 64);
+        SG2_DISPATCH(dtype, T, { conv1x1_smallk_kernel<T><<<g, 256, 0, s>>>(base); });
+        return launch_status("sg2_conv2d (1x1, small Cin)");
+    }
     SG2_DISPATCH(dtype, T, {
         constexpr int V = Traits<T>::V;
         const int BK = (std::is_same<T, float>::value && !f32_exact()) ? KStage<float, true>::BK : Traits<T>::BK;
