@@ -214,13 +214,25 @@ __device__ __forceinline__ float epi_full(const Epi& e, float c, int n, int o, i
 template <typename T>
 __global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
-    const int OG = a.Cout / 8, HW = a.H * a.W;
+    const int OG = a.Cout / 8, HW = a.H * a.W;      // the host guarantees 256 % OG == 0: o0 is fixed per lane
     const int64_t total = (int64_t)a.N * HW * OG;
     const T* x = (const T*)a.x;
     const T* w = (const T*)a.w;
+    const int o0 = (int)(((int64_t)blockIdx.x * 256 + threadIdx.x) % OG) * 8;
+    float wv[8][4], bj[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wv[j][k] = k < a.Cin ? (float)w[(o0 + j) * a.Cin + k] : 0.f;
+        bj[j] = (a.e.on && a.e.bias) ? (float)(T)a.e.bias[o0 + j] : 0.f;
+    }
+    const bool on = a.e.on;
+    const float slope = (on && a.e.act == 1) ? a.e.alpha : 1.f, eg = on ? a.e.gain : 1.f;
+    const bool clamp_on = on && a.e.clamp >= 0.f;
+    const float cl = a.e.clamp;
+    const int aux_mode = on ? a.e.aux_mode : 0;
     for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
         const int64_t pix = idx / OG;
-        const int o0 = (int)(idx - pix * OG) * 8;
         const int n = (int)(pix / HW);
         float xv[4];
 #pragma unroll
@@ -229,23 +241,25 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
             if (a.in_scale && c < a.Cin) v = (float)(T)(v * a.in_scale[(int64_t)n * a.Cin + c]);
             xv[c] = v;
         }
-        vec8 yo, ao;
-        const bool resid = a.e.on && a.e.residual;
-        vec8 rv;
+        const float nv = (on && a.e.noise) ? (float)((const T*)a.e.noise)[pix] * a.e.noise_gain : 0.f;
+        vec8 yo, ao, rv;
+        const bool resid = on && a.e.residual;
         if (resid) rv = *(const vec8*)((const T*)a.e.residual + pix * a.Cout + o0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int o = o0 + j;
             float c = 0.f;
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < a.Cin) c += xv[k] * (float)w[(int64_t)o * a.Cin + k];
-            float v = a.e.on ? epi_full<T>(a.e, c, n, o, pix, a.Cout) : c;
-            ao[j] = (T)(a.e.aux_mode == 1 ? c : v);
+            for (int k = 0; k < 4; ++k) c += xv[k] * wv[j][k];
+            float v = c;
+            if (on && a.e.out_scale) v *= a.e.out_scale[(int64_t)n * a.Cout + o0 + j];
+            v = v + nv + bj[j];                       // epi_full order: scale, noise, bias, act, gain, clamp
+            v = (v > 0.f ? v : v * slope) * eg;
+            if (clamp_on) v = fminf(fmaxf(v, -cl), cl);
+            ao[j] = (T)(aux_mode == 1 ? c : v);
             if (resid) v = (float)(T)v + (float)rv[j];
             yo[j] = (T)v;
         }
-        if (a.e.on && a.e.aux_mode) *(vec8*)((T*)a.e.aux + pix * a.Cout + o0) = ao;
+        if (aux_mode) *(vec8*)((T*)a.e.aux + pix * a.Cout + o0) = ao;
         *(vec8*)((T*)a.y + pix * a.Cout + o0) = yo;
     }
 }
@@ -698,6 +712,103 @@ __device__ __forceinline__ v8_t<T> frag_tr(const T* base, int ld, int k0, int c0
     return __builtin_bit_cast(v8_t<T>, r);
 }
 
+// Weight gradient of a 1x1 convolution with a tiny input depth (B <= 4, fromrgb): dw[a][b] =
+// sum_p g[p,a] x[p,b] is a reduction of the A-wide gradient over all pixels, HBM-bound on g.  A lane
+// owns 8 output channels (fixed, as the grid stride is a multiple of A/8) and accumulates over its
+// pixels in registers; the block reduces through LDS and adds once per element to dw (zeroed).
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad1x1_smallb_kernel(WgradArgs a) {
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    __shared__ float red[2048];                       // [A][B], A * B <= 2048
+    const int OG = a.A / 8;
+    for (int i = threadIdx.x; i < a.A * a.B; i += 256) red[i] = 0.f;
+    __syncthreads();
+    const int64_t total = (int64_t)a.M * OG;
+    const int per = a.OH * a.OW;
+    const T* g = (const T*)a.g;
+    const T* x = (const T*)a.x;
+    int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int a0 = (int)(idx % OG) * 8;
+    float acc[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[j][k] = 0.f;
+    for (; idx < total; idx += (int64_t)gridDim.x * 256) {
+        const int64_t pix = idx / OG;
+        const int n = (int)(pix / per);
+        const vec8 gv = *(const vec8*)(g + pix * a.A + a0);
+        float xv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float v = k < a.B ? (float)x[pix * a.B + k] : 0.f;
+            if (a.b_scale && k < a.B) v = (float)(T)(v * a.b_scale[(int64_t)n * a.B + k]);
+            xv[k] = v;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float gj = (float)gv[j];
+            if (a.a_scale) gj = (float)(T)(gj * a.a_scale[(int64_t)n * a.A + a0 + j]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[j][k] += gj * xv[k];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < a.B) atomicAdd(&red[(a0 + j) * a.B + k], acc[j][k]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.A * a.B; i += 256) atomicAdd(a.dw + i, red[i]);
+}
+
+// Mirror for a tiny output depth (A <= 4, toRGB): the lane owns 8 input channels b of the wide x.
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad1x1_smalla_kernel(WgradArgs a) {
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    __shared__ float red[2048];                       // [A][B], A * B <= 2048
+    const int BG = a.B / 8;
+    for (int i = threadIdx.x; i < a.A * a.B; i += 256) red[i] = 0.f;
+    __syncthreads();
+    const int64_t total = (int64_t)a.M * BG;
+    const int per = a.OH * a.OW;
+    const T* g = (const T*)a.g;
+    const T* x = (const T*)a.x;
+    int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int b0 = (int)(idx % BG) * 8;
+    float acc[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+    for (; idx < total; idx += (int64_t)gridDim.x * 256) {
+        const int64_t pix = idx / BG;
+        const int n = (int)(pix / per);
+        const vec8 xv = *(const vec8*)(x + pix * a.B + b0);
+        float gk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float v = k < a.A ? (float)g[pix * a.A + k] : 0.f;
+            if (a.a_scale && k < a.A) v = (float)(T)(v * a.a_scale[(int64_t)n * a.A + k]);
+            gk[k] = v;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float xj = (float)xv[j];
+            if (a.b_scale) xj = (float)(T)(xj * a.b_scale[(int64_t)n * a.B + b0 + j]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k][j] += gk[k] * xj;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (k < a.A) atomicAdd(&red[k * a.B + b0 + j], acc[k][j]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.A * a.B; i += 256) atomicAdd(a.dw + i, red[i]);
+}
+
 template <typename T, int BM, int BN, bool VEC, bool S3>
 __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a) {
     static_assert(!S3 || std::is_same<T, float>::value, "the split form is for f32 operands");
@@ -1027,7 +1138,7 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
 
     int rc = 0;
     if (!transpose && KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W &&
-        Cin <= 4 && Cout % 8 == 0 && !base.e.dot_out && (uintptr_t)y % 32 == 0 &&
+        Cin <= 4 && Cout % 8 == 0 && 256 % (Cout / 8) == 0 && !base.e.dot_out && (uintptr_t)y % 32 == 0 &&
         (!base.e.aux || (uintptr_t)base.e.aux % 32 == 0) && (!base.e.residual || (uintptr_t)base.e.residual % 32 == 0)) {
         const int64_t total = (int64_t)N * H * W * (Cout / 8);
         const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 64);
@@ -1111,6 +1222,18 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     a.N = N; a.A = A; a.OH = OH; a.OW = OW; a.B = B; a.H = H; a.W = W; a.KH = KH; a.KW = KW;
     a.stride = stride; a.pady = pad_y; a.padx = pad_x;
     a.M = N * OH * OW;
+    if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W && B <= 4 &&
+        A % 8 == 0 && 256 % (A / 8) == 0 && A * B <= 2048 && (uintptr_t)g % 16 == 0) {
+        const int g_ = (int)std::min<int64_t>(cdiv((int64_t)a.M * (A / 8), 256), 1024);
+        SG2_DISPATCH(dtype, T, { wgrad1x1_smallb_kernel<T><<<g_, 256, 0, s>>>(a); });
+        return launch_status("sg2_conv2d_wgrad (1x1, small B)");
+    }
+    if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W && A <= 4 &&
+        B % 8 == 0 && 256 % (B / 8) == 0 && A * B <= 2048 && (uintptr_t)x % 16 == 0) {
+        const int g_ = (int)std::min<int64_t>(cdiv((int64_t)a.M * (B / 8), 256), 1024);
+        SG2_DISPATCH(dtype, T, { wgrad1x1_smalla_kernel<T><<<g_, 256, 0, s>>>(a); });
+        return launch_status("sg2_conv2d_wgrad (1x1, small A)");
+    }
     const bool halo = wgrad_halo_ok(dtype, KH, KW, stride, pad_y, pad_x, OW, A, B) && (uintptr_t)x % 16 == 0 &&
                       (uintptr_t)g % 16 == 0;
     if (halo) return wgrad3x3_launch(dw, g, x, g_scale, x_scale, dtype, N, A, OH, OW, B, H, W, KH, KW, stride, pad_y,

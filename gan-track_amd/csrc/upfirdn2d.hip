@@ -316,7 +316,8 @@ __device__ __forceinline__ void fir4_strip(const UpfParams& p, const vecT* base,
     }
     const float slope = (p.epi && p.act == 1) ? p.alpha : 1.f;
     const float eg = p.epi ? p.egain : 1.f;
-    const float cl = (p.epi && p.clamp >= 0.f) ? p.clamp : __builtin_inff();
+    const bool clamp_on = p.epi && p.clamp >= 0.f;
+    const float cl = p.clamp;
     const bool noise = p.epi && p.noise, resid = p.epi && p.residual;
     const int aux_mode = p.epi ? p.aux_mode : 0;
     float acc[TH][V];
@@ -348,7 +349,7 @@ __device__ __forceinline__ void fir4_strip(const UpfParams& p, const vecT* base,
         for (int j = 0; j < V; ++j) {
             float z = acc[od][j] * os[j] + nv + bj[j];
             z = (z > 0.f ? z : z * slope) * eg;
-            z = fminf(fmaxf(z, -cl), cl);
+            if (clamp_on) z = fminf(fmaxf(z, -cl), cl);
             o[j] = (T)z;
             ax[j] = (T)(aux_mode == 1 ? acc[od][j] : z);
         }

@@ -147,6 +147,8 @@ CONV_CASES = [
     (2, 32, 9, 9, 48, 3, 2, 0),
     (3, 16, 8, 8, 24, 1, 1, 0),
     (2, 1, 8, 8, 16, 1, 1, 0),
+    (2, 16, 8, 8, 1, 1, 1, 0),
+    (2, 64, 6, 6, 3, 1, 1, 0),
     (2, 3, 10, 10, 8, 3, 1, 1),
     (2, 13, 7, 7, 130, 3, 1, 1),
     (2, 513, 4, 4, 64, 3, 1, 1),
