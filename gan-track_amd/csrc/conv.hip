@@ -346,8 +346,17 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
                 ra[i] = Loader<T, VEC>::load(x + (ok ? a_base[i] + tapoff : 0), c, a.Cin);
             if (SI) {
                 const float* sp = a.in_scale + (int64_t)a_n[i] * a.Cin;
+                if constexpr (VEC) {   // c % V == 0 and Cin % V == 0: whole float4s (clamped to the row start)
+                    const float* q = sp + (c < a.Cin ? c : 0);
 #pragma unroll
-                for (int j = 0; j < V; ++j) rsc[i][j] = sp[c + j < a.Cin ? c + j : 0];
+                    for (int j = 0; j < V; j += 4) {
+                        const float4 f = *(const float4*)(q + j);
+                        rsc[i][j] = f.x; rsc[i][j + 1] = f.y; rsc[i][j + 2] = f.z; rsc[i][j + 3] = f.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < V; ++j) rsc[i][j] = sp[c + j < a.Cin ? c + j : 0];
+                }
             }
         }
         const int woff = wt * a.Cin;
@@ -1148,7 +1157,8 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
     SG2_DISPATCH(dtype, T, {
         constexpr int V = Traits<T>::V;
         const int BK = (std::is_same<T, float>::value && !f32_exact()) ? KStage<float, true>::BK : Traits<T>::BK;
-        const bool vec = (Cin % V == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)w % 16 == 0);
+        const bool vec = (Cin % V == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)w % 16 == 0) &&
+                         ((uintptr_t)in_scale % 16 == 0);
         const bool wide = Cout > 64;
         const int BN_ = wide ? 128 : 64;
         base.nck = (Cin + BK - 1) / BK;
