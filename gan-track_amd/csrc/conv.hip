@@ -854,6 +854,8 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
     const int ky = tap / a.KW, kx = tap % a.KW;
     const T* __restrict__ g = (const T*)a.g;
     const T* __restrict__ x = (const T*)a.x;
+    const __amdgpu_buffer_rsrc_t rgw = make_rsrc(g, (int64_t)a.M * a.A * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rxw = make_rsrc(x, (int64_t)a.N * a.H * a.W * a.B * (int64_t)sizeof(T));
 
     const int ga_row = tid / LPA, ga_col = (tid % LPA) * V;
     const int xb_row = tid / LPB, xb_col = (tid % LPB) * V;
@@ -870,15 +872,28 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
             const int m = p0 + r;
             const bool ok = r < BK && m < p_end;
             ra_ok[i] = ok;
-            const T* row = g + (int64_t)(ok ? m : 0) * a.A;
-            ra[i] = Loader<T, VEC>::load(row, a0 + ga_col, a.A);
+            if constexpr (VEC) {
+                ra[i] = buf_load16<vecT>(rgw, ok && a0 + ga_col < a.A ? (m * a.A + a0 + ga_col) * (int)sizeof(T) : -1);
+            } else {
+                const T* row = g + (int64_t)(ok ? m : 0) * a.A;
+                ra[i] = Loader<T, VEC>::load(row, a0 + ga_col, a.A);
+            }
             if (a.a_scale) {
                 const int n = (ok ? m : 0) / (a.OH * a.OW);
                 const float* sp = a.a_scale + (int64_t)n * a.A;
+                if constexpr (VEC) {
+                    const float* q = sp + (a0 + ga_col < a.A ? a0 + ga_col : 0);
 #pragma unroll
-                for (int j = 0; j < V; ++j) {
-                    const int c = a0 + ga_col + j;
-                    asc[i][j] = sp[c < a.A ? c : 0];
+                    for (int j = 0; j < V; j += 4) {
+                        const float4 f = *(const float4*)(q + j);
+                        asc[i][j] = f.x; asc[i][j + 1] = f.y; asc[i][j + 2] = f.z; asc[i][j + 3] = f.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < V; ++j) {
+                        const int c = a0 + ga_col + j;
+                        asc[i][j] = sp[c < a.A ? c : 0];
+                    }
                 }
             }
         }
@@ -898,14 +913,28 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
                 ok = ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
             }
             rb_ok[i] = ok;
-            const T* row = x + (((int64_t)n * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.B;
-            rb[i] = Loader<T, VEC>::load(row, b0 + xb_col, a.B);
+            if constexpr (VEC) {
+                rb[i] = buf_load16<vecT>(rxw, ok && b0 + xb_col < a.B
+                                                  ? (((n * a.H + iy) * a.W + ix) * a.B + b0 + xb_col) * (int)sizeof(T) : -1);
+            } else {
+                const T* row = x + (((int64_t)n * a.H + (ok ? iy : 0)) * a.W + (ok ? ix : 0)) * a.B;
+                rb[i] = Loader<T, VEC>::load(row, b0 + xb_col, a.B);
+            }
             if (a.b_scale) {
                 const float* sp = a.b_scale + (int64_t)n * a.B;
+                if constexpr (VEC) {
+                    const float* q = sp + (b0 + xb_col < a.B ? b0 + xb_col : 0);
 #pragma unroll
-                for (int j = 0; j < V; ++j) {
-                    const int b = b0 + xb_col + j;
-                    rsc[i][j] = sp[b < a.B ? b : 0];
+                    for (int j = 0; j < V; j += 4) {
+                        const float4 f = *(const float4*)(q + j);
+                        rsc[i][j] = f.x; rsc[i][j + 1] = f.y; rsc[i][j + 2] = f.z; rsc[i][j + 3] = f.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < V; ++j) {
+                        const int b = b0 + xb_col + j;
+                        rsc[i][j] = sp[b < a.B ? b : 0];
+                    }
                 }
             }
         }
@@ -916,7 +945,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             const int r = ga_row + i * RPA;
-            vecT v = Loader<T, VEC>::mask(ra[i], a0 + ga_col, a.A, ra_ok[i]);
+            vecT v = VEC ? ra[i] : Loader<T, VEC>::mask(ra[i], a0 + ga_col, a.A, ra_ok[i]);
             if (a.a_scale) {
 #pragma unroll
                 for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * asc[i][j]);
@@ -930,7 +959,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
             const int r = xb_row + i * RPB;
-            vecT v = Loader<T, VEC>::mask(rb[i], b0 + xb_col, a.B, rb_ok[i]);
+            vecT v = VEC ? rb[i] : Loader<T, VEC>::mask(rb[i], b0 + xb_col, a.B, rb_ok[i]);
             if (a.b_scale) {
 #pragma unroll
                 for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * rsc[i][j]);
@@ -1251,7 +1280,8 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     int rc = 0;
     SG2_DISPATCH(dtype, T, {
         constexpr int V = Traits<T>::V;
-        const bool vec = (A % V == 0) && (B % V == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)g % 16 == 0);
+        const bool vec = (A % V == 0) && (B % V == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)g % 16 == 0) &&
+                         ((uintptr_t)g_scale % 16 == 0) && ((uintptr_t)x_scale % 16 == 0);
         if (A > 64 && B > 64) rc = launch_wgrad<T, 128, 128>(a, vec, s);
         else if (A > 64) rc = launch_wgrad<T, 128, 64>(a, vec, s);
         else if (B > 64) rc = launch_wgrad<T, 64, 128>(a, vec, s);
