@@ -35,11 +35,11 @@ __global__ __launch_bounds__(256) void demod_kernel(float* d, const float* s, co
 
 // Demodulation with the per-(o, i) weight energy kept for the backward: wsq[o,i] = sum_k w^2 (written when
 // wsq_out != null), d[n,o] = rsqrt(sum_i s[n,i]^2 wsq[o,i] + eps).  One workgroup per o; after wsq is in
-// LDS each wave takes every fourth sample and reduces over i with shuffles (no block barrier per sample).
+// LDS, eight lanes per sample reduce a row of s each (32 samples per pass, no block barrier per sample).
 __global__ __launch_bounds__(256) void demod_fwd_kernel(float* d, float* wsq_out, const float* s, const float* w,
                                                         int N, int O, int I, int KK, float eps) {
     __shared__ float wsq[1024];
-    const int o = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int o = blockIdx.x;
     for (int i = threadIdx.x; i < I; i += 256) {
         const float* wr = w + ((int64_t)o * I + i) * KK;
         float acc = 0.f;
@@ -48,14 +48,24 @@ __global__ __launch_bounds__(256) void demod_fwd_kernel(float* d, float* wsq_out
         if (wsq_out) wsq_out[(int64_t)o * I + i] = acc;
     }
     __syncthreads();
-    for (int n = wave; n < N; n += 4) {
+    // 8 lanes per sample, 32 samples per pass: a lane sums a contiguous 1/8 of the row of s (all its loads
+    // independent), then three xor shuffles combine the eighths
+    const int seg = threadIdx.x & 7, len = (I + 7) / 8, i0 = seg * len, i1 = min(I, i0 + len);
+    for (int n0 = 0; n0 < N; n0 += 32) {
+        const int n = n0 + (threadIdx.x >> 3);
         float acc = 0.f;
-        for (int i = lane; i < I; i += 64) {
-            const float v = s[(int64_t)n * I + i];
-            acc += v * v * wsq[i];
+        if (n < N) {
+            const float* sr = s + (int64_t)n * I;
+#pragma unroll 8
+            for (int i = i0; i < i1; ++i) {
+                const float v = sr[i];
+                acc += v * v * wsq[i];
+            }
         }
-        for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-        if (lane == 0) d[(int64_t)n * O + o] = rsqrtf(acc + eps);
+        acc += __shfl_xor(acc, 1);
+        acc += __shfl_xor(acc, 2);
+        acc += __shfl_xor(acc, 4);
+        if (seg == 0 && n < N) d[(int64_t)n * O + o] = rsqrtf(acc + eps);
     }
 }
 
@@ -94,8 +104,17 @@ __global__ __launch_bounds__(256) void demod_bwd_s_kernel(float* gs, const float
     }
     __syncthreads();
     float acc = 0.f;
-    if (i < I)
-        for (int o = q; o < O; o += 4) acc += gu[o] * wsq[(int64_t)o * I + i];
+    if (i < I) {
+        // 16 independent loads in flight per lane (L2-latency bound otherwise)
+        float a4[4] = {0.f, 0.f, 0.f, 0.f};
+        int o = q;
+        for (; o + 60 < O; o += 64) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) a4[u & 3] += gu[o + 4 * u] * wsq[(int64_t)(o + 4 * u) * I + i];
+        }
+        for (; o < O; o += 4) a4[0] += gu[o] * wsq[(int64_t)o * I + i];
+        acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    }
     part[q][threadIdx.x & 63] = acc;
     __syncthreads();
     if (q == 0 && i < I)
