@@ -149,8 +149,13 @@ extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, cons
     if ((int64_t)N * HW == 0) return 0;
     SG2_CHECK((int64_t)N * HW * C * 4 < INT32_MAX, "sg2_layer_bwd: tensor too large (32-bit buffer offsets)");
     hipStream_t s = as_stream(stream);
-    if (db) { hipError_t e = hipMemsetAsync(db, 0, C * sizeof(float), s); if (e) { set_error("memset"); return e; } }
-    if (dd) { hipError_t e = hipMemsetAsync(dd, 0, (int64_t)N * C * sizeof(float), s); if (e) { set_error("memset"); return e; } }
+    if (db && dd == db + C) {   // adjacent accumulators (the Python wrapper's layout): one memset
+        hipError_t e = hipMemsetAsync(db, 0, ((int64_t)N + 1) * C * sizeof(float), s);
+        if (e) { set_error("memset"); return e; }
+    } else {
+        if (db) { hipError_t e = hipMemsetAsync(db, 0, C * sizeof(float), s); if (e) { set_error("memset"); return e; } }
+        if (dd) { hipError_t e = hipMemsetAsync(dd, 0, (int64_t)N * C * sizeof(float), s); if (e) { set_error("memset"); return e; } }
+    }
     LBArgs a{};
     a.dy = dy; a.y = y; a.c = c; a.d = d; a.dc = dc; a.db = db; a.dd = dd; a.dnoise = dnoise;
     a.N = N; a.HW = HW; a.C = C; a.alpha = alpha; a.gain = gain; a.clamp = clamp; a.act = act;

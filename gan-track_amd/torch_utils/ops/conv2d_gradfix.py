@@ -156,8 +156,13 @@ def layer_bwd(dy, y, c=None, d=None, act=1, alpha=0.2, gain=1.0, clamp=-1.0, wan
     n, ch, h, w = y.shape
     dc = torch.empty_like(y)
     f32 = dict(dtype=torch.float32, device=y.device)
-    db = torch.empty([ch], **f32) if want_db else None
-    dd = torch.empty([n, ch], **f32) if (want_dd and d is not None) else None
+    want_dd = want_dd and d is not None
+    if want_db and want_dd:   # one buffer: the library zeroes both accumulators with one memset
+        acc = torch.empty([ch + n * ch], **f32)
+        db, dd = acc[:ch], acc[ch:].view(n, ch)
+    else:
+        db = torch.empty([ch], **f32) if want_db else None
+        dd = torch.empty([n, ch], **f32) if want_dd else None
     dn = torch.empty([n, 1, h, w], **f32) if want_dnoise else None
     c = _nhwc(c) if c is not None else None
     _hip.check(_hip.lib().sg2_layer_bwd(
