@@ -303,9 +303,12 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_f4(UpfParams p) {
 // up-to-4 output rows that use it; an output row is stored as soon as its last input row is in.  The
 // layer epilogue (store_out's semantics) is resolved to per-lane constants once, so the per-row store
 // is branch-free apart from the uniform noise/residual/aux pointer tests.
-template <typename T, int V, typename vecT, int TW, int TH, int CG>
-__device__ __forceinline__ void fir4_strip(const UpfParams& p, const vecT* base, const float* wf, int n, int ty0,
-                                           int ox, int cv) {
+// SEP: the 4x4 taps are an exact outer product wf[ky][kx] = fy[ky] * fx[kx] (the [1,3,3,1] resample
+// filter): every input row is filtered horizontally once (4 FMAs) and the output rows combine those
+// row sums vertically (4 FMAs), 9.5 FMAs per output vector instead of 16.
+template <typename T, int V, typename vecT, int TW, int TH, int CG, bool SEP>
+__device__ __forceinline__ void fir4_strip(const UpfParams& p, const vecT* base, const float* wf, const float* fy,
+                                           const float* fx, int n, int ty0, int ox, int cv) {
     constexpr int F = 4, IW = TW + F - 1, IH = TH + F - 1;
     float os[V], bj[V];
 #pragma unroll
@@ -330,14 +333,31 @@ __device__ __forceinline__ void fir4_strip(const UpfParams& p, const vecT* base,
         vecT v[F];
 #pragma unroll
         for (int kx = 0; kx < F; ++kx) v[kx] = base[(ry * IW + kx) * CG];
+        if constexpr (SEP) {
+            float h[V];
 #pragma unroll
-        for (int ky = 0; ky < F; ++ky) {
-            const int o = ry - ky;                    // output row fed by input row ry through tap row ky
-            if (o < 0 || o >= TH) continue;
+            for (int j = 0; j < V; ++j) {
+                h[j] = 0.f;
 #pragma unroll
-            for (int kx = 0; kx < F; ++kx)
+                for (int kx = 0; kx < F; ++kx) h[j] += (float)v[kx][j] * fx[kx];
+            }
 #pragma unroll
-                for (int j = 0; j < V; ++j) acc[o][j] += (float)v[kx][j] * wf[ky * F + kx];
+            for (int ky = 0; ky < F; ++ky) {
+                const int o = ry - ky;
+                if (o < 0 || o >= TH) continue;
+#pragma unroll
+                for (int j = 0; j < V; ++j) acc[o][j] += h[j] * fy[ky];
+            }
+        } else {
+#pragma unroll
+            for (int ky = 0; ky < F; ++ky) {
+                const int o = ry - ky;                // output row fed by input row ry through tap row ky
+                if (o < 0 || o >= TH) continue;
+#pragma unroll
+                for (int kx = 0; kx < F; ++kx)
+#pragma unroll
+                    for (int j = 0; j < V; ++j) acc[o][j] += (float)v[kx][j] * wf[ky * F + kx];
+            }
         }
         const int od = ry - (F - 1);                  // output row completed by input row ry
         if (od < 0) continue;
@@ -422,7 +442,20 @@ __global__ __launch_bounds__(256, 2) void upfirdn_nhwc_f4s(UpfParams p) {
     __syncthreads();
     const int c = tid % CG, col = tid / CG;
     if (cv0 + c >= CV) return;
-    fir4_strip<T, V, vecT, TW, TH, CG>(p, tile + col * CG + c, wf, n, ty0, tx0 + col, cv0 + c);
+    // exact rank-1 test of the taps (uniform): wf = fy (x) fx with fy[ky] = wf[ky][0] / wf[0][0], fx = wf[0][:]
+    float fy[F], fx[F];
+    bool sep = wf[0] != 0.f;
+#pragma unroll
+    for (int k = 0; k < F; ++k) {
+        fx[k] = wf[k];
+        fy[k] = sep ? wf[k * F] / wf[0] : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < F * F; ++t) sep = sep && (fy[t / F] * fx[t % F] == wf[t]);
+    if (sep)
+        fir4_strip<T, V, vecT, TW, TH, CG, true>(p, tile + col * CG + c, wf, fy, fx, n, ty0, tx0 + col, cv0 + c);
+    else
+        fir4_strip<T, V, vecT, TW, TH, CG, false>(p, tile + col * CG + c, wf, fy, fx, n, ty0, tx0 + col, cv0 + c);
 }
 
 template <typename T>
