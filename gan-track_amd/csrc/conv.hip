@@ -264,6 +264,56 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
     }
 }
 
+// 1x1 convolution with a tiny output depth (Cout <= 4: G's toRGB, Cin % 8 == 0): a dot product per
+// pixel, HBM-bound on the Cin-wide input.  Eight lanes share a pixel, each summing every eighth
+// 8-channel chunk (16-byte loads, x * in_scale rounded to T as in conv_fwd_kernel), three xor shuffles
+// combine them and the group's first lane applies the epilogue.
+template <typename T>
+__global__ __launch_bounds__(256) void conv1x1_smallo_kernel(ConvArgs a) {
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    const int HW = a.H * a.W, NCH = a.Cin / 8, g = threadIdx.x & 7;
+    const int64_t npix = (int64_t)a.N * HW;
+    const T* x = (const T*)a.x;
+    const T* w = (const T*)a.w;
+    const bool on = a.e.on;
+    for (int64_t pix = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3; pix < npix; pix += (int64_t)gridDim.x * 32) {
+        const int n = (int)(pix / HW);
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int ch = g; ch < NCH; ch += 8) {
+            vec8 v = *(const vec8*)(x + pix * a.Cin + ch * 8);
+            if (a.in_scale) {
+                const float4 s0 = *(const float4*)(a.in_scale + (int64_t)n * a.Cin + ch * 8);
+                const float4 s1 = *(const float4*)(a.in_scale + (int64_t)n * a.Cin + ch * 8 + 4);
+                const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (T)((float)v[j] * sc[j]);
+            }
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                if (o >= a.Cout) break;
+                const vec8 wv = *(const vec8*)(w + (int64_t)o * a.Cin + ch * 8);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[o] += (float)v[j] * (float)wv[j];
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+            acc[o] += __shfl_xor(acc[o], 1);
+            acc[o] += __shfl_xor(acc[o], 2);
+            acc[o] += __shfl_xor(acc[o], 4);
+        }
+        if (g == 0) {
+            for (int o = 0; o < a.Cout; ++o) {
+                const float c = acc[o];
+                float v = on ? epi_full<T>(a.e, c, n, o, pix, a.Cout) : c;
+                if (on && a.e.aux_mode) ((T*)a.e.aux)[pix * a.Cout + o] = (T)(a.e.aux_mode == 1 ? c : v);
+                if (on && a.e.residual) v = (float)(T)v + (float)((const T*)a.e.residual)[pix * a.Cout + o];
+                ((T*)a.y)[pix * a.Cout + o] = (T)v;
+            }
+        }
+    }
+}
+
 template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI, bool S3>
 __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
     static_assert(!S3 || std::is_same<T, float>::value, "the split form is for f32 operands");
@@ -1175,7 +1225,16 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
     }
 
     int rc = 0;
-    if (!transpose && KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W &&
+    if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W && Cout <= 4 &&
+        Cin % 8 == 0 && Cin >= 8 && !base.e.dot_out && (uintptr_t)x % 16 == 0 && (uintptr_t)w % 16 == 0 &&
+        (uintptr_t)in_scale % 16 == 0 && dtype != SG2_F32) {
+        const int64_t groups = (int64_t)N * H * W;
+        const int g = (int)std::min<int64_t>(cdiv(groups * 8, 256), 256 * 64);
+        SG2_DISPATCH(dtype, T, { conv1x1_smallo_kernel<T><<<g, 256, 0, s>>>(base); });
+        return launch_status("sg2_conv2d (1x1, small Cout)");
+    }
+    // (a 1x1 stride-1 transposed conv is the same product with the caller's transposed pack: dgrad of toRGB)
+    if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W &&
         Cin <= 4 && Cout % 8 == 0 && 256 % (Cout / 8) == 0 && !base.e.dot_out && (uintptr_t)y % 32 == 0 &&
         (!base.e.aux || (uintptr_t)base.e.aux % 32 == 0) && (!base.e.residual || (uintptr_t)base.e.residual % 32 == 0)) {
         const int64_t total = (int64_t)N * H * W * (Cout / 8);
