@@ -778,3 +778,42 @@ def test_demod_kernel():
         ref.append([t.detach().double().cpu() for t in (d, gw, gs, gw2, gwf, gsf)])
     for a, b in zip(*ref):
         assert rel_err(a, b) < 1e-5
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('cin,cout', [(1, 64), (3, 16), (64, 1), (128, 3)])
+def test_conv1x1_small_depth(dtype, cin, cout):
+    """1x1 convolutions with <= 4 channels on one side (conv1x1_smallk / conv1x1_smallo, and the
+    1x1 weight gradients wgrad1x1_small{a,b}): modulation, the full epilogue (out_scale, noise, bias,
+    lrelu, gain, clamp, aux, residual) and the scaled weight gradient vs fp64."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(11)
+    n, h, w = 2, 9, 13
+    tol = {torch.float16: 3e-3, torch.bfloat16: 2e-2}[dtype]
+    x = torch.randn(n, cin, h, w).to(dtype)
+    wt = (torch.randn(cout, cin, 1, 1) / cin ** 0.5).to(dtype)
+    s_in = torch.rand(n, cin) + 0.5
+    s_out = torch.rand(n, cout) + 0.5
+    noise = torch.randn(n, h, w).to(dtype)
+    bias = torch.randn(cout).to(dtype).float()
+    res = torch.randn(n, cout, h, w).to(dtype)
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    for aux_mode in (1, 2):
+        y, aux = cg.conv_fused(xd, cg._pack_conv(wt.to(DEV)), cout, h, w, 1, 1, 1, (0, 0), in_scale=s_in.to(DEV),
+                               out_scale=s_out.to(DEV), noise=noise.to(DEV), noise_gain=0.3, bias=bias.to(DEV), act=1,
+                               alpha=0.2, gain=1.4, clamp=2.5, residual=res.to(DEV), aux_mode=aux_mode)
+        xs = (x.float() * s_in[:, :, None, None]).to(dtype).double()          # operand rounded as in the kernels
+        c = F.conv2d(xs, wt.double())
+        z = c * s_out[:, :, None, None].double() + noise[:, None].double() * 0.3 + bias[None, :, None, None].double()
+        z = (torch.where(z > 0, z, z * 0.2) * 1.4).clamp(-2.5, 2.5)
+        assert rel_err(aux.float(), c if aux_mode == 1 else z) < tol, (cin, cout, aux_mode)
+        assert rel_err(y.float(), z.to(dtype).double() + res.double()) < tol, (cin, cout, aux_mode)
+    # weight gradient of the 1x1 conv with both operands modulated
+    g = torch.randn(n, cout, h, w).to(dtype)
+    gs, xsc = torch.rand(n, cout) + 0.5, torch.rand(n, cin) + 0.5
+    dw = cg._wgrad_raw(g.to(DEV).contiguous(memory_format=torch.channels_last), xd, 1, 1, 1, (0, 0),
+                       x_scale=xsc.to(DEV), g_scale=gs.to(DEV))
+    ga = (g.float() * gs[:, :, None, None]).to(dtype).double()
+    xa = (x.float() * xsc[:, :, None, None]).to(dtype).double()
+    ref = torch.einsum('nahw,nbhw->ab', ga, xa)[:, :, None, None]
+    assert rel_err(dw.cpu(), ref) < 1e-4, (cin, cout)
