@@ -135,6 +135,37 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(LBArgs a) {
         for (int p = p0 + tid; p < p1; p += 256) a.dnoise[(int64_t)n * a.HW + p] = s_dn[p - p0];
 }
 
+// out[n, c] = sum_p a[n, p, c] * b[n, p, c] over the pixels of NHWC tensors, f32 accumulation: the
+// modulation / demodulation gradients of the path-length pass (sum_p dz*c, sum_p dxs*x), which autograd
+// would run as a full-size multiply plus a reduction.  Same lane layout as layer_bwd_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void dot_hw_kernel(float* out, const T* a, const T* b, int HW, int C,
+                                                     int pix_per_block) {
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    extern __shared__ __attribute__((aligned(16))) float red[];   // [C]
+    const int LP = C / 8, PPP = 256 / LP;
+    const int tid = threadIdx.x, n = blockIdx.y;
+    const int p0 = blockIdx.x * pix_per_block, p1 = min(HW, p0 + pix_per_block);
+    for (int i = tid; i < C; i += 256) red[i] = 0.f;
+    __syncthreads();
+    const int cg = tid % LP, pl = tid / LP;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    if (pl < PPP) {
+        for (int p = p0 + pl; p < p1; p += PPP) {
+            const int64_t off = ((int64_t)n * HW + p) * C + cg * 8;
+            const vec8 av = *(const vec8*)(a + off), bv = *(const vec8*)(b + off);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += (float)(T)((float)av[j] * (float)bv[j]);   // product rounded as torch's
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomicAdd(&red[cg * 8 + j], acc[j]);
+    }
+    __syncthreads();
+    for (int i = tid; i < C; i += 256) atomicAdd(&out[(int64_t)n * C + i], red[i]);
+}
+
 }  // namespace
 }  // namespace sg2
 
@@ -169,4 +200,23 @@ extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, cons
     else if (dtype == SG2_BF16) layer_bwd_kernel<bf16_t><<<grid, 256, lds, s>>>(a);
     else layer_bwd_kernel<float><<<grid, 256, lds, s>>>(a);
     return launch_status("sg2_layer_bwd");
+}
+
+extern "C" int sg2_dot_hw(float* out, const void* a, const void* b, int dtype, int N, int HW, int C, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(out && a && b, "sg2_dot_hw: null pointer");
+    SG2_CHECK(C % 8 == 0 && C >= 8 && C <= 2048, "sg2_dot_hw: C must be a multiple of 8 (<= 2048)");
+    SG2_CHECK(dtype == SG2_F16 || dtype == SG2_BF16, "sg2_dot_hw: f16/bf16 only");
+    SG2_CHECK(((uintptr_t)a % 16) == 0 && ((uintptr_t)b % 16) == 0, "sg2_dot_hw: 16-byte alignment required");
+    if ((int64_t)N * HW == 0) return 0;
+    hipStream_t s = as_stream(stream);
+    hipError_t e = hipMemsetAsync(out, 0, (int64_t)N * C * sizeof(float), s);
+    if (e) { set_error("sg2_dot_hw: memset failed"); return e; }
+    const int PPP = std::max(1, 256 / (C / 8));
+    const int ppb = std::min(HW, PPP * 32);
+    dim3 grid((unsigned)cdiv(HW, ppb), (unsigned)N);
+    const size_t lds = C * sizeof(float);
+    if (dtype == SG2_F16) dot_hw_kernel<f16_t><<<grid, 256, lds, s>>>(out, (const f16_t*)a, (const f16_t*)b, HW, C, ppb);
+    else dot_hw_kernel<bf16_t><<<grid, 256, lds, s>>>(out, (const bf16_t*)a, (const bf16_t*)b, HW, C, ppb);
+    return launch_status("sg2_dot_hw");
 }

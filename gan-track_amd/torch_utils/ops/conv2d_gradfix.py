@@ -172,6 +172,35 @@ def layer_bwd(dy, y, c=None, d=None, act=1, alpha=0.2, gain=1.0, clamp=-1.0, wan
     return dc, db, dd, dn
 
 
+class _DotHW(torch.autograd.Function):
+    """out[n, c] = sum_{h,w} round(a * b) in f32 (sg2_dot_hw): (a * b).sum([2, 3], dtype=float32) without
+    the full-size product in HBM.  The backward is composed of differentiable ops (double backward)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = _nhwc(a), _nhwc(b)
+        n, c, h, w = a.shape
+        out = torch.empty([n, c], dtype=torch.float32, device=a.device)
+        _hip.check(_hip.lib().sg2_dot_hw(_hip.ptr(out), _hip.ptr(a), _hip.ptr(b), _hip.dtype_code(a), n, h * w, c,
+                                         _hip.stream_ptr(a.device)), 'sg2_dot_hw')
+        ctx.save_for_backward(a, b)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g_ = g.to(a.dtype)[:, :, None, None]
+        return (g_ * b if ctx.needs_input_grad[0] else None), (g_ * a if ctx.needs_input_grad[1] else None)
+
+
+def dot_hw(a, b):
+    """(a * b).sum([2, 3], dtype=float32) for 16-bit [N, C, H, W] tensors (C % 8 == 0) on the HIP kernel."""
+    if a.dtype in (torch.float16, torch.bfloat16) and b.dtype == a.dtype and a.shape == b.shape and \
+            a.shape[1] % 8 == 0 and a.is_cuda:
+        return _DotHW.apply(a, b)
+    return (a * b).sum([2, 3], dtype=torch.float32)
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pad, out_hw):

@@ -170,14 +170,14 @@ def _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c
             c_ = _cg._Conv2d.apply(_mul(x, s_), weight.to(dt), stride, (pad, pad), (oh, ow))
         else:
             c_ = c
-        dd = (dz * c_).sum([2, 3], dtype=torch.float32).to(dcoefs.dtype)
+        dd = _cg.dot_hw(dz, c_).to(dcoefs.dtype)
     dc = dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None else dz
     if need[0] or need[1]:
         dxs = _cg._ConvT2d.apply(dc, weight.to(dt), stride, (pad, pad), (h, w))
         if need[0]:
             dx = _mul(dxs, s_)
         if need[1] and styles is not None:
-            ds = (dxs * x).sum([2, 3], dtype=torch.float32).to(styles.dtype)
+            ds = _cg.dot_hw(dxs, x).to(styles.dtype)
     if need[2] and not _cg.weight_gradients_disabled:
         dw = _cg._WGrad.apply(dc, _mul(x, s_), (kh, kw), stride, (pad, pad)).to(weight.dtype)
     return dx, ds, dw, dd, dnoise, db
@@ -285,7 +285,7 @@ class UpModConv(torch.autograd.Function):
             if need[3] and dcoefs is not None:
                 t_ = _cg._ConvT2d.apply(xs, wt, 2, tpad, (th, tw))
                 c_ = _up.upfirdn2d(t_, f, padding=fpad, gain=4)
-                dd = (dz * c_).sum([2, 3], dtype=torch.float32)
+                dd = _cg.dot_hw(dz, c_)
             dc = dz * dcoefs.to(dt).reshape(n, -1, 1, 1)
             dt_ = _up.upfirdn2d(dc, f, up=aup, down=adown, padding=apad, flip_filter=aflip, gain=4)
             if need[0] or need[1]:
@@ -293,7 +293,7 @@ class UpModConv(torch.autograd.Function):
                 if need[0]:
                     dx = dxs * s_
                 if need[1]:
-                    ds = (dxs * x).sum([2, 3], dtype=torch.float32)
+                    ds = _cg.dot_hw(dxs, x)
             if need[2] and not _cg.weight_gradients_disabled:
                 dw = _cg._WGrad.apply(xs, dt_, (kh, kw), 2, tpad).transpose(0, 1)
         cast = lambda g, ref: g.to(ref.dtype) if (g is not None and ref is not None) else g

@@ -161,6 +161,12 @@ int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, const void* dy,
                   const float* d, int dtype, int N, int HW, int C, int act, float alpha, float gain, float clamp,
                   void* stream);
 
+/* out[n, c] = sum_p a[n, p, c] * b[n, p, c] (f32 accumulation; a, b: [N, HW, C] NHWC f16/bf16, C % 8 == 0;
+ * out zeroed by the call).  The reductions (dz * c).sum([2, 3]) and (dxs * x).sum([2, 3]) of the
+ * modulated-conv backward (SG3/training/networks_stylegan2.py:59-70 under autograd) without the
+ * full-size product in HBM. */
+int sg2_dot_hw(float* out, const void* a, const void* b, int dtype, int N, int HW, int C, void* stream);
+
 /* Bilinear grid sample, zeros padding, align_corners = False (the only mode the reference uses,
  * grid_sample_gradfix.py:9-12).  in [N,C,Hi,Wi] any strides; grid float32 [N,Ho,Wo,2] contiguous;
  * out [N,C,Ho,Wo] any strides. */

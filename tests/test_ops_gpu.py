@@ -817,3 +817,25 @@ def test_conv1x1_small_depth(dtype, cin, cout):
     xa = (x.float() * xsc[:, :, None, None]).to(dtype).double()
     ref = torch.einsum('nahw,nbhw->ab', ga, xa)[:, :, None, None]
     assert rel_err(dw.cpu(), ref) < 1e-4, (cin, cout)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_dot_hw(dtype):
+    """sg2_dot_hw (sum over pixels of a rounded 16-bit product, f32 accumulation) and its differentiable
+    wrapper vs the composed (a * b).sum([2, 3], dtype=float32): value, gradient, double backward."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(5)
+    a = torch.randn(3, 64, 11, 17, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(3, 64, 11, 17, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    a1, b1 = a.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    a2, b2 = a.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    y1 = cg.dot_hw(a1, b1)
+    y2 = (a2 * b2).sum([2, 3], dtype=torch.float32)
+    assert rel_err(y1, y2.double().cpu()) < 1e-5
+    g = torch.randn(3, 64, device=DEV)
+    ga1, gb1 = torch.autograd.grad(y1, [a1, b1], g, create_graph=True)
+    ga2, gb2 = torch.autograd.grad(y2, [a2, b2], g, create_graph=True)
+    assert rel_err(ga1.float(), ga2.double().cpu()) < 1e-3 and rel_err(gb1.float(), gb2.double().cpu()) < 1e-3
+    h1, = torch.autograd.grad((ga1.float() ** 2).sum(), [b1])
+    h2, = torch.autograd.grad((ga2.float() ** 2).sum(), [b2])
+    assert rel_err(h1.float(), h2.double().cpu()) < 1e-2
