@@ -146,6 +146,23 @@ __global__ __launch_bounds__(256) void lerp_kernel(float* __restrict__ dst, cons
     }
 }
 
+
+// Conv weight pack: out[a][k][b] = in[a*sa + b*sb + k'*sk] (k' = K-1-k when flip), cast to Tout.  One lane
+// per output element: the stores are coalesced runs of b, the gathered loads of a wavefront touch the same
+// cache lines as its neighbours' (the other taps of the same rows), so the input is read from HBM once.
+// Every lane issues its single load at once -- no serial per-lane loop, which left small packs
+// latency-bound.  Replaces the strided-permute copy of _pack_conv / _pack_convT.
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(256) void pack_weight_kernel(Tout* __restrict__ out, const Tin* __restrict__ in, int A,
+                                                          int B, int K, int64_t sa, int64_t sb, int64_t sk, int flip) {
+    const unsigned e = blockIdx.x * 256u + threadIdx.x;      // 32-bit index math (A*B*K < 2^31, host-checked)
+    if (e >= (unsigned)A * B * K) return;
+    const unsigned r = e / (unsigned)B, b = e - r * B;
+    const unsigned a = r / (unsigned)K, k = r - a * K;
+    const int kk = flip ? K - 1 - (int)k : (int)k;
+    out[e] = from_f32<Tout>(to_f32(in[(int64_t)a * sa + (int64_t)b * sb + kk * sk]));
+}
+
 }  // namespace
 }  // namespace sg2
 
@@ -209,4 +226,17 @@ extern "C" int sg2_lerp(float* dst, const float* src, int64_t n, float beta, voi
     const int g = (int)std::min<int64_t>(cdiv(n, 256), 8192);
     lerp_kernel<<<g, 256, 0, as_stream(stream)>>>(dst, src, n, beta);
     return launch_status("sg2_lerp");
+}
+
+extern "C" int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_dtype, int A, int B, int K,
+                               int64_t sa, int64_t sb, int64_t sk, int flip, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(out && in, "sg2_pack_weight: null pointer");
+    SG2_CHECK(A > 0 && B > 0 && K >= 1 && K <= 9 && (int64_t)A * B * K < (1LL << 31),
+              "sg2_pack_weight: unsupported shape (K <= 9, A*B*K < 2^31)");
+    const unsigned grid = (unsigned)cdiv((int64_t)A * B * K, 256);
+    hipStream_t s = as_stream(stream);
+    SG2_DISPATCH(in_dtype, Tin, SG2_DISPATCH(out_dtype, Tout,
+        pack_weight_kernel<Tin, Tout><<<grid, 256, 0, s>>>((Tout*)out, (const Tin*)in, A, B, K, sa, sb, sk, flip)));
+    return launch_status("sg2_pack_weight");
 }

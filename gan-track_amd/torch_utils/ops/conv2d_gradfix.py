@@ -112,14 +112,30 @@ def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None):
     return dw.permute(0, 3, 1, 2)
 
 
-def _pack_conv(w, dtype=None):      # [O, I, kh, kw] -> [O][kh][kw][I], cast to dtype in the same copy
-    out = torch.empty([w.shape[0], w.shape[2], w.shape[3], w.shape[1]], dtype=dtype or w.dtype, device=w.device)
-    return out.copy_(w.permute(0, 2, 3, 1))
+def _pack(w, a_dim, dtype, flip):
+    """out[a][ky][kx][b] = w[.., ky', kx'] with (a, b) = dims (a_dim, 1 - a_dim) of w, cast to dtype, the
+    taps reversed when flip -- one sg2_pack_weight launch (LDS-tiled transpose) instead of a strided copy."""
+    b_dim = 1 - a_dim
+    A, B, kh, kw = w.shape[a_dim], w.shape[b_dim], w.shape[2], w.shape[3]
+    if kh * kw > 9:    # no such conv in the networks; layout copy on the device
+        w = w.flip([2, 3]) if flip else w
+        return w.permute(a_dim, 2, 3, b_dim).to(dtype or w.dtype, memory_format=torch.contiguous_format)
+    if w.stride(2) != kw * w.stride(3):
+        w = w.contiguous()
+    out = torch.empty([A, kh, kw, B], dtype=dtype or w.dtype, device=w.device)
+    _hip.require_device(w)
+    _hip.check(_hip.lib().sg2_pack_weight(
+        _hip.ptr(out), _hip.dtype_code(out), _hip.ptr(w), _hip.dtype_code(w), A, B, kh * kw, w.stride(a_dim),
+        w.stride(b_dim), w.stride(3), 1 if flip else 0, _hip.stream_ptr(w.device)), 'sg2_pack_weight')
+    return out
 
 
-def _pack_convT(w, dtype=None):     # [I, O, kh, kw] -> [O][kh][kw][I]
-    out = torch.empty([w.shape[1], w.shape[2], w.shape[3], w.shape[0]], dtype=dtype or w.dtype, device=w.device)
-    return out.copy_(w.permute(1, 2, 3, 0))
+def _pack_conv(w, dtype=None, flip=False):      # [O, I, kh, kw] -> [O][kh][kw][I], cast to dtype in the same pass
+    return _pack(w, 0, dtype, flip)
+
+
+def _pack_convT(w, dtype=None, flip=False):     # [I, O, kh, kw] -> [O][kh][kw][I]
+    return _pack(w, 1, dtype, flip)
 
 
 def _halo_ok(x, kh, kw, stride, pad, out_hw):
@@ -238,7 +254,7 @@ class _ConvT2d(torch.autograd.Function):
         oh, ow = out_hw
         if _halo_ok(x, kh, kw, stride, pad, out_hw):
             # stride-1 transposed conv == correlation with the spatially flipped, transposed kernel
-            y = conv3x3_fused(x, _pack_convT(w.flip([2, 3])), o)[0]
+            y = conv3x3_fused(x, _pack_convT(w, flip=True), o)[0]
         else:
             y = _conv_raw(x, _pack_convT(w), o, oh, ow, kh, kw, stride, pad, True)
         ctx.save_for_backward(x, w)

@@ -125,7 +125,7 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
     want_ds = need[1] and styles is not None
     if need[0] or want_ds:
         if _halo(dc, kh, kw, stride, pad):
-            wT = _cg._pack_convT(weight.flip([2, 3]), dt)
+            wT = _cg._pack_convT(weight, dt, flip=True)
             if want_ds:
                 dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
             else:

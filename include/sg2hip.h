@@ -218,6 +218,14 @@ int sg2_demod_fwd(float* d, float* wsq, const float* s, const float* w, int N, i
 int sg2_demod_bwd(float* gs, float* gw, const float* dd, const float* d, const float* s, const float* w,
                   const float* wsq, int N, int O, int I, int KK, void* stream);
 
+/* Convolution weight pack (replaces the strided-permute copies that feed every conv launch,
+ * conv2d_gradfix.py _pack_conv / _pack_convT; the reference feeds cuDNN the [O,I,kh,kw] weight
+ * directly, networks_stylegan2.py:70/176):  out[a][k][b] = in[a*sa + b*sb + k'*sk], k' = K-1-k when
+ * flip != 0, else k.  Strides in elements; in/out dtypes SG2_F32/F16/BF16 (cast in the same pass); K <= 9.
+ * [O,I,kh,kw] -> [O][kh][kw][I]: A=O, B=I, K=kh*kw, sa=I*K, sb=K, sk=1. */
+int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_dtype, int A, int B, int K, int64_t sa,
+                    int64_t sb, int64_t sk, int flip, void* stream);
+
 /* Adam step on a flat float32 parameter vector (torch.optim.Adam semantics, no weight decay,
  * amsgrad off) with the reference's gradient sanitation fused in front:
  *   g = nan_to_num(g * grad_scale, nan=0, posinf=1e5, neginf=-1e5)  (training_loop_mi_multimodal.py:346-347)

@@ -839,3 +839,23 @@ def test_dot_hw(dtype):
     h1, = torch.autograd.grad((ga1.float() ** 2).sum(), [b1])
     h2, = torch.autograd.grad((ga2.float() ** 2).sum(), [b2])
     assert rel_err(h1.float(), h2.double().cpu()) < 1e-2
+
+
+@pytest.mark.parametrize('src,dst', [(torch.float32, torch.float32), (torch.float32, torch.float16),
+                                     (torch.float32, torch.bfloat16), (torch.float16, torch.float16)])
+@pytest.mark.parametrize('o,i,k', [(512, 512, 3), (64, 1, 1), (3, 70, 3), (45, 33, 1), (96, 40, 3)])
+def test_pack_weight(src, dst, o, i, k):
+    """sg2_pack_weight (conv2d_gradfix._pack_conv / _pack_convT, flipped taps, transposed views, ragged
+    tiles) vs the torch permute-copy it replaces: bit-exact (a layout move plus one rounding)."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(7)
+    w = torch.randn(o, i, k, k, device=DEV).to(src)
+    cases = [(cg._pack_conv(w, dst), w.permute(0, 2, 3, 1)),
+             (cg._pack_convT(w, dst), w.permute(1, 2, 3, 0)),
+             (cg._pack_convT(w, dst, flip=True), w.flip([2, 3]).permute(1, 2, 3, 0)),
+             (cg._pack_conv(w, dst, flip=True), w.flip([2, 3]).permute(0, 2, 3, 1)),
+             (cg._pack_conv(w.transpose(0, 1), dst), w.transpose(0, 1).permute(0, 2, 3, 1))]
+    for got, ref in cases:
+        ref = ref.to(dst).contiguous()
+        assert got.shape == ref.shape and got.dtype == dst and got.is_contiguous()
+        assert torch.equal(got, ref)
