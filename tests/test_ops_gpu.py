@@ -843,7 +843,7 @@ def test_dot_hw(dtype):
 
 @pytest.mark.parametrize('src,dst', [(torch.float32, torch.float32), (torch.float32, torch.float16),
                                      (torch.float32, torch.bfloat16), (torch.float16, torch.float16)])
-@pytest.mark.parametrize('o,i,k', [(512, 512, 3), (64, 1, 1), (3, 70, 3), (45, 33, 1), (96, 40, 3)])
+@pytest.mark.parametrize('o,i,k', [(512, 512, 3), (64, 1, 1), (3, 70, 3), (45, 33, 1), (96, 40, 3), (20, 37, 2)])
 def test_pack_weight(src, dst, o, i, k):
     """sg2_pack_weight (conv2d_gradfix._pack_conv / _pack_convT, flipped taps, transposed views, ragged
     tiles) vs the torch permute-copy it replaces: bit-exact (a layout move plus one rounding)."""
