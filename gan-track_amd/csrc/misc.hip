@@ -163,6 +163,60 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(Tout* __restrict__ out
     out[e] = from_f32<Tout>(to_f32(in[(int64_t)a * sa + (int64_t)b * sb + kk * sk]));
 }
 
+// Row-wise infinity-norm pre-normalisation of the fp16 modulated layers (networks_stylegan2.py:52-54):
+// n = max_i |t[r,i]|; mode 0: y = t * ((1/n) * c) (the weight: torch's scalar / tensor is a reciprocal and a
+// scale), mode 1: y = t / n (the styles).  One workgroup per row, the row reread from L2 for the store.
+__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const float o = __shfl_xor(v, off);
+        v = is_max ? fmaxf(v, o) : v + o;
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return is_max ? fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])) : (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void infnorm_fwd_kernel(float* __restrict__ y, float* __restrict__ nrm,
+                                                          const float* __restrict__ t, int L, float c, int mode) {
+    __shared__ float red[4];
+    const float* tr = t + (int64_t)blockIdx.x * L;
+    float m = 0.f;
+    for (int i = threadIdx.x; i < L; i += 256) m = fmaxf(m, fabsf(tr[i]));
+    m = block_reduce(m, red, true);
+    if (threadIdx.x == 0) nrm[blockIdx.x] = m;
+    float* yr = y + (int64_t)blockIdx.x * L;
+    const float k = (1.0f / m) * c;
+    for (int i = threadIdx.x; i < L; i += 256) yr[i] = mode == 0 ? tr[i] * k : tr[i] / m;
+}
+
+// First-order gradient: dt = dy * k + [|t| == n] sgn(t) g_n / cnt, g_n = -(k / n) sum_i dy t, with k = c / n
+// (mode 0) or 1 / n (mode 1; the direct term as dy / n); cnt = the number of maxima (torch's
+// infinity-norm backward splits the gradient evenly between ties).
+__global__ __launch_bounds__(256) void infnorm_bwd_kernel(float* __restrict__ dt, const float* __restrict__ dy,
+                                                          const float* __restrict__ t, const float* __restrict__ nrm,
+                                                          int L, float c, int mode) {
+    __shared__ float red[4];
+    const int64_t base = (int64_t)blockIdx.x * L;
+    const float n = nrm[blockIdx.x];
+    float s1 = 0.f, cnt = 0.f;
+    for (int i = threadIdx.x; i < L; i += 256) {
+        const float tv = t[base + i];
+        s1 += dy[base + i] * tv;
+        cnt += fabsf(tv) == n ? 1.f : 0.f;
+    }
+    s1 = block_reduce(s1, red, false);
+    cnt = block_reduce(cnt, red, false);
+    const float k = mode == 0 ? (1.0f / n) * c : 1.0f / n;
+    const float gm = -(k / n) * s1 / cnt;
+    for (int i = threadIdx.x; i < L; i += 256) {
+        const float tv = t[base + i], g = dy[base + i];
+        float d = mode == 0 ? g * k : g / n;
+        if (fabsf(tv) == n) d += (tv > 0.f ? gm : (tv < 0.f ? -gm : 0.f));
+        dt[base + i] = d;
+    }
+}
+
 }  // namespace
 }  // namespace sg2
 
@@ -239,4 +293,22 @@ extern "C" int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_
     SG2_DISPATCH(in_dtype, Tin, SG2_DISPATCH(out_dtype, Tout,
         pack_weight_kernel<Tin, Tout><<<grid, 256, 0, s>>>((Tout*)out, (const Tin*)in, A, B, K, sa, sb, sk, flip)));
     return launch_status("sg2_pack_weight");
+}
+
+extern "C" int sg2_infnorm_fwd(float* y, float* nrm, const float* t, int rows, int L, float c, int mode,
+                               void* stream) {
+    using namespace sg2;
+    SG2_CHECK(y && nrm && t, "sg2_infnorm_fwd: null pointer");
+    SG2_CHECK(rows > 0 && L > 0 && (mode == 0 || mode == 1), "sg2_infnorm_fwd: bad arguments");
+    infnorm_fwd_kernel<<<rows, 256, 0, as_stream(stream)>>>(y, nrm, t, L, c, mode);
+    return launch_status("sg2_infnorm_fwd");
+}
+
+extern "C" int sg2_infnorm_bwd(float* dt, const float* dy, const float* t, const float* nrm, int rows, int L, float c,
+                               int mode, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(dt && dy && t && nrm, "sg2_infnorm_bwd: null pointer");
+    SG2_CHECK(rows > 0 && L > 0 && (mode == 0 || mode == 1), "sg2_infnorm_bwd: bad arguments");
+    infnorm_bwd_kernel<<<rows, 256, 0, as_stream(stream)>>>(dt, dy, t, nrm, L, c, mode);
+    return launch_status("sg2_infnorm_bwd");
 }

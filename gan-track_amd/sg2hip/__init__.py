@@ -59,6 +59,8 @@ SIGNATURES = {
     'sg2_demod_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
     'sg2_adam_step': [_vp, _vp, _vp, _vp, _i64, _f, _f, _f, _f, _f, _i64, _vp],
     'sg2_lerp': [_vp, _vp, _i64, _f, _vp],
+    'sg2_infnorm_fwd': [_vp, _vp, _vp, _i, _i, _f, _i, _vp],
+    'sg2_infnorm_bwd': [_vp, _vp, _vp, _vp, _i, _i, _f, _i, _vp],
     'sg2_pack_weight': [_vp, _i, _vp, _i, _i, _i, _i, _i64, _i64, _i64, _i, _vp],
 }
 ABI_VERSION = 1

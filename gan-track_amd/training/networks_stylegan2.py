@@ -34,6 +34,53 @@ def normalize_2nd_moment(x, dim=1, eps=1e-8):
     return x * (x.square().mean(dim=dim, keepdim=True) + eps).rsqrt()
 
 
+class _InfNorm(torch.autograd.Function):
+    """fp16 range pre-normalisation (:52-54), row-wise over t [rows, L]: mode 0 is the weight,
+    t * (c / max|t|) with c = 1/sqrt(fan_in); mode 1 the styles, t / max|t|.  One kernel forward
+    (sg2_infnorm_fwd) and one first-order backward (sg2_infnorm_bwd) in place of the ~20 launches of the
+    composed norm / reciprocal / scale / multiply and their autograd.  Under create_graph (the path-length
+    pass) the backward re-derives the reference expression with autograd so that second-order terms exist."""
+
+    @staticmethod
+    def forward(ctx, t_in, c, mode):
+        t = t_in.contiguous()
+        rows, L = t.shape
+        y = torch.empty_like(t)
+        nrm = torch.empty([rows], dtype=torch.float32, device=t.device)
+        _hip.check(_hip.lib().sg2_infnorm_fwd(_hip.ptr(y), _hip.ptr(nrm), _hip.ptr(t), rows, L, float(c), mode,
+                                              _hip.stream_ptr(t.device)), 'sg2_infnorm_fwd')
+        ctx.save_for_backward(t_in, nrm)    # the input itself: the create_graph backward differentiates it
+        ctx.c, ctx.mode = c, mode
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        t, nrm = ctx.saved_tensors
+        if not ctx.needs_input_grad[0]:
+            return None, None, None
+        if torch.is_grad_enabled():
+            n = t.norm(float('inf'), dim=1, keepdim=True)
+            y = t * (ctx.c / n) if ctx.mode == 0 else t / n
+            dt, = torch.autograd.grad(y, t, dy, create_graph=True)
+            return dt, None, None
+        dy, t = dy.contiguous(), t.contiguous()
+        dt = torch.empty_like(t)
+        _hip.check(_hip.lib().sg2_infnorm_bwd(_hip.ptr(dt), _hip.ptr(dy), _hip.ptr(t), _hip.ptr(nrm), t.shape[0],
+                                              t.shape[1], float(ctx.c), ctx.mode, _hip.stream_ptr(t.device)),
+                   'sg2_infnorm_bwd')
+        return dt, None, None
+
+
+def _prenorm(weight, styles):
+    """(:52-54) weight * (1/sqrt(I*k*k) / ||weight||_inf per output channel), styles / ||styles||_inf per sample."""
+    o, i, kh, kw = weight.shape
+    if weight.dtype != torch.float32 or styles.dtype != torch.float32:
+        return (weight * (1 / np.sqrt(i * kh * kw) / weight.norm(float('inf'), dim=[1, 2, 3], keepdim=True)),
+                styles / styles.norm(float('inf'), dim=1, keepdim=True))
+    w = _InfNorm.apply(weight.reshape(o, -1), float(np.float32(1 / np.sqrt(i * kh * kw))), 0).reshape(o, i, kh, kw)
+    return w, _InfNorm.apply(styles, 1.0, 1)
+
+
 class _Demod(torch.autograd.Function):
     """d[n,o] = rsqrt(sum_i s[n,i]^2 sum_k w[o,i,k]^2 + 1e-8) in one kernel (sg2_demod_fwd) where autograd
     of the reference's expression (:59-63) runs six elementwise / reduction / GEMM launches, and the
@@ -88,8 +135,7 @@ def modulated_conv2d(x, weight, styles, noise=None, up=1, down=1, padding=0, res
     misc.assert_shape(x, [n, in_ch, None, None])
     misc.assert_shape(styles, [n, in_ch])
     if x.dtype == torch.float16 and demodulate:   # keep fp16 in range (:52-54)
-        weight = weight * (1 / np.sqrt(in_ch * kh * kw) / weight.norm(float('inf'), dim=[1, 2, 3], keepdim=True))
-        styles = styles / styles.norm(float('inf'), dim=1, keepdim=True)
+        weight, styles = _prenorm(weight, styles)
     dcoefs = _demod(weight, styles) if demodulate else None
     x = x * styles.to(x.dtype).reshape(n, -1, 1, 1)
     x = conv2d_resample.conv2d_resample(x=x, w=weight.to(x.dtype), f=resample_filter, up=up, down=down,
@@ -308,9 +354,7 @@ class SynthesisLayer(torch.nn.Module):
             # one-kernel modulated conv + demod + noise + bias + lrelu + clamp (sg2_conv3x3 / sg2_conv2d_fused)
             weight = self.weight
             if x.dtype == torch.float16:   # fp16 range pre-normalisation (:52-54)
-                weight = weight * (1 / np.sqrt(self.in_channels * 9) / weight.norm(float('inf'), dim=[1, 2, 3],
-                                                                                   keepdim=True))
-                styles = styles / styles.norm(float('inf'), dim=1, keepdim=True)
+                weight, styles = _prenorm(weight, styles)
             if noise is not None and noise.ndim == 2:
                 noise = noise.reshape(1, 1, *noise.shape).expand(x.shape[0], 1, -1, -1)
             clamp = self.conv_clamp * gain if self.conv_clamp is not None else None

@@ -226,6 +226,16 @@ int sg2_demod_bwd(float* gs, float* gw, const float* dd, const float* d, const f
 int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_dtype, int A, int B, int K, int64_t sa,
                     int64_t sb, int64_t sk, int flip, void* stream);
 
+/* fp16 range pre-normalisation, row-wise (SG3/training/networks_stylegan2.py:52-54): t [rows, L] f32,
+ * n[r] = max_i |t[r,i]| (written to nrm [rows]); mode 0: y = t * ((1/n) * c)  (the weight, c = 1/sqrt(fan_in)),
+ * mode 1: y = t / n  (the styles). */
+int sg2_infnorm_fwd(float* y, float* nrm, const float* t, int rows, int L, float c, int mode, void* stream);
+
+/* First-order gradient of sg2_infnorm_fwd w.r.t. t (torch's infinity-norm backward: the norm's gradient split
+ * evenly between tied maxima). */
+int sg2_infnorm_bwd(float* dt, const float* dy, const float* t, const float* nrm, int rows, int L, float c, int mode,
+                    void* stream);
+
 /* Adam step on a flat float32 parameter vector (torch.optim.Adam semantics, no weight decay,
  * amsgrad off) with the reference's gradient sanitation fused in front:
  *   g = nan_to_num(g * grad_scale, nan=0, posinf=1e5, neginf=-1e5)  (training_loop_mi_multimodal.py:346-347)

@@ -859,3 +859,36 @@ def test_pack_weight(src, dst, o, i, k):
         ref = ref.to(dst).contiguous()
         assert got.shape == ref.shape and got.dtype == dst and got.is_contiguous()
         assert torch.equal(got, ref)
+
+
+def test_infnorm_prenorm():
+    """sg2_infnorm_fwd / _bwd (networks_stylegan2._prenorm, the fp16 pre-normalisation of :52-54) vs the
+    reference expression under torch autograd: forward bit-exact; first-order gradients (with tied and
+    negative maxima) and a create_graph second order to 1e-6."""
+    from training import networks_stylegan2 as net
+    torch.manual_seed(5)
+    w = torch.randn(48, 40, 3, 3, device=DEV)
+    w[3, 5, 1, 1] = w[3].abs().max() + 1.0          # a tie: two entries of equal magnitude, opposite sign
+    w[3, 7, 0, 2] = -w[3, 5, 1, 1]
+    w[9, 0, 0, 0] = -(w[9].abs().max() + 0.5)       # negative maximum
+    s = torch.randn(6, 40, device=DEV)
+    s[2, 4] = s[2, 11] = s[2].abs().max() + 0.25
+    gy_w, gy_s = torch.randn_like(w), torch.randn_like(s)
+
+    def ref(w_, s_):
+        return (w_ * (1 / np.sqrt(40 * 9) / w_.norm(float('inf'), dim=[1, 2, 3], keepdim=True)),
+                s_ / s_.norm(float('inf'), dim=1, keepdim=True))
+
+    out = []
+    for fn in (net._prenorm, ref):
+        wd, sd = w.clone().requires_grad_(True), s.clone().requires_grad_(True)
+        yw, ys = fn(wd, sd)
+        gw, gs = torch.autograd.grad((yw * gy_w).sum() + (ys * gy_s).sum(), [wd, sd])
+        wd2, sd2 = w.clone().requires_grad_(True), s.clone().requires_grad_(True)
+        yw2, ys2 = fn(wd2, sd2)
+        g1w, g1s = torch.autograd.grad((yw2 * gy_w).sum() + (ys2 * gy_s).sum(), [wd2, sd2], create_graph=True)
+        g2w, g2s = torch.autograd.grad((g1w * gy_w).sum() + (g1s * gy_s).sum() + (yw2.square()).sum(), [wd2, sd2])
+        out.append([yw.detach(), ys.detach(), gw, gs, g1w.detach(), g1s.detach(), g2w, g2s])
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    for a, b in zip(out[0][2:], out[1][2:]):
+        assert rel_err(a.double().cpu(), b.double().cpu()) < 1e-6
