@@ -103,6 +103,68 @@ class FusedConv(torch.autograd.Function):
         return g + (dres, None, None, None, None, None, None)
 
 
+def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, pad):
+    """Gradients of c = conv(x * s, W) given dc: dx = convT(dc, W) * s and ds = sum_hw convT(dc, W) * x in
+    one dgrad launch (out_scale / dot_src epilogue), dw = the s-scaled weight gradient."""
+    n, cin, h, w = x.shape
+    cout, _, kh, kw = weight.shape
+    dt = x.dtype
+    dx = ds = dw = None
+    s32 = _f32(styles)
+    want_ds = need_s and styles is not None
+    if need_x or want_ds:
+        if _halo(dc, kh, kw, stride, pad):
+            wT = _cg._pack_convT(weight, dt, flip=True)
+            if want_ds:
+                dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
+            else:
+                dx, _ = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32)
+        else:
+            if want_ds:
+                dx, _, ds = _cg.conv_fused(dc, _cg._pack_convT(weight, dt), cin, h, w, kh, kw, stride, (pad, pad),
+                                           transpose=True, out_scale=s32, dot_src=x)
+            else:
+                dx, _ = _cg.conv_fused(dc, _cg._pack_convT(weight, dt), cin, h, w, kh, kw, stride, (pad, pad),
+                                       transpose=True, out_scale=s32)
+        ds = ds.to(styles.dtype) if want_ds else None
+        dx = dx if need_x else None
+    if need_w and not _cg.weight_gradients_disabled:
+        dw = _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32).to(weight.dtype)
+    return dx, ds, dw
+
+
+class _SavedRaw(torch.autograd.Function):
+    """c = conv(x * s, W), the layer's raw (pre-demodulation) conv output, as a differentiable value for the
+    create_graph backward (dL/dd = sum_hw dz * c).  The forward hands back the c the fused forward kernel
+    already wrote (aux) instead of recomputing the modulated conv; the backward is the first-order
+    _scaled_input_grads (the reference differentiates the recomputed grouped conv, networks_stylegan2.py:80-89).
+    A third order falls back to differentiating a recomputed conv."""
+
+    @staticmethod
+    def forward(ctx, x, styles, weight, c, stride, pad):
+        ctx.save_for_backward(x, styles, weight)
+        ctx.cfg = (stride, pad)
+        return c.view_as(c)
+
+    @staticmethod
+    def backward(ctx, dc):
+        x, styles, weight = ctx.saved_tensors
+        stride, pad = ctx.cfg
+        need = ctx.needs_input_grad
+        if torch.is_grad_enabled():
+            dt = x.dtype
+            n = x.shape[0]
+            oh, ow = dc.shape[2], dc.shape[3]
+            ins = [t for t, nd in zip((x, styles, weight), need[:3]) if nd]
+            cc = _cg._Conv2d.apply(_mul(x, styles.to(dt).reshape(n, -1, 1, 1)), weight.to(dt), stride, (pad, pad),
+                                   (oh, ow))
+            gs = iter(torch.autograd.grad(cc, ins, dc, create_graph=True, allow_unused=True))
+            return tuple(next(gs) if nd else None for nd in need[:3]) + (None, None, None)
+        dx, ds, dw = _scaled_input_grads(_cg._nhwc(dc.to(x.dtype)), x, styles,
+                                         weight, need[0], need[1], need[2], stride, pad)
+        return dx, ds, dw, None, None, None
+
+
 def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain, clamp):
     """First order in three kernels: sg2_layer_bwd; dgrad with the *s scale (+ ds); scaled wgrad."""
     n, cin, h, w = x.shape
@@ -120,27 +182,7 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
         dd = (dz * c).sum([2, 3], dtype=torch.float32) if want_dd else None
         dn = dz.sum(1, keepdim=True, dtype=torch.float32) if want_dn else None
         dc = _cg._nhwc(dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None else dz)
-    dx = ds = dw = None
-    s32 = _f32(styles)
-    want_ds = need[1] and styles is not None
-    if need[0] or want_ds:
-        if _halo(dc, kh, kw, stride, pad):
-            wT = _cg._pack_convT(weight, dt, flip=True)
-            if want_ds:
-                dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
-            else:
-                dx, _ = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32)
-        else:
-            if want_ds:
-                dx, _, ds = _cg.conv_fused(dc, _cg._pack_convT(weight, dt), cin, h, w, kh, kw, stride, (pad, pad),
-                                           transpose=True, out_scale=s32, dot_src=x)
-            else:
-                dx, _ = _cg.conv_fused(dc, _cg._pack_convT(weight, dt), cin, h, w, kh, kw, stride, (pad, pad),
-                                       transpose=True, out_scale=s32)
-        ds = ds.to(styles.dtype) if want_ds else None
-        dx = dx if need[0] else None
-    if need[2] and not _cg.weight_gradients_disabled:
-        dw = _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32).to(weight.dtype)
+    dx, ds, dw = _scaled_input_grads(dc, x, styles, weight, need[0], need[1], need[2], stride, pad)
     db = db.to(bias.dtype) if db is not None else None
     dd = dd.to(dcoefs.dtype) if dd is not None else None
     dn = dn.to(noise.dtype) if dn is not None else None
@@ -166,7 +208,9 @@ def _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c
         dnoise = dz.sum(1, keepdim=True, dtype=torch.float32).to(noise.dtype)
     s_ = styles.to(dt).reshape(n, -1, 1, 1) if styles is not None else None
     if need[3] and dcoefs is not None:
-        if torch.is_grad_enabled():
+        if torch.is_grad_enabled() and c is not None and styles is not None:
+            c_ = _SavedRaw.apply(x, styles, weight, c, stride, pad)
+        elif torch.is_grad_enabled():
             c_ = _cg._Conv2d.apply(_mul(x, s_), weight.to(dt), stride, (pad, pad), (oh, ow))
         else:
             c_ = c
