@@ -133,6 +133,56 @@ def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, p
     return dx, ds, dw
 
 
+class _ScaledConvT(torch.autograd.Function):
+    """dxs = convT(dz * d, W), the create_graph backward's dgrad with the demodulation scale d [N, Cout] on
+    the operand staging (no dz * d pass in HBM).  Backward: one conv launch gives d(dz) = conv(G, W) * d
+    (out_scale) and dd = sum_p conv(G, W) * dz (dot_src); dW is the d-scaled weight gradient.  A third
+    order falls back to differentiating the composed form."""
+
+    @staticmethod
+    def forward(ctx, dz, d, weight, stride, pad, out_hw):
+        dz = _cg._nhwc(dz)
+        cin, kh, kw = weight.shape[1], weight.shape[2], weight.shape[3]
+        dt = dz.dtype
+        if _halo(dz, kh, kw, stride, pad):
+            y, _ = _cg.conv3x3_fused(dz, _cg._pack_convT(weight, dt, flip=True), cin, in_scale=_f32(d))
+        else:
+            y, _ = _cg.conv_fused(dz, _cg._pack_convT(weight, dt), cin, out_hw[0], out_hw[1], kh, kw, stride,
+                                  (pad, pad), transpose=True, in_scale=_f32(d))
+        ctx.save_for_backward(dz, d, weight)
+        ctx.cfg = (stride, pad, tuple(out_hw))
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        dz, d, weight = ctx.saved_tensors
+        stride, pad, out_hw = ctx.cfg
+        need = ctx.needs_input_grad
+        dt = dz.dtype
+        n, cout, oh, ow = dz.shape
+        kh, kw = weight.shape[2], weight.shape[3]
+        if torch.is_grad_enabled():
+            ins = [t for t, nd in zip((dz, d, weight), need[:3]) if nd]
+            y = _cg._ConvT2d.apply(dz * d.to(dt).reshape(n, -1, 1, 1), weight.to(dt), stride, (pad, pad), out_hw)
+            gs = iter(torch.autograd.grad(y, ins, g, create_graph=True, allow_unused=True))
+            return tuple(next(gs) if nd else None for nd in need[:3]) + (None, None, None)
+        g = _cg._nhwc(g.to(dt))
+        d32 = _f32(d)
+        gdz = gd = gw = None
+        if need[0] or need[1]:
+            src = dz if need[1] else None
+            if _halo(g, kh, kw, stride, pad):
+                res = _cg.conv3x3_fused(g, _cg._pack_conv(weight, dt), cout, out_scale=d32, dot_src=src)
+            else:
+                res = _cg.conv_fused(g, _cg._pack_conv(weight, dt), cout, oh, ow, kh, kw, stride, (pad, pad),
+                                     out_scale=d32, dot_src=src)
+            gdz = res[0] if need[0] else None
+            gd = res[2].to(d.dtype) if need[1] else None
+        if need[2] and not _cg.weight_gradients_disabled:
+            gw = _cg._wgrad_raw(dz, g, kh, kw, stride, (pad, pad), g_scale=d32).to(weight.dtype)
+        return gdz, gd, gw, None, None, None
+
+
 class _SavedRaw(torch.autograd.Function):
     """c = conv(x * s, W), the layer's raw (pre-demodulation) conv output, as a differentiable value for the
     create_graph backward (dL/dd = sum_hw dz * c).  The forward hands back the c the fused forward kernel
@@ -215,9 +265,14 @@ def _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c
         else:
             c_ = c
         dd = _cg.dot_hw(dz, c_).to(dcoefs.dtype)
-    dc = dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None else dz
+    want_dw = need[2] and not _cg.weight_gradients_disabled
+    scaled_t = dcoefs is not None and not want_dw       # the PL pass: dc feeds the dgrad only
+    dc = dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None and not scaled_t else dz
     if need[0] or need[1]:
-        dxs = _cg._ConvT2d.apply(dc, weight.to(dt), stride, (pad, pad), (h, w))
+        if scaled_t:
+            dxs = _ScaledConvT.apply(dz, dcoefs, weight, stride, pad, (h, w))
+        else:
+            dxs = _cg._ConvT2d.apply(dc, weight.to(dt), stride, (pad, pad), (h, w))
         if need[0]:
             dx = _mul(dxs, s_)
         if need[1] and styles is not None:
