@@ -1,37 +1,10 @@
-// Small kernels of the training step: demodulation coefficients, fused gradient sanitation + Adam,
-// and the G_ema lerp.  All HBM-bound, grid-stride, 16-byte vectorised where the data allow.
+// Small kernels of the training step: demodulation coefficients and their gradient, conv weight packs,
+// fp16 range pre-normalisation, and the optimiser step (multi-tensor Adam with the gradient sanitation
+// fused in front, the G_ema lerp).  All HBM- or latency-bound.
 #include "sg2_common.h"
 
 namespace sg2 {
 namespace {
-
-// d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps);  wsq[o,i] = sum_k w[o,i,k]^2.
-// One workgroup per (o, block of samples): the 256 lanes reduce over i.
-__global__ __launch_bounds__(256) void demod_kernel(float* d, const float* s, const float* w, int N, int O, int I,
-                                                    int KK, float eps) {
-    __shared__ float wsq[1024];
-    __shared__ float red[4];
-    const int o = blockIdx.x;
-    for (int i = threadIdx.x; i < I; i += 256) {
-        const float* wr = w + ((int64_t)o * I + i) * KK;
-        float acc = 0.f;
-        for (int k = 0; k < KK; ++k) acc += wr[k] * wr[k];
-        wsq[i] = acc;
-    }
-    __syncthreads();
-    for (int n = blockIdx.y; n < N; n += gridDim.y) {
-        float acc = 0.f;
-        for (int i = threadIdx.x; i < I; i += 256) {
-            const float v = s[(int64_t)n * I + i];
-            acc += v * v * wsq[i];
-        }
-        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-        __syncthreads();
-        if (threadIdx.x == 0) d[(int64_t)n * O + o] = rsqrtf(red[0] + red[1] + red[2] + red[3] + eps);
-        __syncthreads();
-    }
-}
 
 // Demodulation with the per-(o, i) weight energy kept for the backward: wsq[o,i] = sum_k w^2 (written when
 // wsq_out != null), d[n,o] = rsqrt(sum_i s[n,i]^2 wsq[o,i] + eps).  One workgroup per o; after wsq is in
@@ -122,27 +95,60 @@ __global__ __launch_bounds__(256) void demod_bwd_s_kernel(float* gs, const float
                                                                  part[2][threadIdx.x] + part[3][threadIdx.x]);
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
-                                                   const float* __restrict__ g, int64_t n, float lr, float b1, float b2,
-                                                   float eps, float gscale, float bc1, float bc2_sqrt) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        float gi = g[i] * gscale;
-        if (gi != gi) gi = 0.f;
-        gi = fminf(fmaxf(gi, -1e5f), 1e5f);
-        const float mi = m[i] * b1 + (1.f - b1) * gi;
-        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
-        m[i] = mi;
-        v[i] = vi;
+// Multi-tensor kernels of the optimiser step.  A launch walks a block table: entry = (segment << 40) | start,
+// one workgroup per SEG_CHUNK elements of one segment (a parameter tensor), so a whole module's ~100
+// tensors of very different sizes are one launch with no idle lanes beyond each tensor's last chunk.
+constexpr int SEG_CHUNK = 4096;     // 256 lanes x 16 elements
+
+// torch.optim.Adam (foreach arithmetic, no weight decay, amsgrad off) on every parameter of one exchanged
+// gradient, with the reference's sanitation in front (training_loop_mi_multimodal.py:345-347):
+//   g = nan_to_num(grad * gscale, nan=0, posinf=1e5, neginf=-1e5)
+//   m = lerp(m, g, 1 - b1); v = v * b2 + (1 - b2) * g * g
+//   p += -step_size * (m / (sqrt(v) / bc2_sqrt + eps))
+// seg[s] = {param address, offset of the segment in grad/m/v, numel}; coef[s] = {step_size, bc2_sqrt}.
+// write_grad: store the sanitised g back (the caller's .grad views then hold the exchanged gradient).
+__global__ __launch_bounds__(256) void adam_multi_kernel(const int64_t* __restrict__ seg, const float* __restrict__ coef,
+                                                         const int64_t* __restrict__ blocks, float* __restrict__ grad,
+                                                         float* __restrict__ m, float* __restrict__ v, float b1, float b2,
+                                                         float eps, float gscale, int write_grad) {
+    const int64_t e = blocks[blockIdx.x];
+    const int s = (int)(e >> 40);
+    const int64_t start = e & ((1LL << 40) - 1);
+    float* __restrict__ p = reinterpret_cast<float*>(seg[3 * s]);
+    const int64_t off = seg[3 * s + 1], n = seg[3 * s + 2];
+    const float step_size = coef[2 * s], bc2_sqrt = coef[2 * s + 1];
+    const float w = 1.f - b1;
+    const int64_t end = start + SEG_CHUNK < n ? start + SEG_CHUNK : n;
+    for (int64_t i = start + threadIdx.x; i < end; i += 256) {
+        float g = grad[off + i] * gscale;
+        if (g != g) g = 0.f;
+        else if (isinf(g)) g = g > 0.f ? 1e5f : -1e5f;
+        if (write_grad) grad[off + i] = g;
+        float mi = m[off + i];
+        mi = w < 0.5f ? mi + w * (g - mi) : g - (g - mi) * (1.f - w);      // torch lerp
+        float vi = v[off + i] * b2;
+        vi = vi + (1.f - b2) * g * g;                                      // addcmul
+        m[off + i] = mi;
+        v[off + i] = vi;
         const float denom = sqrtf(vi) / bc2_sqrt + eps;
-        p[i] -= (lr / bc1) * mi / denom;
+        p[i] = p[i] + (-step_size) * (mi / denom);                         // addcdiv
     }
 }
 
-__global__ __launch_bounds__(256) void lerp_kernel(float* __restrict__ dst, const float* __restrict__ src, int64_t n,
-                                                   float beta) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float a = src[i];
-        dst[i] = a + beta * (dst[i] - a);
+// G_ema update (training_loop_mi_multimodal.py:363-364): dst = src.lerp(dst, beta), torch's lerp formula.
+// seg[s] = {dst address, src address, numel}.
+__global__ __launch_bounds__(256) void lerp_multi_kernel(const int64_t* __restrict__ seg,
+                                                         const int64_t* __restrict__ blocks, float beta) {
+    const int64_t e = blocks[blockIdx.x];
+    const int s = (int)(e >> 40);
+    const int64_t start = e & ((1LL << 40) - 1);
+    float* __restrict__ dst = reinterpret_cast<float*>(seg[3 * s]);
+    const float* __restrict__ src = reinterpret_cast<const float*>(seg[3 * s + 1]);
+    const int64_t n = seg[3 * s + 2];
+    const int64_t end = start + SEG_CHUNK < n ? start + SEG_CHUNK : n;
+    for (int64_t i = start + threadIdx.x; i < end; i += 256) {
+        const float a = src[i], b = dst[i];
+        dst[i] = beta < 0.5f ? a + beta * (b - a) : b - (b - a) * (1.f - beta);
     }
 }
 
@@ -220,16 +226,6 @@ __global__ __launch_bounds__(256) void infnorm_bwd_kernel(float* __restrict__ dt
 }  // namespace
 }  // namespace sg2
 
-extern "C" int sg2_demod_coefs(float* d, const float* s, const float* w, int N, int O, int I, int KK, float eps,
-                               void* stream) {
-    using namespace sg2;
-    SG2_CHECK(d && s && w, "sg2_demod_coefs: null pointer");
-    SG2_CHECK(I <= 1024 && I > 0 && O > 0 && N > 0 && KK > 0, "sg2_demod_coefs: unsupported shape");
-    dim3 grid(O, std::min(N, 64));
-    demod_kernel<<<grid, 256, 0, as_stream(stream)>>>(d, s, w, N, O, I, KK, eps);
-    return launch_status("sg2_demod_coefs");
-}
-
 extern "C" int sg2_demod_fwd(float* d, float* wsq, const float* s, const float* w, int N, int O, int I, int KK,
                              float eps, void* stream) {
     using namespace sg2;
@@ -259,27 +255,25 @@ extern "C" int sg2_demod_bwd(float* gs, float* gw, const float* dd, const float*
     return 0;
 }
 
-extern "C" int sg2_adam_step(float* param, float* exp_avg, float* exp_avg_sq, const float* grad, int64_t n, float lr,
-                             float beta1, float beta2, float eps, float grad_scale, int64_t step, void* stream) {
+extern "C" int sg2_adam_multi(const int64_t* seg, const float* coef, const int64_t* blocks, int nblocks,
+                              float* grad, float* exp_avg, float* exp_avg_sq, float beta1, float beta2, float eps,
+                              float grad_scale, int write_grad, void* stream) {
     using namespace sg2;
-    SG2_CHECK(param && exp_avg && exp_avg_sq && grad, "sg2_adam_step: null pointer");
-    SG2_CHECK(step >= 1, "sg2_adam_step: step must be >= 1");
-    if (n == 0) return 0;
-    const float bc1 = 1.f - powf(beta1, (float)step);
-    const float bc2 = 1.f - powf(beta2, (float)step);
-    const int g = (int)std::min<int64_t>(cdiv(n, 256), 8192);
-    adam_kernel<<<g, 256, 0, as_stream(stream)>>>(param, exp_avg, exp_avg_sq, grad, n, lr, beta1, beta2, eps,
-                                                 grad_scale, bc1, sqrtf(bc2));
-    return launch_status("sg2_adam_step");
+    SG2_CHECK(seg && coef && blocks && grad && exp_avg && exp_avg_sq, "sg2_adam_multi: null pointer");
+    SG2_CHECK(nblocks >= 0, "sg2_adam_multi: nblocks < 0");
+    if (nblocks == 0) return 0;
+    adam_multi_kernel<<<nblocks, 256, 0, as_stream(stream)>>>(seg, coef, blocks, grad, exp_avg, exp_avg_sq, beta1,
+                                                               beta2, eps, grad_scale, write_grad);
+    return launch_status("sg2_adam_multi");
 }
 
-extern "C" int sg2_lerp(float* dst, const float* src, int64_t n, float beta, void* stream) {
+extern "C" int sg2_lerp_multi(const int64_t* seg, const int64_t* blocks, int nblocks, float beta, void* stream) {
     using namespace sg2;
-    SG2_CHECK(dst && src, "sg2_lerp: null pointer");
-    if (n == 0) return 0;
-    const int g = (int)std::min<int64_t>(cdiv(n, 256), 8192);
-    lerp_kernel<<<g, 256, 0, as_stream(stream)>>>(dst, src, n, beta);
-    return launch_status("sg2_lerp");
+    SG2_CHECK(seg && blocks, "sg2_lerp_multi: null pointer");
+    SG2_CHECK(nblocks >= 0, "sg2_lerp_multi: nblocks < 0");
+    if (nblocks == 0) return 0;
+    lerp_multi_kernel<<<nblocks, 256, 0, as_stream(stream)>>>(seg, blocks, beta);
+    return launch_status("sg2_lerp_multi");
 }
 
 extern "C" int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_dtype, int A, int B, int K,

@@ -54,16 +54,15 @@ SIGNATURES = {
     'sg2_affine_grid_sample_fwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
     'sg2_affine_grid_sample_bwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
     'sg2_reflect_pad_dyn': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp],
-    'sg2_demod_coefs': [_vp, _vp, _vp, _i, _i, _i, _i, _f, _vp],
     'sg2_demod_fwd': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp],
     'sg2_demod_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
-    'sg2_adam_step': [_vp, _vp, _vp, _vp, _i64, _f, _f, _f, _f, _f, _i64, _vp],
-    'sg2_lerp': [_vp, _vp, _i64, _f, _vp],
+    'sg2_adam_multi': [_vp, _vp, _vp, _i, _vp, _vp, _vp, _f, _f, _f, _f, _i, _vp],
+    'sg2_lerp_multi': [_vp, _vp, _i, _f, _vp],
     'sg2_infnorm_fwd': [_vp, _vp, _vp, _i, _i, _f, _i, _vp],
     'sg2_infnorm_bwd': [_vp, _vp, _vp, _vp, _i, _i, _f, _i, _vp],
     'sg2_pack_weight': [_vp, _i, _vp, _i, _i, _i, _i, _i64, _i64, _i64, _i, _vp],
 }
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib = None
 

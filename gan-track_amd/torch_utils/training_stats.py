@@ -1,8 +1,20 @@
-"""Cross-rank scalar statistics (the ADA heuristic reads 'Loss/signs/real' through it).
+"""Training statistics: per-name moments [count, sum, sum of squares] accumulated on the device and
+reduced across ranks on demand.
 
-Same API and semantics as SG3/torch_utils/training_stats.py: `report`/`report0` accumulate
-[count, sum, sum of squares] per name per device without host syncs (:55-99); `Collector.update`
-sums the deltas of all names in ONE all_reduce of a [num_names, 3] float64 tensor (:234-266)."""
+Public surface of SG3/torch_utils/training_stats.py (`init_multiprocessing` :34-51, `report` :55-99,
+`report0` :103-109, `Collector` :113-230): the ADA heuristic (training_loop_mi_multimodal.py:373-376)
+and the per-tick stats.jsonl (:461-469) read it.
+
+Design (this build's own):
+  * every statistic name owns one row of a per-device float64 table (`_Board`), rows in first-report
+    order; `report` adds the value's three moments into that row in place: no host sync and, once the
+    row exists, no allocation -- so reports inside a HIP-graph-captured phase replay correctly;
+  * `Collector.update` drains ALL device tables in one pass into one `[rows, 3]` tensor, all-reduces it
+    once across ranks, and folds it into a process-wide CPU cumulative table (numpy float64); each
+    collector remembers the cumulative totals it saw last and exposes the difference.
+As in the reference, every rank must report the same names in the same order (`report0` registers
+the name on every rank).
+"""
 import re
 
 import numpy as np
@@ -10,119 +22,136 @@ import torch
 
 import dnnlib
 
-_num_moments = 3
-_reduce_dtype = torch.float32
-_counter_dtype = torch.float64
-_rank = 0
-_sync_device = None
-_sync_called = False
-_counters = {}     # name -> device -> tensor[3]
-_cumulative = {}   # name -> cpu tensor[3]
+
+class _Board:
+    def __init__(self):
+        self.rows = {}               # name -> row index
+        self.tables = {}             # device -> float64 [capacity, 3]
+        self.capacity = 64
+        self.total = np.zeros([0, 3], np.float64)   # cumulative moments after the last drain
+        self.rank = 0
+        self.sync_device = None
+        self.synced = False
+
+    def row(self, name):
+        r = self.rows.get(name)
+        if r is None:
+            r = self.rows[name] = len(self.rows)
+            if r >= self.capacity:           # grow every table (never during a graph capture: rows are
+                self.capacity *= 2           # registered by the eager warm-up step)
+                for dev, t in self.tables.items():
+                    g = torch.zeros([self.capacity, 3], dtype=torch.float64, device=dev)
+                    g[:t.shape[0]].copy_(t)
+                    self.tables[dev] = g
+        return r
+
+    def table(self, device):
+        t = self.tables.get(device)
+        if t is None:
+            t = self.tables[device] = torch.zeros([self.capacity, 3], dtype=torch.float64, device=device)
+        return t
+
+    def drain(self):
+        """Move every device's pending moments into the cumulative table (one all_reduce over ranks)."""
+        n = len(self.rows)
+        if n == 0:
+            return self.total
+        self.synced = True
+        dev = self.sync_device if self.sync_device is not None else torch.device('cpu')
+        acc = torch.zeros([n, 3], dtype=torch.float64, device=dev)
+        for t in self.tables.values():
+            acc.add_(t[:n].to(dev))
+            t.zero_()
+        if self.sync_device is not None:
+            torch.distributed.all_reduce(acc)
+        if self.total.shape[0] < n:
+            self.total = np.concatenate([self.total, np.zeros([n - self.total.shape[0], 3])])
+        self.total[:n] += acc.cpu().numpy()
+        return self.total
+
+
+_board = _Board()
 
 
 def init_multiprocessing(rank, sync_device):
-    global _rank, _sync_device
-    assert not _sync_called
-    _rank = rank
-    _sync_device = sync_device
+    """Call after init_process_group and before the first Collector.update (reference :34-51)."""
+    assert not _board.synced, 'init_multiprocessing must precede the first Collector.update()'
+    _board.rank = rank
+    _board.sync_device = sync_device
 
 
 def report(name, value):
-    if name not in _counters:
-        _counters[name] = {}
-    elems = torch.as_tensor(value)
-    if elems.numel() == 0:
+    """Accumulate the moments of `value` (any scalar set) under `name`; returns `value` unchanged."""
+    r = _board.row(name)
+    v = torch.as_tensor(value)
+    if v.numel() == 0:
         return value
-    elems = elems.detach().flatten().to(_reduce_dtype)
-    moments = torch.stack([torch.ones_like(elems).sum(), elems.sum(), elems.square().sum()])
-    assert moments.ndim == 1 and moments.shape[0] == _num_moments
-    moments = moments.to(_counter_dtype)
-    dev = moments.device
-    if dev not in _counters[name]:
-        _counters[name][dev] = torch.zeros_like(moments)
-    _counters[name][dev].add_(moments)
+    v = v.detach().flatten().float()
+    moments = torch.stack([v.sum(), v.square().sum()]).double()
+    row = _board.table(v.device)[r]
+    row[1:].add_(moments)
+    row[:1].add_(float(v.numel()))
     return value
 
 
 def report0(name, value):
-    report(name, value if _rank == 0 else [])
+    """`report` on rank 0 only; the other ranks register the name with no scalars."""
+    report(name, value if _board.rank == 0 else [])
     return value
 
 
 class Collector:
+    """Means / standard deviations of the reported scalars between the last two `update()` calls, for
+    names matching `regex`.  With keep_previous, a name that received nothing keeps its last values."""
+
     def __init__(self, regex='.*', keep_previous=True):
         self._regex = re.compile(regex)
         self._keep_previous = keep_previous
-        self._cumulative = {}
-        self._moments = {}
+        self._seen = {}      # name -> cumulative moments at the last update
+        self._delta = {}     # name -> moments between the last two updates
         self.update()
-        self._moments.clear()
+        self._delta.clear()
 
     def names(self):
-        return [n for n in _counters if self._regex.fullmatch(n)]
+        return [n for n in _board.rows if self._regex.fullmatch(n)]
 
     def update(self):
         if not self._keep_previous:
-            self._moments.clear()
-        for name, cum in _sync(self.names()):
-            if name not in self._cumulative:
-                self._cumulative[name] = torch.zeros([_num_moments], dtype=_counter_dtype)
-            delta = cum - self._cumulative[name]
-            self._cumulative[name].copy_(cum)
-            if float(delta[0]) != 0:
-                self._moments[name] = delta
+            self._delta.clear()
+        names = self.names()
+        if not names:
+            return
+        total = _board.drain()
+        for n in names:
+            cur = total[_board.rows[n]].copy()
+            d = cur - self._seen.get(n, 0.0)
+            self._seen[n] = cur
+            if d[0] != 0:
+                self._delta[n] = d
 
-    def _get_delta(self, name):
+    def _moments(self, name):
         assert self._regex.fullmatch(name)
-        if name not in self._moments:
-            self._moments[name] = torch.zeros([_num_moments], dtype=_counter_dtype)
-        return self._moments[name]
+        return self._delta.get(name, np.zeros(3))
 
     def num(self, name):
-        return int(self._get_delta(name)[0])
+        return int(self._moments(name)[0])
 
     def mean(self, name):
-        d = self._get_delta(name)
-        return float('nan') if int(d[0]) == 0 else float(d[1] / d[0])
+        cnt, s, _ = self._moments(name)
+        return float('nan') if int(cnt) == 0 else float(s / cnt)
 
     def std(self, name):
-        d = self._get_delta(name)
-        if int(d[0]) == 0 or not np.isfinite(float(d[1])):
+        cnt, s, sq = self._moments(name)
+        if int(cnt) == 0 or not np.isfinite(s):
             return float('nan')
-        if int(d[0]) == 1:
+        if int(cnt) == 1:
             return 0.0
-        m = float(d[1] / d[0])
-        return float(np.sqrt(max(float(d[2] / d[0]) - m * m, 0)))
+        m = s / cnt
+        return float(np.sqrt(max(sq / cnt - m * m, 0.0)))
 
     def as_dict(self):
-        out = dnnlib.EasyDict()
-        for n in self.names():
-            out[n] = dnnlib.EasyDict(num=self.num(n), mean=self.mean(n), std=self.std(n))
-        return out
+        return dnnlib.EasyDict({n: dnnlib.EasyDict(num=self.num(n), mean=self.mean(n), std=self.std(n))
+                                for n in self.names()})
 
     def __getitem__(self, name):
         return self.mean(name)
-
-
-def _sync(names):
-    if len(names) == 0:
-        return []
-    global _sync_called
-    _sync_called = True
-    device = _sync_device if _sync_device is not None else torch.device('cpu')
-    deltas = []
-    for name in names:
-        d = torch.zeros([_num_moments], dtype=_counter_dtype, device=device)
-        for c in _counters[name].values():
-            d.add_(c.to(device))
-            c.zero_()
-        deltas.append(d)
-    deltas = torch.stack(deltas)
-    if _sync_device is not None:
-        torch.distributed.all_reduce(deltas)
-    deltas = deltas.cpu()
-    for i, name in enumerate(names):
-        if name not in _cumulative:
-            _cumulative[name] = torch.zeros([_num_moments], dtype=_counter_dtype)
-        _cumulative[name].add_(deltas[i])
-    return [(n, _cumulative[n]) for n in names]

@@ -69,77 +69,95 @@ class StyleGAN2Loss(Loss):
             img = self.augment_pipe(img, allow_aug_debug_print)
         return self.D(img, c, update_emas=update_emas)
 
+    # Which terms a phase evaluates (reference loss.py:64-139): G non-saturating loss, G path-length
+    # regulariser, D loss on generated images, D loss and/or R1 on real images.  A phase whose
+    # regulariser weight is zero degenerates as in the reference (:66-69).
+    _TERMS = {'Gmain': ('G',), 'Greg': ('Gpl',), 'Gboth': ('G', 'Gpl'),
+              'Dmain': ('Dfake', 'Dreal'), 'Dreg': ('Dr1',), 'Dboth': ('Dfake', 'Dreal', 'Dr1')}
+
     def accumulate_gradients(self, phase, real_img, real_c, gen_z, gen_c, gain, cur_nimg):
-        assert phase in ['Gmain', 'Greg', 'Gboth', 'Dmain', 'Dreg', 'Dboth']
+        assert phase in self._TERMS
+        terms = set(self._TERMS[phase])
         if self.pl_weight == 0:
-            phase = {'Greg': 'none', 'Gboth': 'Gmain'}.get(phase, phase)
+            terms.discard('Gpl')
         if self.r1_gamma == 0:
-            phase = {'Dreg': 'none', 'Dboth': 'Dmain'}.get(phase, phase)
-        blur_sigma = max(1 - cur_nimg / (self.blur_fade_kimg * 1e3), 0) * self.blur_init_sigma \
-            if self.blur_fade_kimg > 0 else 0
-        report = training_stats.report
+            terms.discard('Dr1')
+        sigma = 0
+        if self.blur_fade_kimg > 0:
+            sigma = self.blur_init_sigma * max(1 - cur_nimg / (self.blur_fade_kimg * 1e3), 0)
+        # The order below is the reference's: it fixes the RNG draw sequence and the stats order.
+        if 'G' in terms:
+            self._generator_term(gen_z, gen_c, gain, sigma)
+        if 'Gpl' in terms:
+            self._path_length_term(gen_z, gen_c, gain)
+        fake_loss = self._discriminator_fake_term(gen_z, gen_c, gain, sigma) if 'Dfake' in terms else 0
+        if 'Dreal' in terms or 'Dr1' in terms:
+            self._discriminator_real_term(real_img, real_c, gain, sigma, fake_loss,
+                                          main='Dreal' in terms, r1='Dr1' in terms)
 
-        if phase in ['Gmain', 'Gboth']:
-            with torch.autograd.profiler.record_function('Gmain_forward'):
-                gen_img, _ = self.run_G(gen_z, gen_c)
-                logits = self.run_D(gen_img, gen_c, blur_sigma=blur_sigma)
-                report('Loss/scores/fake', logits)
-                report('Loss/signs/fake', logits.sign())
-                loss_G = torch.nn.functional.softplus(-logits)
-                report('Loss/G/loss', loss_G)
-            with torch.autograd.profiler.record_function('Gmain_backward'):
-                loss_G.mean().mul(gain).backward()
+    def _report_logits(self, kind, logits):
+        training_stats.report(f'Loss/scores/{kind}', logits)
+        training_stats.report(f'Loss/signs/{kind}', logits.sign())
 
-        if phase in ['Greg', 'Gboth']:
-            with torch.autograd.profiler.record_function('Gpl_forward'):
-                bs = gen_z.shape[0] // self.pl_batch_shrink
-                gen_img, gen_ws = self.run_G(gen_z[:bs], gen_c[:bs])
-                pl_noise = torch.randn_like(gen_img) / np.sqrt(gen_img.shape[2] * gen_img.shape[3])
-                with torch.autograd.profiler.record_function('pl_grads'), \
-                        conv2d_gradfix.no_weight_gradients(self.pl_no_weight_grad):
-                    pl_grads = torch.autograd.grad(outputs=[(gen_img * pl_noise).sum()], inputs=[gen_ws],
-                                                   create_graph=True, only_inputs=True)[0]
-                pl_lengths = pl_grads.square().sum(2).mean(1).sqrt()
-                pl_mean = self.pl_mean.lerp(pl_lengths.mean(), self.pl_decay)
-                self.pl_mean.copy_(pl_mean.detach())
-                pl_penalty = (pl_lengths - pl_mean).square()
-                report('Loss/pl_penalty', pl_penalty)
-                loss_Gpl = pl_penalty * self.pl_weight
-                report('Loss/G/reg', loss_Gpl)
-            with torch.autograd.profiler.record_function('Gpl_backward'):
-                loss_Gpl.mean().mul(gain).backward()
+    def _generator_term(self, z, c, gain, sigma):
+        """-log sigmoid(D(G(z))) on a full batch (reference :73-82)."""
+        with torch.autograd.profiler.record_function('G_nonsat'):
+            img, _ = self.run_G(z, c)
+            logits = self.run_D(img, c, blur_sigma=sigma)
+            self._report_logits('fake', logits)
+            term = torch.nn.functional.softplus(-logits)
+            training_stats.report('Loss/G/loss', term)
+            term.mean().mul(gain).backward()
 
-        loss_Dgen = 0
-        if phase in ['Dmain', 'Dboth']:
-            with torch.autograd.profiler.record_function('Dgen_forward'):
-                gen_img, _ = self.run_G(gen_z, gen_c, update_emas=True)
-                logits = self.run_D(gen_img, gen_c, blur_sigma=blur_sigma, update_emas=True)
-                report('Loss/scores/fake', logits)
-                report('Loss/signs/fake', logits.sign())
-                loss_Dgen = torch.nn.functional.softplus(logits)
-            with torch.autograd.profiler.record_function('Dgen_backward'):
-                loss_Dgen.mean().mul(gain).backward()
+    def _path_length_term(self, z, c, gain):
+        """Path-length penalty pl_weight * (|J^T y| - a)^2 on 1/pl_batch_shrink of the batch, y ~ N(0, 1/HW)
+        per pixel, a the running mean of |J^T y| (reference :85-100).  J^T y is a create_graph VJP through
+        the synthesis network; inside no_weight_gradients the weight-gradient kernels are skipped."""
+        with torch.autograd.profiler.record_function('G_path_length'):
+            n = z.shape[0] // self.pl_batch_shrink
+            img, ws = self.run_G(z[:n], c[:n])
+            y = torch.randn_like(img) / np.sqrt(img.shape[2] * img.shape[3])
+            with conv2d_gradfix.no_weight_gradients(self.pl_no_weight_grad):
+                jty, = torch.autograd.grad(outputs=[(img * y).sum()], inputs=[ws], create_graph=True,
+                                           only_inputs=True)
+            lengths = jty.square().sum(2).mean(1).sqrt()
+            a = self.pl_mean.lerp(lengths.mean(), self.pl_decay)
+            self.pl_mean.copy_(a.detach())
+            penalty = (lengths - a).square()
+            training_stats.report('Loss/pl_penalty', penalty)
+            term = penalty * self.pl_weight
+            training_stats.report('Loss/G/reg', term)
+            term.mean().mul(gain).backward()
 
-        if phase in ['Dmain', 'Dreg', 'Dboth']:
-            name = 'Dreal' if phase == 'Dmain' else 'Dr1' if phase == 'Dreg' else 'Dreal_Dr1'
-            with torch.autograd.profiler.record_function(name + '_forward'):
-                real_tmp = real_img.detach().requires_grad_(phase in ['Dreg', 'Dboth'])
-                logits = self.run_D(real_tmp, real_c, blur_sigma=blur_sigma,
-                                    allow_aug_debug_print=self.allow_aug_debug_print)
-                report('Loss/scores/real', logits)
-                report('Loss/signs/real', logits.sign())
-                loss_Dreal = 0
-                if phase in ['Dmain', 'Dboth']:
-                    loss_Dreal = torch.nn.functional.softplus(-logits)
-                    report('Loss/D/loss', loss_Dgen + loss_Dreal)
-                loss_Dr1 = 0
-                if phase in ['Dreg', 'Dboth']:
-                    with torch.autograd.profiler.record_function('r1_grads'), conv2d_gradfix.no_weight_gradients():
-                        r1_grads = torch.autograd.grad(outputs=[logits.sum()], inputs=[real_tmp], create_graph=True,
-                                                       only_inputs=True)[0]
-                    r1_penalty = r1_grads.square().sum([1, 2, 3])
-                    loss_Dr1 = r1_penalty * (self.r1_gamma / 2)
-                    report('Loss/r1_penalty', r1_penalty)
-                    report('Loss/D/reg', loss_Dr1)
-            with torch.autograd.profiler.record_function(name + '_backward'):
-                (loss_Dreal + loss_Dr1).mean().mul(gain).backward()
+    def _discriminator_fake_term(self, z, c, gain, sigma):
+        """-log(1 - sigmoid(D(G(z)))), with the mapping / D EMAs updated (reference :104-112).  Returns the
+        per-sample term for the D loss statistic."""
+        with torch.autograd.profiler.record_function('D_fake'):
+            img, _ = self.run_G(z, c, update_emas=True)
+            logits = self.run_D(img, c, blur_sigma=sigma, update_emas=True)
+            self._report_logits('fake', logits)
+            term = torch.nn.functional.softplus(logits)
+            term.mean().mul(gain).backward()
+        return term
+
+    def _discriminator_real_term(self, real, c, gain, sigma, fake_loss, main, r1):
+        """-log sigmoid(D(x)) and/or the R1 penalty gamma/2 * |d D(x) / dx|^2 on reals, one backward
+        (reference :116-139).  The R1 gradient is a create_graph VJP back through D and the ADA pipe."""
+        with torch.autograd.profiler.record_function('D_real'):
+            x = real.detach().requires_grad_(r1)
+            logits = self.run_D(x, c, blur_sigma=sigma, allow_aug_debug_print=self.allow_aug_debug_print)
+            self._report_logits('real', logits)
+            total = 0
+            if main:
+                term = torch.nn.functional.softplus(-logits)
+                training_stats.report('Loss/D/loss', fake_loss + term)
+                total = term
+            if r1:
+                with conv2d_gradfix.no_weight_gradients():
+                    gx, = torch.autograd.grad(outputs=[logits.sum()], inputs=[x], create_graph=True, only_inputs=True)
+                penalty = gx.square().sum([1, 2, 3])
+                reg = penalty * (self.r1_gamma / 2)
+                training_stats.report('Loss/r1_penalty', penalty)
+                training_stats.report('Loss/D/reg', reg)
+                total = total + reg
+            total.mean().mul(gain).backward()

@@ -1,7 +1,7 @@
 """One StyleGAN2-ADA training iteration, data-parallel over ranks (one process per GPU).
 
 This is the hot loop of SG3/training/training_loop_mi_multimodal.py:308-376, factored out so the
-training loop, bench.py and the tests drive the same code:
+training loop (training/training_loop.py), bench.py and the tests drive the same code:
 
     for phase in [Gmain, Greg(every 4), Dmain, Dreg(every 16)]:           (:326-336)
         zero_grad; module.requires_grad_(True); accumulate over batch_gpu chunks
@@ -10,12 +10,17 @@ training loop, bench.py and the tests drive the same code:
     G_ema = lerp(G, G_ema, beta)                                         (:358-366)
     every ada_interval: p += sign(E[sign(D(real))] - target) * B*I/(ada_kimg*1000)   (:373-376)
 
-Data parallel on MI355X: the gradient exchange is RCCL (torch.distributed backend 'nccl') over
-xGMI.  Gradients are exchanged in buckets of `bucket_mb` MiB; with `overlap=True` each bucket's
-all_reduce is issued from a post-accumulate-grad hook during the LAST micro-batch's backward, so
-the collectives run on RCCL's stream while the remaining backward kernels execute.  The reduction is
-a SUM then /N, then nan_to_num(0, +-1e5) -- the reference's arithmetic, bucketed (fp32 summation
-order differs only by rounding).
+Gradient exchange (`GradExchange`).  Each module owns one persistent flat float32 gradient buffer laid
+out in backward order (reverse registration) and cut into ~`bucket_mb` MiB buckets.  A bucket is filled
+(one cat) as soon as all its parameters hold their final gradient -- from post-accumulate-grad hooks of
+the LAST micro-batch's backward -- and, with several ranks, all-reduced asynchronously (RCCL over xGMI,
+on RCCL's stream) while the rest of the backward runs.  In HIP-graph mode the same hooks run during
+capture, so the fills AND the RCCL all_reduces are captured into the phase graph on a forked stream
+branch and joined at its end: a replay overlaps them with the replayed backward (RCCL collectives capture
+into hipGraphs on this stack: tools/probe_graph_rccl.py).  The optimiser (training/optim.py FlatAdam,
+torch.optim.Adam arithmetic) then reads the flat buffer directly: /N, nan_to_num(0, +-1e5) and Adam are
+one launch.  Summation order of the all_reduce differs from the reference's single flat all_reduce only
+by fp32 rounding.
 """
 import numpy as np
 import torch
@@ -23,95 +28,143 @@ import torch
 import dnnlib
 from torch_utils import misc
 from torch_utils import training_stats
+from training.optim import FlatAdam, EmaLerp, fused_adam_ok
 
 
-class GradReducer:
-    """Bucketed, optionally backward-overlapped, flat gradient all-reduce for one module."""
+class GradExchange:
+    """Flat, bucketed, backward-overlapped gradient all-reduce of one module's parameters."""
 
     def __init__(self, module, num_gpus, bucket_mb=32, overlap=True):
-        self.params = [p for p in module.parameters()]
+        self.params = list(module.parameters())
         self.num_gpus = num_gpus
         self.overlap = overlap and num_gpus > 1
-        self.bucket_elems = max(1, int(bucket_mb * (1 << 20) // 4))
-        self._hooks = []
-        self._armed = False
-        self._pending = []
-
-    # Buckets follow reverse registration order (roughly the order backward produces gradients).
-    def _buckets(self, params):
-        buckets, cur, size = [], [], 0
-        for p in reversed(params):
-            cur.append(p)
-            size += p.numel()
-            if size >= self.bucket_elems:
-                buckets.append(cur)
-                cur, size = [], 0
+        self.order = list(range(len(self.params)))[::-1]          # backward order
+        self.offsets = [0] * len(self.params)
+        bucket_elems = max(1, int(bucket_mb * (1 << 20) // 4))
+        self.buckets = []                                          # (start, end, [param idx])
+        off, cur, start = 0, [], 0
+        for i in self.order:
+            self.offsets[i] = off
+            off += self.params[i].numel()
+            cur.append(i)
+            if off - start >= bucket_elems:
+                self.buckets.append((start, off, cur))
+                cur, start = [], off
         if cur:
-            buckets.append(cur)
-        return buckets
+            self.buckets.append((start, off, cur))
+        self.bucket_of = {i: b for b, (_, _, idx) in enumerate(self.buckets) for i in idx}
+        self.total = off
+        self.flat = None
+        self.expect = {}         # phase name -> participating parameter indices (learned from the last run)
+        self._zeros = {}
+        self._reset()
 
-    def arm(self, expected=1):
-        """Call before the last micro-batch: launch a bucket's all_reduce once every parameter in it
-        has accumulated `expected` gradients (the number of backward passes of this micro-batch)."""
+    def _reset(self):
+        self._filled = [False] * len(self.buckets)
+        self._works = []
+        self._hooks = []
+        self._ready = [0] * len(self.buckets)
+
+    def _flat(self, device):
+        if self.flat is None or self.flat.device != device:
+            self.flat = torch.zeros([self.total], dtype=torch.float32, device=device)
+        return self.flat
+
+    def _fill(self, b):
+        """Copy bucket b's gradients into its flat range (zeros for a parameter without one)."""
+        s, e, idx = self.buckets[b]
+        grads = []
+        for i in idx:
+            g = self.params[i].grad
+            if g is None:
+                z = self._zeros.get(i)
+                if z is None:
+                    z = self._zeros[i] = torch.zeros_like(self.params[i])
+                g = z
+            grads.append(g.reshape(-1))
+        flat = self._flat(grads[0].device)
+        torch.cat(grads, out=flat[s:e])
+        self._filled[b] = True
+
+    def _reduce(self, b):
+        if self.num_gpus > 1:
+            s, e, _ = self.buckets[b]
+            self._works.append(torch.distributed.all_reduce(self.flat[s:e], async_op=True))
+
+    def arm(self, phase, passes=1):
+        """Before the last micro-batch: fill and all-reduce each bucket once every participating parameter
+        in it has accumulated `passes` gradients (eagerly, or into the graph being captured)."""
+        self._reset()
         if not self.overlap:
             return
-        self._armed = True
-        self._pending = []
-        trainable = [p for p in self.params if p.requires_grad]
-        self._bucket_of = {}
-        self._ready = []
-        self._bucket_list = self._buckets(trainable)
-        for bi, b in enumerate(self._bucket_list):
-            self._ready.append(0)
-            for p in b:
-                self._bucket_of[p] = bi
-        self._launched = [False] * len(self._bucket_list)
+        part = set(self.expect.get(phase, range(len(self.params))))
+        need = [sum(1 for i in idx if i in part) * passes for _, _, idx in self.buckets]
 
-        def hook(p):
-            bi = self._bucket_of.get(p)
-            if bi is None or p.grad is None:   # the hook also fires for structurally-zero (undefined) grads
+        def hook(p, i):
+            b = self.bucket_of[i]
+            if p.grad is None or i not in part or self._filled[b]:
                 return
-            self._ready[bi] += 1
-            if self._ready[bi] == expected * len(self._bucket_list[bi]) and not self._launched[bi]:
-                self._launch(bi)
+            self._ready[b] += 1
+            if self._ready[b] == need[b]:
+                self._fill(b)
+                self._reduce(b)
 
-        self._hooks = [p.register_post_accumulate_grad_hook(hook) for p in trainable]
+        self._hooks = [p.register_post_accumulate_grad_hook(lambda p_, i_=i: hook(p_, i_))
+                       for i, p in enumerate(self.params) if p.requires_grad]
 
-    def _launch(self, bi):
-        b = self._bucket_list[bi]
-        flat = torch.cat([p.grad.flatten() for p in b])
-        work = torch.distributed.all_reduce(flat, async_op=True)
-        self._pending.append((b, flat, work))
-        self._launched[bi] = True
-
-    def finish(self):
-        """Reduce whatever is not reduced yet, average, sanitise and write back into .grad."""
+    def disarm(self):
         for h in self._hooks:
             h.remove()
         self._hooks = []
-        params = [p for p in self.params if p.grad is not None]
-        if not params:
-            return
-        done = set()
-        results = []
-        for b, flat, work in self._pending:
-            results.append((b, flat, work))
-            done.update(id(p) for p in b)
-        rest = [p for p in params if id(p) not in done]
-        if rest:
-            flat = torch.cat([p.grad.flatten() for p in rest])
-            work = torch.distributed.all_reduce(flat, async_op=True) if self.num_gpus > 1 else None
-            results.append((rest, flat, work))
-        for b, flat, work in results:
-            if work is not None:
-                work.wait()
-            if self.num_gpus > 1:
-                flat /= self.num_gpus
-            misc.nan_to_num(flat, nan=0, posinf=1e5, neginf=-1e5, out=flat)
-            for p, g in zip(b, flat.split([p.numel() for p in b])):
-                p.grad = g.reshape(p.shape)
-        self._pending = []
-        self._armed = False
+
+    def fill_rest(self):
+        """Fill every bucket the hooks did not (end of the backward, or of a phase graph)."""
+        self.disarm()
+        for b in range(len(self.buckets)):
+            if not self._filled[b]:
+                self._fill(b)
+
+    def close_capture(self):
+        """End of a captured phase: fill and reduce the remaining buckets and join every collective back
+        into the capture stream, so the graph ends with the exchange complete."""
+        self.disarm()
+        hooked = sum(self._filled)
+        for b in range(len(self.buckets)):
+            if not self._filled[b]:
+                self._fill(b)
+                self._reduce(b)
+        for w in self._works:
+            w.wait()
+        self._reset()
+        return hooked
+
+    def finish(self, phase, part=None):
+        """Complete the exchange: fill / reduce what is left, wait, point each participating parameter's
+        .grad at its range of the flat buffer.  Returns the participating parameter indices (those with a
+        gradient; a replayed graph passes the set it captured)."""
+        learn = part is None
+        if part is None:
+            part = [i for i in range(len(self.params)) if self.params[i].grad is not None]
+        if not any(self._filled):
+            self.fill_rest()
+            for b in range(len(self.buckets)):
+                self._reduce(b)
+        else:
+            self.disarm()
+            for b in range(len(self.buckets)):
+                if not self._filled[b]:
+                    self._fill(b)
+                    self._reduce(b)
+        for w in self._works:
+            w.wait()
+        self._works = []
+        if learn:
+            self.expect[phase] = part
+        for i in part:
+            p = self.params[i]
+            p.grad = self.flat[self.offsets[i]:self.offsets[i] + p.numel()].view_as(p)
+        self._reset()
+        return part
 
 
 class Trainer:
@@ -130,66 +183,79 @@ class Trainer:
         self.phases = []
         for name, module, opt_kwargs, reg_interval in [('G', G, G_opt_kwargs, G_reg_interval),
                                                        ('D', D, D_opt_kwargs, D_reg_interval)]:
-            reducer = GradReducer(module, num_gpus, bucket_mb=bucket_mb, overlap=overlap)
-            if reg_interval is None:
-                opt = dnnlib.util.construct_class_by_name(params=module.parameters(), **opt_kwargs)
-                self.phases.append(dnnlib.EasyDict(name=name + 'both', module=module, opt=opt, interval=1,
-                                                   reducer=reducer))
-            else:   # lazy regularisation (:248-255)
+            exchange = GradExchange(module, num_gpus, bucket_mb=bucket_mb, overlap=overlap)
+            kw = dnnlib.EasyDict(opt_kwargs)
+            if reg_interval is not None:          # lazy regularisation (:248-255)
                 ratio = reg_interval / (reg_interval + 1)
-                kw = dnnlib.EasyDict(opt_kwargs)
                 kw.lr = kw.lr * ratio
                 kw.betas = [b ** ratio for b in kw.betas]
+            if fused_adam_ok(kw, device):
+                opt = FlatAdam(module.parameters(), **{k: v for k, v in kw.items() if k != 'class_name'})
+            else:
                 opt = dnnlib.util.construct_class_by_name(module.parameters(), **kw)
+            if reg_interval is None:
+                self.phases.append(dnnlib.EasyDict(name=name + 'both', module=module, opt=opt, interval=1,
+                                                   exchange=exchange))
+            else:
                 self.phases.append(dnnlib.EasyDict(name=name + 'main', module=module, opt=opt, interval=1,
-                                                   reducer=reducer))
+                                                   exchange=exchange))
                 self.phases.append(dnnlib.EasyDict(name=name + 'reg', module=module, opt=opt,
-                                                   interval=reg_interval, reducer=reducer))
+                                                   interval=reg_interval, exchange=exchange))
         for ph in self.phases:
             ph.start_event = ph.end_event = None
             if phase_timing and device is not None and device.type == 'cuda':
                 ph.start_event = torch.cuda.Event(enable_timing=True)
                 ph.end_event = torch.cuda.Event(enable_timing=True)
+        self.ema = EmaLerp(G_ema, G) if isinstance(self.phases[0].opt, FlatAdam) else None
         self.cur_nimg = 0
         self.batch_idx = 0
         self.on_grads = None   # optional callback(phase_name, module) after the gradient exchange
-        # HIP-graph mode: each phase's forward + backward (all micro-batches) is captured once and
-        # replayed; the gradient exchange, the optimiser, EMA and ADA stay eager.  Capture the first
-        # time a phase runs in graph mode -- run at least one eager step first so every lazily created
-        # state (kernel attributes, statistics counters, cached constants) exists before capture.
+        # HIP-graph mode: each phase's forward + backward (all micro-batches) and its bucket fills are
+        # captured once and replayed (with the gradient exchange); the optimiser, EMA and ADA stay eager.  Capture the
+        # first time a phase runs in graph mode -- run at least one eager step first so every lazily created
+        # state (kernel attributes, statistics rows, cached constants, participation sets) exists.
         self.graphs = graphs
         self._graphs = {}
 
-    def _accumulate(self, phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c, arm):
+    @staticmethod
+    def _passes(name):
+        return 2 if name in ('Dmain', 'Dboth') else 1    # D phases backward once for fakes, once for reals
+
+    def _accumulate(self, phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c):
         chunks = list(zip(phase_real_img, phase_real_c, phase_gen_z, phase_gen_c))
         for ci, (real_img, real_c, gen_z, gen_c) in enumerate(chunks):
-            if arm and ci == len(chunks) - 1:
-                phase.reducer.arm(expected=2 if phase.name in ('Dmain', 'Dboth') else 1)
+            if ci == len(chunks) - 1:
+                phase.exchange.arm(phase.name, self._passes(phase.name))
             self.loss.accumulate_gradients(phase=phase.name, real_img=real_img, real_c=real_c, gen_z=gen_z,
                                            gen_c=gen_c, gain=phase.interval, cur_nimg=self.cur_nimg)
 
     def _graph_phase(self, phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c):
+        """Replay the phase's graph (capturing it the first time): forward + backward of every micro-batch,
+        the bucket fills and (several ranks) the overlapped all_reduces.  Returns the participating
+        parameter indices of the captured exchange."""
         st = self._graphs.get(phase.name)
+        ex = phase.exchange
         if st is None:
             st = dnnlib.EasyDict()
             st.inputs = [[t.clone() for t in lst] for lst in (phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)]
-            st.params = list(phase.module.parameters())
             phase.opt.zero_grad(set_to_none=True)
+            ex._flat(self.device)
             torch.cuda.synchronize(self.device)
             st.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(st.graph):
                 phase.module.requires_grad_(True)
-                self._accumulate(phase, *st.inputs, arm=False)
+                self._accumulate(phase, *st.inputs)
+                st.part = [i for i, p in enumerate(ex.params) if p.grad is not None]
+                st.overlapped = ex.close_capture()
                 phase.module.requires_grad_(False)
-            st.grads = [p.grad for p in st.params]      # the graph writes these buffers on every replay
             self._graphs[phase.name] = st
         else:
             for dst, src in zip(st.inputs, (phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)):
                 for d, s_ in zip(dst, src):
                     d.copy_(s_)
-        for p, g in zip(st.params, st.grads):
-            p.grad = g
         st.graph.replay()
+        ex._filled = [True] * len(ex.buckets)     # filled and reduced inside the graph
+        return st.part
 
     def step(self, phase_real_img, phase_real_c, all_gen_z, all_gen_c):
         """One iteration.  phase_real_img/c: lists of batch_gpu chunks; all_gen_z/c: per phase, lists
@@ -199,18 +265,29 @@ class Trainer:
                 continue
             if phase.start_event is not None:
                 phase.start_event.record(torch.cuda.current_stream(self.device))
+            part = None
             if self.graphs:
-                self._graph_phase(phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)
+                part = self._graph_phase(phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)
             else:
                 phase.opt.zero_grad(set_to_none=True)
                 phase.module.requires_grad_(True)
-                self._accumulate(phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c, arm=True)
+                self._accumulate(phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)
                 phase.module.requires_grad_(False)
             with torch.autograd.profiler.record_function(phase.name + '_opt'):
-                phase.reducer.finish()
+                ex = phase.exchange
+                part = ex.finish(phase.name, part)
+                if isinstance(phase.opt, FlatAdam):
+                    phase.opt.step_flat(ex.flat, ex.offsets, part, grad_scale=1.0 / self.num_gpus,
+                                        write_grad=self.on_grads is not None)
+                else:
+                    flat = ex.flat
+                    if self.num_gpus > 1:
+                        flat /= self.num_gpus
+                    misc.nan_to_num(flat, nan=0, posinf=1e5, neginf=-1e5, out=flat)
                 if self.on_grads is not None:
                     self.on_grads(phase.name, phase.module)
-                phase.opt.step()
+                if not isinstance(phase.opt, FlatAdam):
+                    phase.opt.step()
             if phase.end_event is not None:
                 phase.end_event.record(torch.cuda.current_stream(self.device))
 
@@ -220,11 +297,13 @@ class Trainer:
                 ema_nimg = min(ema_nimg, self.cur_nimg * self.ema_rampup)
             ema_beta = 0.5 ** (self.batch_size / max(ema_nimg, 1e-8))
             with torch.no_grad():
-                ema_p = list(self.G_ema.parameters())
-                cur_p = list(self.G.parameters())
-                torch._foreach_lerp_(ema_p, cur_p, 1.0 - ema_beta)   # p.lerp(p_ema, beta) written into p_ema
-                for b_ema, b in zip(self.G_ema.buffers(), self.G.buffers()):
-                    b_ema.copy_(b)
+                if self.ema is not None:
+                    self.ema(ema_beta)
+                else:
+                    for p_ema, p in zip(self.G_ema.parameters(), self.G.parameters()):
+                        p_ema.copy_(p.lerp(p_ema, ema_beta))
+                    for b_ema, b in zip(self.G_ema.buffers(), self.G.buffers()):
+                        b_ema.copy_(b)
 
         self.cur_nimg += self.batch_size
         self.batch_idx += 1

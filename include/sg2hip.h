@@ -14,9 +14,10 @@
  *   autograd weight gradient of those convolutions (cuDNN wgrad)          -> sg2_conv2d_wgrad
  *   SG3/torch_utils/ops/grid_sample_gradfix.py:28-65 (aten grid_sampler_2d fwd/bwd)
  *                                                                          -> sg2_grid_sample_fwd / _bwd
- *   SG3/training/networks_stylegan2.py:59-63 demodulation coefficients    -> sg2_demod_coefs
- *   SG3/training/training_loop_mi_multimodal.py:343-351,363-364 (nan_to_num + Adam, EMA lerp)
- *                                                                          -> sg2_adam_step, sg2_lerp
+ *   SG3/training/networks_stylegan2.py:59-63 demodulation coefficients    -> sg2_demod_fwd / _bwd
+ *   SG3/training/training_loop_mi_multimodal.py:341-351 (flat grad, /N, nan_to_num, torch.optim.Adam)
+ *                                                                          -> sg2_adam_multi
+ *   SG3/training/training_loop_mi_multimodal.py:358-366 (G_ema lerp)      -> sg2_lerp_multi
  *
  * Conventions
  *  - Every pointer is a device pointer; the library never allocates or frees device memory and keeps
@@ -38,7 +39,7 @@
 extern "C" {
 #endif
 
-#define SG2_ABI_VERSION 1
+#define SG2_ABI_VERSION 2
 
 enum sg2_dtype { SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2 };
 
@@ -203,11 +204,8 @@ int sg2_reflect_pad_dyn(float* y, const float* x, const int* margins, int N, int
                         int adjoint, void* stream);
 
 /* Demodulation coefficients d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps), wsq[o,i] = sum_k w[o,i,k]^2
- * (SG3/training/networks_stylegan2.py:59-63, summation regrouped).  s [N,I] f32, w [O,I*KK] f32. */
-int sg2_demod_coefs(float* d, const float* s, const float* w, int N, int O, int I, int KK, float eps,
-                    void* stream);
-
-/* sg2_demod_coefs that also writes wsq [O, I] (may be NULL) for the backward. */
+ * (SG3/training/networks_stylegan2.py:59-63, summation regrouped); s [N,I] f32, w [O,I*KK] f32.  Also
+ * writes wsq [O, I] (may be NULL) for the backward. */
 int sg2_demod_fwd(float* d, float* wsq, const float* s, const float* w, int N, int O, int I, int KK, float eps,
                   void* stream);
 
@@ -236,15 +234,24 @@ int sg2_infnorm_fwd(float* y, float* nrm, const float* t, int rows, int L, float
 int sg2_infnorm_bwd(float* dt, const float* dy, const float* t, const float* nrm, int rows, int L, float c, int mode,
                     void* stream);
 
-/* Adam step on a flat float32 parameter vector (torch.optim.Adam semantics, no weight decay,
- * amsgrad off) with the reference's gradient sanitation fused in front:
- *   g = nan_to_num(g * grad_scale, nan=0, posinf=1e5, neginf=-1e5)  (training_loop_mi_multimodal.py:346-347)
- * step is the 1-based step count after increment. */
-int sg2_adam_step(float* param, float* exp_avg, float* exp_avg_sq, const float* grad, int64_t n, float lr,
-                  float beta1, float beta2, float eps, float grad_scale, int64_t step, void* stream);
+/* Multi-tensor launches of the optimiser step.  A segment is one parameter tensor; `blocks` [nblocks] lists
+ * the work items as (segment << 40) | start, one per 4096 elements of a segment (start = 0, 4096, ...),
+ * so one launch covers a whole module.  Tables are device int64 / float arrays built by the caller. */
 
-/* dst = src + (dst - src) * beta  == src.lerp(dst, beta)   (G_ema update, training_loop:363-364). */
-int sg2_lerp(float* dst, const float* src, int64_t n, float beta, void* stream);
+/* torch.optim.Adam (no weight decay, amsgrad off; foreach arithmetic) of every parameter in one exchanged
+ * flat gradient, with the reference's sanitation in front (training_loop_mi_multimodal.py:341-351):
+ *   g = nan_to_num(grad * grad_scale, nan=0, posinf=1e5, neginf=-1e5)      (grad_scale = 1/num_gpus)
+ *   m = m.lerp(g, 1-beta1);  v = v*beta2 + (1-beta2)*g*g;  p += -step_size * m / (sqrt(v)/bc2_sqrt + eps)
+ * seg [nseg][3] = {float* param, offset of the segment in grad / exp_avg / exp_avg_sq, numel};
+ * coef [nseg][2] f32 = {step_size = lr / (1 - beta1^step), bc2_sqrt = sqrt(1 - beta2^step)} (the caller's
+ * per-parameter step counts, as torch keeps them).  write_grad != 0 stores the sanitised g back. */
+int sg2_adam_multi(const int64_t* seg, const float* coef, const int64_t* blocks, int nblocks, float* grad,
+                   float* exp_avg, float* exp_avg_sq, float beta1, float beta2, float eps, float grad_scale,
+                   int write_grad, void* stream);
+
+/* dst = src.lerp(dst, beta) per segment (the G_ema update, training_loop_mi_multimodal.py:363-364);
+ * seg [nseg][3] = {float* dst, const float* src, numel}. */
+int sg2_lerp_multi(const int64_t* seg, const int64_t* blocks, int nblocks, float beta, void* stream);
 
 #ifdef __cplusplus
 }

@@ -20,6 +20,10 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+# The oracle's real type.  float32 is the reference's CPU arithmetic; tests/golden/make_golden.py sets
+# float64 to evaluate the exact (rounding-free) answer the fp32 results are judged against.
+REAL = torch.float32
+
 # =============================================================================================
 # upfirdn2d  (SG3/torch_utils/ops/upfirdn2d.py)
 # =============================================================================================
@@ -49,7 +53,7 @@ def filter_size(f):
 
 def setup_filter(f, normalize=True, flip_filter=False, gain=1, separable=None):
     """SG3 upfirdn2d.py:70-114."""
-    f = torch.as_tensor(1 if f is None else f, dtype=torch.float32)
+    f = torch.as_tensor(1 if f is None else f, dtype=REAL)
     if f.ndim == 0:
         f = f.reshape(1)
     if separable is None:
@@ -66,7 +70,7 @@ def setup_filter(f, normalize=True, flip_filter=False, gain=1, separable=None):
 def upfirdn2d(x, f, up=1, down=1, padding=0, flip_filter=False, gain=1):
     """Zero-insert upsample, pad/crop, FIR, decimate.  SG3 upfirdn2d.py:166-211."""
     if f is None:
-        f = torch.ones([1, 1], dtype=torch.float32)
+        f = torch.ones([1, 1], dtype=REAL)
     n, c, h, w = x.shape
     ux, uy = _pair(up)
     dx, dy = _pair(down)
@@ -294,7 +298,7 @@ class FullyConnectedLayer(torch.nn.Module):
         super().__init__()
         self.activation = activation
         self.weight = torch.nn.Parameter(torch.randn([out_features, in_features]) / lr_multiplier)
-        self.bias = torch.nn.Parameter(torch.full([out_features], np.float32(bias_init))) if bias else None
+        self.bias = torch.nn.Parameter(torch.full([out_features], float(np.float32(bias_init)), dtype=REAL)) if bias else None
         self.weight_gain = lr_multiplier / np.sqrt(in_features)
         self.bias_gain = lr_multiplier
 
@@ -365,9 +369,9 @@ class MappingNetwork(torch.nn.Module):
     def forward(self, z, c, truncation_psi=1, truncation_cutoff=None, update_emas=False):
         x = None
         if self.z_dim > 0:
-            x = normalize_2nd_moment(z.float())
+            x = normalize_2nd_moment(z.to(REAL))
         if self.c_dim > 0:
-            y = normalize_2nd_moment(self.embed(c.float()))
+            y = normalize_2nd_moment(self.embed(c.to(REAL)))
             x = torch.cat([x, y], dim=1) if x is not None else y
         for i in range(self.num_layers):
             x = getattr(self, f'fc{i}')(x)
@@ -480,7 +484,7 @@ class SynthesisBlock(torch.nn.Module):
         if img is not None:
             img = upsample2d(img, self.resample_filter)
         if self.is_last or self.architecture == 'skip':
-            y = self.torgb(x, next(w_iter), fused_modconv=fused_modconv).float()
+            y = self.torgb(x, next(w_iter), fused_modconv=fused_modconv).to(REAL)
             img = img + y if img is not None else y
         return x, img
 
@@ -507,7 +511,7 @@ class SynthesisNetwork(torch.nn.Module):
             setattr(self, f'b{r}', block)
 
     def forward(self, ws, **block_kwargs):
-        ws = ws.float()
+        ws = ws.to(REAL)
         x = img = None
         idx = 0
         for r in self.block_resolutions:
@@ -612,9 +616,9 @@ class DiscriminatorEpilogue(torch.nn.Module):
         self.out = FullyConnectedLayer(in_channels, 1 if cmap_dim == 0 else cmap_dim)
 
     def forward(self, x, img, cmap, force_fp32=False):
-        x = x.float()
+        x = x.to(REAL)
         if self.architecture == 'skip':
-            x = x + self.fromrgb(img.float())
+            x = x + self.fromrgb(img.to(REAL))
         if self.mbstd is not None:
             x = self.mbstd(x)
         x = self.conv(x)
@@ -676,7 +680,7 @@ def _mat(*rows):
     """Batched homogeneous matrix from rows of tensors/scalars (augment_mi.py:52-60)."""
     ref = [v for r in rows for v in r if isinstance(v, torch.Tensor)]
     if not ref:
-        return torch.tensor(np.asarray(rows), dtype=torch.float32)
+        return torch.tensor(np.asarray(rows), dtype=REAL)
     shape = ref[0].shape
     elems = [v if isinstance(v, torch.Tensor) else torch.full(shape, float(v)) for r in rows for v in r]
     return torch.stack(elems, dim=-1).reshape(*shape, len(rows), -1)
@@ -745,11 +749,11 @@ class AugmentPipe(torch.nn.Module):
             setattr(self, k, float(v))
         self.imgfilter_bands = list(imgfilter_bands)
         self.register_buffer('Hz_geom', setup_filter(WAVELETS['sym6']))
-        self.register_buffer('Hz_fbank', torch.as_tensor(_filter_bank(), dtype=torch.float32))
+        self.register_buffer('Hz_fbank', torch.as_tensor(_filter_bank(), dtype=REAL))
 
     def forward(self, images, allow_aug_debug_print=False, debug_percentile=None):
         n, c, h, w = images.shape
-        dp = None if debug_percentile is None else torch.as_tensor(debug_percentile, dtype=torch.float32)
+        dp = None if debug_percentile is None else torch.as_tensor(debug_percentile, dtype=REAL)
         I3 = torch.eye(3)
         G = I3
         if self.xflip > 0:                                                       # :213-218
@@ -809,9 +813,9 @@ class AugmentPipe(torch.nn.Module):
             hz_pad = self.Hz_geom.shape[0] // 4
             margin = cp[:, :2, :].permute(1, 0, 2).flatten(1)
             margin = torch.cat([-margin, margin]).max(dim=1).values
-            margin = margin + torch.tensor([hz_pad * 2 - cx, hz_pad * 2 - cy] * 2, dtype=torch.float32)
-            margin = margin.max(torch.tensor([0, 0] * 2, dtype=torch.float32))
-            margin = margin.min(torch.tensor([w - 1, h - 1] * 2, dtype=torch.float32))
+            margin = margin + torch.tensor([hz_pad * 2 - cx, hz_pad * 2 - cy] * 2, dtype=REAL)
+            margin = margin.max(torch.tensor([0, 0] * 2, dtype=REAL))
+            margin = margin.min(torch.tensor([w - 1, h - 1] * 2, dtype=REAL))
             mx0, my0, mx1, my1 = [int(v) for v in margin.ceil().to(torch.int32)]
             images = F.pad(images, [mx0, mx1, my0, my1], mode='reflect')
             G = translate2d((mx0 - mx1) / 2, (my0 - my1) / 2) @ G
@@ -838,7 +842,7 @@ class AugmentPipe(torch.nn.Module):
             if dp is not None:
                 k = torch.full_like(k, torch.exp2(torch.erfinv(dp * 2 - 1) * self.contrast_std))
             C = scale3d(k, k, k) @ C
-        v = torch.tensor(np.asarray([1, 1, 1, 0]) / np.sqrt(3), dtype=torch.float32)
+        v = torch.tensor(np.asarray([1, 1, 1, 0]) / np.sqrt(3), dtype=REAL)
         if self.lumaflip > 0:                                                    # :349-354
             i = torch.floor(torch.rand([n, 1, 1]) * 2)
             i = torch.where(torch.rand([n, 1, 1]) < self.lumaflip * self.p, i, torch.zeros_like(i))
@@ -870,7 +874,7 @@ class AugmentPipe(torch.nn.Module):
 
         if self.imgfilter > 0:                                                   # :392-420
             nb = self.Hz_fbank.shape[0]
-            power = torch.tensor(np.array([10, 1, 1, 1]) / 13, dtype=torch.float32)
+            power = torch.tensor(np.array([10, 1, 1, 1]) / 13, dtype=REAL)
             g = torch.ones([n, nb])
             for i, bs in enumerate(self.imgfilter_bands):
                 ti = torch.exp2(torch.randn([n]) * self.imgfilter_std)
@@ -906,7 +910,7 @@ class AugmentPipe(torch.nn.Module):
             cy_ = torch.arange(h).reshape(1, 1, -1, 1)
             mx = ((cx_ + 0.5) / w - center[:, 0]).abs() >= size[:, 0] / 2
             my = ((cy_ + 0.5) / h - center[:, 1]).abs() >= size[:, 1] / 2
-            images = images * torch.logical_or(mx, my).float()
+            images = images * torch.logical_or(mx, my).to(REAL)
         return images
 
 

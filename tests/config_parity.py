@@ -1,0 +1,323 @@
+"""Training-iteration parity at BASELINE.json configuration widths (test infrastructure).
+
+One full iteration (Gmain, Greg, Dmain, Dreg with the reference's gains, nan_to_num, lazy-reg Adam,
+G_ema) runs on identical states (golden_init.init_state, keyed by parameter names), inputs and RNG
+draws (rngtape.Tape) through
+  * the product (HIP kernels, cuda:0, training/trainer.py Trainer),
+  * the CPU oracle (oracle/sg2_oracle.py, fp32),
+and is compared by `golden_init.summarize` (per-tensor L2 norm + 8 sampled entries) -- against the
+reference-generated fixture (tests/golden/train_c1.npz, BASELINE configs[0]) or against the oracle run
+in the same test (C2/C4/C5 widths, where a reference fixture would be too large to commit).
+
+Error measures (all relative):
+  * norm:    |‖a‖ - ‖b‖| / ‖b‖ per tensor;
+  * samples: max_i |a_i - b_i| / rms(b) per tensor, rms = ‖b‖ / sqrt(numel) -- entry errors scaled
+             by the tensor's typical magnitude, so near-zero entries do not blow the ratio up;
+  * stats:   relative L2 of each reported loss vector (signs skipped: sign(0±eps) is rounding).
+"""
+import ast
+import copy
+
+import numpy as np
+import torch
+
+from golden_init import init_state, summarize, unpack
+from rngtape import Tape
+
+CLARO_AUG = dict(xflip=1, xint=1, scale=1, rotate=1, aniso=1, xfrac=1, xint_max=0.05, rotate_max=3 / 360,
+                 xfrac_std=0.05, scale_std=0.05, aniso_std=0.05)
+PHASES = ['Gmain', 'Greg', 'Dmain', 'Dreg']
+
+
+def _nets(mod, cfg, num_fp16_res, fp16_dtype=None, **extra):
+    gk, dk = {}, {}
+    if fp16_dtype is not None:
+        gk['fp16_dtype'] = fp16_dtype
+        dk['block_kwargs'] = dict(fp16_dtype=fp16_dtype)
+    G = mod.Generator(z_dim=cfg['z_dim'], c_dim=cfg['c_dim'], w_dim=cfg['w_dim'], img_resolution=cfg['img_resolution'],
+                      img_channels=cfg['img_channels'], channel_base=cfg['channel_base'],
+                      channel_max=cfg['channel_max'], num_fp16_res=num_fp16_res, conv_clamp=256,
+                      fused_modconv_default='inference_only', mapping_kwargs=dict(num_layers=cfg['map_depth']),
+                      **gk).train().requires_grad_(False)
+    D = mod.Discriminator(c_dim=cfg['c_dim'], img_resolution=cfg['img_resolution'], img_channels=cfg['img_channels'],
+                          channel_base=cfg['channel_base'], channel_max=cfg['channel_max'], num_fp16_res=num_fp16_res,
+                          conv_clamp=256, epilogue_kwargs=dict(mbstd_group_size=cfg['mbstd']),
+                          **dk).train().requires_grad_(False)
+    init_state(G, seed=1)
+    init_state(D, seed=2)
+    return G, D
+
+
+def make_inputs(cfg, seed=31):
+    r = np.random.RandomState(seed)
+    B, c_dim = cfg['batch'], cfg['c_dim']
+    z = r.standard_normal((B, cfg['z_dim'])).astype(np.float32)
+    c = np.eye(max(c_dim, 1), dtype=np.float32)[r.randint(max(c_dim, 1), size=B)][:, :c_dim]
+    real = r.uniform(-1, 1, (B, cfg['img_channels'], cfg['img_resolution'], cfg['img_resolution'])).astype(np.float32)
+    gen_z = r.standard_normal((4, B, cfg['z_dim'])).astype(np.float32)
+    gen_c = np.eye(max(c_dim, 1), dtype=np.float32)[r.randint(max(c_dim, 1), size=(4, B))][..., :c_dim]
+    return dict(z=z, c=c, real=real, gen_z=gen_z, gen_c=gen_c)
+
+
+def run_oracle(cfg, inp, tape, aug_p=0.3):
+    """The CPU oracle's iteration; `tape` records (mode 'record') or replays its draws."""
+    from oracle import sg2_oracle as O
+    torch.manual_seed(0)
+    G, D = _nets(O, cfg, 4)
+    G_ema = copy.deepcopy(G).eval()
+    aug = O.AugmentPipe(**CLARO_AUG)
+    aug.p.fill_(aug_p)
+    stats = []
+    loss = O.StyleGAN2Loss(None, G, D, augment_pipe=aug, r1_gamma=0.4096, style_mixing_prob=0.9, pl_weight=2,
+                           pl_no_weight_grad=True, report=lambda n, v: stats.append((n, v.detach().clone())))
+    out = {}
+
+    def on_grads(name, module):
+        out.update(summarize({n: p.grad for n, p in module.named_parameters() if p.grad is not None},
+                             f'grad/{name}'))
+
+    T = lambda a: torch.from_numpy(np.array(a, dtype=np.float32)).to(O.REAL)  # noqa: E731
+    ctx = tape.record() if not tape.entries else tape.replay()
+    with ctx:
+        O.train_iteration(loss, O.make_phases(G, D), G, G_ema, T(inp['real']), T(inp['c']), T(inp['gen_z']),
+                          T(inp['gen_c']), batch_idx=0, cur_nimg=1000, batch_size=cfg['batch'], on_grads=on_grads)
+    out['pl_mean'] = loss.pl_mean.detach().numpy()
+    out.update(summarize(dict(G.named_parameters()), 'G1'))
+    out.update(summarize(dict(D.named_parameters()), 'D1'))
+    out.update(summarize(dict(G_ema.named_parameters()), 'Gema1'))
+    return out, [(n, v.numpy()) for n, v in stats]
+
+
+def run_oracle_f64(cfg, inp, tape, aug_p=0.3):
+    """The oracle evaluated in float64 on the same draws: the rounding-free answer that f32 results (the
+    reference's and the product's alike) are judged against."""
+    from oracle import sg2_oracle as O
+    prev = (O.REAL, torch.get_default_dtype())
+    O.REAL = torch.float64
+    torch.set_default_dtype(torch.float64)
+    try:
+        return run_oracle(cfg, inp, tape, aug_p)
+    finally:
+        O.REAL = prev[0]
+        torch.set_default_dtype(prev[1])
+
+
+def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False):
+    """The product's iteration on `dev`.  fp16_dtype None: all-f32 (num_fp16_res=0, the reference's CPU
+    arithmetic); else the reference's GPU default num_fp16_res=4 in that 16-bit type."""
+    from training import networks_stylegan2 as net, augment_mi, loss as loss_mod, trainer as trainer_mod
+    torch.manual_seed(0)
+    G, D = _nets(net, cfg, 0 if fp16_dtype is None else 4, fp16_dtype)
+    G, D = G.to(dev), D.to(dev)
+    G_ema = copy.deepcopy(G).eval()
+    aug = augment_mi.AugmentPipe(run_dir=None, batch_size=cfg['batch'], **CLARO_AUG).train().requires_grad_(False).to(dev)
+    aug.p.copy_(torch.as_tensor(aug_p))
+    loss = loss_mod.StyleGAN2Loss(device=dev, G=G, D=D, augment_pipe=aug, r1_gamma=0.4096, style_mixing_prob=0.9,
+                                  pl_weight=2, pl_no_weight_grad=True)
+    opt = dict(class_name='torch.optim.Adam', lr=0.0025, betas=[0, 0.99], eps=1e-8)
+    tr = trainer_mod.Trainer(G, D, G_ema, loss, opt, opt, batch_size=cfg['batch'], batch_gpu=cfg['batch'],
+                             num_gpus=1, rank=0, device=dev)
+    out, stats = {}, []
+
+    def on_grads(name, module):
+        out.update(summarize({n: p.grad for n, p in module.named_parameters() if p.grad is not None},
+                             f'grad/{name}'))
+
+    tr.on_grads = on_grads
+    tr.cur_nimg = 1000
+    orig = loss_mod.training_stats.report
+    loss_mod.training_stats.report = lambda n, v: (stats.append((n, v.detach().float().cpu().numpy())), v)[1]
+    T = lambda a: torch.from_numpy(np.array(a, dtype=np.float32)).to(dev)  # noqa: E731
+    try:
+        with tape.replay():
+            gz, gc = T(inp['gen_z']), T(inp['gen_c'])
+            tr.step([T(inp['real'])], [T(inp['c'])], [[gz[i]] for i in range(4)], [[gc[i]] for i in range(4)])
+        torch.cuda.synchronize(dev)
+    finally:
+        loss_mod.training_stats.report = orig
+    assert tape.pos == len(tape.entries), 'product consumed a different number of random draws'
+    out['pl_mean'] = loss.pl_mean.detach().cpu().numpy()
+    out.update(summarize(dict(G.named_parameters()), 'G1'))
+    out.update(summarize(dict(D.named_parameters()), 'D1'))
+    out.update(summarize(dict(G_ema.named_parameters()), 'Gema1'))
+    return out, stats
+
+
+def compare(got, want, tol_norm, tol_samples, groups=('grad/', 'G1/', 'D1/', 'Gema1/')):
+    """Returns {group: (worst norm err, worst sample err, key)}; asserts key sets match."""
+    keys_w, keys_g = _keys(want, groups), _keys(got, groups)
+    _one_sided_zero(got, want, keys_g, keys_w)
+    keys_w = sorted(set(keys_w) & set(keys_g))
+    worst = {}
+    for k in keys_w:
+        nw, ng = float(want[k + '/norm']), float(got[k + '/norm'])
+        sw, sg = np.asarray(want[k + '/samples'], np.float64), np.asarray(got[k + '/samples'], np.float64)
+        if nw == 0:
+            e_norm = 0.0 if ng == 0 else float('inf')
+        else:
+            e_norm = abs(ng - nw) / nw
+        rms = max(nw / np.sqrt(float(want[k + '/numel'])), 1e-30)
+        e_s = float(np.max(np.abs(sg - sw))) / rms if nw > 0 else float(np.max(np.abs(sg), initial=0.0))
+        g = 'grad/' + k.split('/')[1] if k.startswith('grad/') else k.split('/')[0]
+        w = worst.get(g, (0.0, 0.0, None))
+        worst[g] = (max(w[0], e_norm), max(w[1], e_s), k if (e_norm > w[0] or e_s > w[1]) else w[2])
+        assert e_norm <= tol_norm, f'{k}: norm rel err {e_norm:.3g} > {tol_norm}'
+        assert e_s <= tol_samples, f'{k}: sampled-entry err {e_s:.3g} (x rms) > {tol_samples}'
+    return worst
+
+
+def _tensor_errs(a, b, k):
+    """(norm error, sampled-entry error) of summary `a` against summary `b` for tensor key k."""
+    nb, na = float(b[k + '/norm']), float(a[k + '/norm'])
+    if nb == 0:
+        return (0.0 if na == 0 else float('inf')), float(np.max(np.abs(np.asarray(a[k + '/samples'])), initial=0.0))
+    rms = nb / np.sqrt(float(b[k + '/numel']))
+    sa, sb = np.asarray(a[k + '/samples'], np.float64), np.asarray(b[k + '/samples'], np.float64)
+    return abs(na - nb) / nb, float(np.max(np.abs(sa - sb), initial=0.0)) / rms
+
+
+# (norm, sampled-entry) floors: gradients; parameters after the step -- Adam's first steps move an element by
+# ~lr * sign(g), so a gradient element that is zero up to rounding (in the reference's f32 as much as here)
+# may move the other way: one such element of a 512-bias (|p| ~ 0.1) shifts its norm by ~2e-4 and the
+# element by ~0.05 of the tensor's rms.
+F32_FLOORS = {'grad': (1e-4, 1e-3), 'param': (1e-3, 1e-1)}
+
+
+def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True):
+    """f32 results against the float64 answer (fixture keys 'f64/...'), per tensor:
+
+        err(got, f64) <= max(floor, factor * err(reference f32, f64))
+
+    i.e. well-conditioned tensors are held to the floor (1e-4 on a gradient's norm), and a tensor whose
+    value is a near-cancelling sum (noise-strength gradients, R1 bias gradients through the minibatch-std
+    second derivative: the reference's own f32 result is off by percent there) to a multiple of the
+    reference's own f32 deviation.  Returns ({group: (worst norm err, worst sample err, worst reference
+    norm err, worst ratio to the bound, its tensor)}, sorted ratios); raises on the first violation
+    (after computing everything) when `check`."""
+    truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
+    kw, kg = _keys(truth, groups), _keys(got, groups)
+    _one_sided_zero(got, truth, kg, kw)
+    worst, ratios, fails = {}, [], []
+    for k in sorted(set(kw) & set(kg)):
+        gn, gs = _tensor_errs(got, truth, k)
+        rn, rs_ = _tensor_errs(fix, truth, k)
+        floor = floors['grad' if k.startswith('grad/') else 'param']
+        bn, bs = max(floor[0], factor * rn), max(floor[1], factor * rs_)
+        g = 'grad/' + k.split('/')[1] if k.startswith('grad/') else k.split('/')[0]
+        w = worst.get(g, (0.0, 0.0, 0.0, 0.0, ''))
+        ratio = max(gn / bn, gs / bs)
+        ratios.append(ratio)
+        worst[g] = (max(w[0], gn), max(w[1], gs), max(w[2], rn), max(w[3], ratio), k if ratio > w[3] else w[4])
+        if gn > bn:
+            fails.append(f'{k}: norm err vs f64 {gn:.3g} > max({floor[0]}, {factor} x reference f32 err {rn:.3g})')
+        if gs > bs:
+            fails.append(f'{k}: sampled-entry err vs f64 {gs:.3g} > max({floor[1]}, {factor} x reference {rs_:.3g})')
+    if check:
+        assert not fails, f'{len(fails)} tensors out of bounds; first: {fails[0]}'
+    return worst, sorted(ratios)
+
+
+def judge_stats_f32(got, fix, floor=1e-4, factor=4.0, check=True):
+    names, ref_vals = fixture_stats(fix)
+    assert [n for n, _ in got] == names, 'reported statistics differ in name or order'
+    worst = 0.0
+    for j, ((n, v), r) in enumerate(zip(got, ref_vals)):
+        if 'signs' in n:
+            continue
+        t = np.asarray(fix[f'f64/stats/{j}'], np.float64)
+        den = max(np.linalg.norm(t), 1e-30)
+        e = np.linalg.norm(np.asarray(v, np.float64) - t) / den
+        er = np.linalg.norm(np.asarray(r, np.float64) - t) / den
+        worst = max(worst, e)
+        assert not check or e <= max(floor, factor * er), f'stat {n}: rel err vs f64 {e:.3g} (reference f32 {er:.3g})'
+    return worst
+
+
+def judge_pl_mean(got, fix, floor=1e-4, factor=4.0, check=True):
+    t = float(fix['f64/pl_mean'])
+    e = abs(float(got['pl_mean']) - t) / abs(t)
+    er = abs(float(fix['pl_mean']) - t) / abs(t)
+    assert not check or e <= max(floor, factor * er), f'pl_mean rel err vs f64 {e:.3g} (reference f32 {er:.3g})'
+    return e
+
+
+def _keys(d, groups):
+    return sorted(k[:-5] for k in d if k.endswith('/norm') and k.startswith(tuple(groups)))
+
+
+def _one_sided_zero(got, want, keys_g, keys_w):
+    """A parameter whose gradient is structurally zero (e.g. a toRGB bias in the path-length pass) may be
+    materialised as zeros on one side and absent on the other -- the reference's own CUDA and CPU paths
+    differ there.  Anything else must be present on both sides."""
+    for k in sorted(set(keys_g) ^ set(keys_w)):
+        d = got if k in keys_g else want
+        assert float(d[k + '/norm']) == 0.0, f'{k} present on one side only with norm {float(d[k + "/norm"]):.3g}'
+
+
+def compare_stats(got, want_names, want_vals, tol):
+    assert [n for n, _ in got] == list(want_names), 'reported statistics differ in name or order'
+    worst = 0.0
+    for (n, v), w in zip(got, want_vals):
+        if 'signs' in n:
+            continue
+        v, w = np.asarray(v, np.float64), np.asarray(w, np.float64)
+        e = np.linalg.norm(v - w) / max(np.linalg.norm(w), 1e-30)
+        worst = max(worst, e)
+        assert e <= tol, f'stat {n}: rel err {e:.3g} > {tol}'
+    return worst
+
+
+def fixture_stats(z):
+    names, vals = [], []
+    for ph in PHASES:
+        nm = [str(s) for s in z[f'stats_names/{ph}']]
+        names += nm
+        vals += [z[f'stats/{ph}/{j}'] for j in range(len(nm))]
+    return names, vals
+
+
+def load_fixture(npz):
+    """-> (cfg, inputs, tape, fixture dict with the summaries unpacked)"""
+    z = unpack(npz)
+    cfg = ast.literal_eval(str(z['cfg']))
+    return cfg, make_inputs(cfg, cfg['input_seed']), Tape.from_npz(z, 'tape'), z
+
+
+def compare_flat(got, want, groups):
+    """Mixed-precision measure, per group (a phase's gradients, or a network's parameters):
+      * the relative L2 error of the vector of tensor norms;
+      * the relative L2 error of the group's whole flat vector, estimated from the sampled entries:
+        sqrt(sum_i numel_i * mean_s (a_s - b_s)^2) / sqrt(sum_i |b_i|^2) -- the measure of a flat
+        concatenated gradient (the vector the all-reduce exchanges), weighting tensors by their size."""
+    res = {}
+    for g in groups:
+        kw, kg = _keys(want, [g + '/']), _keys(got, [g + '/'])
+        _one_sided_zero(got, want, kg, kw)
+        keys = sorted(set(kw) & set(kg))
+        assert keys, g
+        na = np.array([float(got[k + '/norm']) for k in keys])
+        nb = np.array([float(want[k + '/norm']) for k in keys])
+        err2 = sum(float(want[k + '/numel']) * float(np.mean((np.asarray(got[k + '/samples'], np.float64) -
+                                                               np.asarray(want[k + '/samples'], np.float64)) ** 2))
+                   for k in keys)
+        res[g] = (float(np.linalg.norm(na - nb) / np.linalg.norm(nb)), float(np.sqrt(err2) / np.linalg.norm(nb)))
+    return res
+
+
+def save_summary(tag, got):
+    """Keep the product's summaries next to the measured errors (gpurun_out/summ_<tag>.npz)."""
+    import os
+    from golden_init import pack
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'gpurun_out')
+    os.makedirs(d, exist_ok=True)
+    np.savez_compressed(os.path.join(d, f'summ_{tag}.npz'), **pack({k: v for k, v in got.items()}))
+
+
+def record(tag, data):
+    """Append measured errors to gpurun_out/config_parity.jsonl (evidence for the tolerances)."""
+    import json
+    import os
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'gpurun_out')
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, 'config_parity.jsonl'), 'a') as f:
+        f.write(json.dumps({'tag': tag, **{k: v for k, v in data.items()}}, default=str) + '\n')

@@ -3,8 +3,8 @@ on CPU in the build container.  Test infrastructure only; never imported by the 
 
 Run (from the repo root, build container only -- /root/reference does not exist on the GPU box):
 
-    PYTHONDONTWRITEBYTECODE=1 PYTHONPATH=/root/reference/src/models/stylegan3:tests/golden \
-        python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 PYTHONPATH=/root/reference/src/models/stylegan3:tests/golden:tests:. \
+        python tests/golden/make_golden.py [ops] [nets] [c1] [c2] [c4] [c5]
 
 Harness shims; the reference tree itself is not modified:
   * ``openpyxl`` is stubbed (imported by genlib/utils/util_general.py:8, unused on this path);
@@ -45,6 +45,7 @@ from training import networks_stylegan2 as net  # noqa: E402
 from training import augment_mi  # noqa: E402
 from training import loss as loss_mod  # noqa: E402
 from rngtape import Tape  # noqa: E402
+from golden_init import init_state, summarize, pack  # noqa: E402
 
 conv2d_gradfix.enabled = True
 grid_sample_gradfix.enabled = True
@@ -357,13 +358,128 @@ def gen_network(c_dim, img_channels, tag):
     np.savez_compressed(os.path.join(OUT, f'train_{tag}.npz'), **d)
 
 
+# ---------------------------------------------------------------------------- configuration-width iterations
+# One full iteration at each BASELINE.json configuration's real width, through the REFERENCE (fp32 CPU,
+# as its CPU path runs) and through the oracle in float64 (the rounding-free answer both fp32 results
+# are judged against).  Full-width networks are too large to commit, so the state is derived from the
+# parameter names (golden_init.init_state), the inputs from a seed (config_parity.make_inputs), the RNG
+# tape is stored as its seed, and the results as norms + sampled entries (golden_init.summarize).
+CONFIGS = {
+    # configs[0]: claro_stylegan2-ada.yaml / the Claro job at 64^2 (cbase 16384, map 8, c_dim 2, batch 8)
+    'c1': dict(z_dim=512, w_dim=512, img_resolution=64, channel_base=16384, channel_max=512, map_depth=8, mbstd=4,
+               batch=8, c_dim=2, img_channels=1),
+    # configs[1..2]: the 256^2 1-ch Claro network (batch 4 of the per-GPU 32: CPU time)
+    'c2': dict(z_dim=512, w_dim=512, img_resolution=256, channel_base=16384, channel_max=512, map_depth=8, mbstd=4,
+               batch=4, c_dim=2, img_channels=1),
+    # configs[3]: 512^2 3-ch, cbase 32768 (batch 2 of 16)
+    'c4': dict(z_dim=512, w_dim=512, img_resolution=512, channel_base=32768, channel_max=512, map_depth=8, mbstd=4,
+               batch=2, c_dim=0, img_channels=3),
+    # configs[4]: 1024^2 3-ch, cbase 32768 (batch 2 of 8)
+    'c5': dict(z_dim=512, w_dim=512, img_resolution=1024, channel_base=32768, channel_max=512, map_depth=8, mbstd=4,
+               batch=2, c_dim=0, img_channels=3),
+}
+
+
+def gen_config_iteration(tag, cfg, input_seed=31, tape_seed=13, aug_p=0.3):
+    import config_parity as cp
+    d = {}
+    torch.manual_seed(0)
+    c_dim, img_channels = cfg['c_dim'], cfg['img_channels']
+    G = net.Generator(z_dim=cfg['z_dim'], c_dim=c_dim, w_dim=cfg['w_dim'], img_resolution=cfg['img_resolution'],
+                      img_channels=img_channels, channel_base=cfg['channel_base'], channel_max=cfg['channel_max'],
+                      num_fp16_res=4, conv_clamp=256, fused_modconv_default='inference_only',
+                      mapping_kwargs=dict(num_layers=cfg['map_depth'])).train().requires_grad_(False)
+    D = net.Discriminator(c_dim=c_dim, img_resolution=cfg['img_resolution'], img_channels=img_channels,
+                          channel_base=cfg['channel_base'], channel_max=cfg['channel_max'], num_fp16_res=4,
+                          conv_clamp=256, epilogue_kwargs=dict(mbstd_group_size=cfg['mbstd'])).train().requires_grad_(False)
+    init_state(G, seed=1)
+    init_state(D, seed=2)
+    G_ema = copy.deepcopy(G).eval()
+    B = cfg['batch']
+    inp = cp.make_inputs(cfg, input_seed)
+    if cfg['img_resolution'] <= 64:
+        with torch.no_grad():
+            img = G_ema(T(inp['z']), T(inp['c']), noise_mode='const')
+            d['ema_img_const'] = npy(img)
+            d['D_logits_ema'] = npy(D(img, T(inp['c'])))
+    aug = augment_mi.AugmentPipe(run_dir=None, batch_size=B, **CLARO_AUG).train().requires_grad_(False)
+    aug.p.copy_(torch.as_tensor(aug_p))
+    stats = []
+
+    def rep(name, value):
+        stats.append((name, npy(torch.as_tensor(value))))
+        return value
+
+    orig_report = training_stats.report
+    loss_mod.training_stats.report = rep
+    loss = loss_mod.StyleGAN2Loss(device=torch.device('cpu'), G=G, D=D, augment_pipe=aug, r1_gamma=0.4096,
+                                  style_mixing_prob=0.9, pl_weight=2, pl_no_weight_grad=True)
+    phases = []
+    for name, module, reg_interval in [('G', G, 4), ('D', D, 16)]:
+        mb_ratio = reg_interval / (reg_interval + 1)
+        opt = torch.optim.Adam(module.parameters(), lr=0.0025 * mb_ratio, betas=[b ** mb_ratio for b in [0, 0.99]],
+                               eps=1e-8)
+        phases += [dict(name=name + 'main', module=module, opt=opt, interval=1),
+                   dict(name=name + 'reg', module=module, opt=opt, interval=reg_interval)]
+    gen_z, gen_c = inp['gen_z'], inp['gen_c']
+    cur_nimg = 1000
+    tape = Tape(seed=tape_seed)
+    with tape.record():
+        for pi, ph in enumerate(phases):
+            ph['opt'].zero_grad(set_to_none=True)
+            ph['module'].requires_grad_(True)
+            n0 = len(stats)
+            loss.accumulate_gradients(phase=ph['name'], real_img=T(inp['real']), real_c=T(inp['c']),
+                                      gen_z=T(gen_z[pi]), gen_c=T(gen_c[pi]), gain=ph['interval'], cur_nimg=cur_nimg)
+            ph['module'].requires_grad_(False)
+            named = [(n_, p) for n_, p in ph['module'].named_parameters() if p.grad is not None]
+            flat = torch.cat([p.grad.flatten() for _, p in named])
+            torch.nan_to_num(flat, nan=0, posinf=1e5, neginf=-1e5, out=flat)
+            for (_, p), g in zip(named, flat.split([p.numel() for _, p in named])):
+                p.grad = g.reshape(p.shape)
+            d.update(summarize({n_: p.grad for n_, p in named}, f'grad/{ph["name"]}'))
+            ph['opt'].step()
+            d[f'stats_names/{ph["name"]}'] = np.array([s_[0] for s_ in stats[n0:]])
+            for j, s_ in enumerate(stats[n0:]):
+                d[f'stats/{ph["name"]}/{j}'] = s_[1]
+            if ph['name'] == 'Greg':
+                d['pl_mean'] = npy(loss.pl_mean)
+    loss_mod.training_stats.report = orig_report
+    ema_beta = 0.5 ** (B / max(min(10 * 1000, cur_nimg * 0.05), 1e-8))
+    with torch.no_grad():
+        for p_ema, p in zip(G_ema.parameters(), G.parameters()):
+            p_ema.copy_(p.lerp(p_ema, ema_beta))
+    d.update(summarize(dict(G.named_parameters()), 'G1'))
+    d.update(summarize(dict(D.named_parameters()), 'D1'))
+    d.update(summarize(dict(G_ema.named_parameters()), 'Gema1'))
+    d.update(tape.to_compact_npz_dict('tape'))
+    # the float64 oracle on the same state, inputs and draws
+    replay = Tape.from_npz(tape.to_compact_npz_dict('t'), 't')
+    f64, f64_stats = cp.run_oracle_f64(cfg, inp, replay, aug_p)
+    assert replay.pos == len(replay.entries)
+    for k, v in f64.items():
+        d[f'f64/{k}'] = v
+    for j, (n_, v) in enumerate(f64_stats):
+        d[f'f64/stats/{j}'] = np.asarray(v, np.float64)
+    d['cfg'] = np.array(repr(dict(cfg, aug_p=aug_p, init_seeds=(1, 2), input_seed=input_seed)))
+    np.savez_compressed(os.path.join(OUT, f'train_{tag}.npz'), **pack(d))
+    print(tag, 'written', flush=True)
+
+
 if __name__ == '__main__':
+    which = sys.argv[1:] or ['ops', 'nets'] + list(CONFIGS)
+    for tag in CONFIGS:
+        if tag in which:
+            gen_config_iteration(tag, CONFIGS[tag])
+    if 'ops' not in which:
+        sys.exit(0)
     gen_upfirdn2d()
     gen_bias_act()
     gen_conv()
     gen_augment()
-    gen_network(c_dim=2, img_channels=1, tag='claro')
-    gen_network(c_dim=0, img_channels=2, tag='pelvis')
+    if 'nets' in which:
+        gen_network(c_dim=2, img_channels=1, tag='claro')
+        gen_network(c_dim=0, img_channels=2, tag='pelvis')
     for f in sorted(os.listdir(OUT)):
         if f.endswith('.npz'):
             print(f, os.path.getsize(os.path.join(OUT, f)))

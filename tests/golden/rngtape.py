@@ -27,8 +27,10 @@ def _shape(args, kwargs):
 
 class Tape:
     def __init__(self, seed=1234, entries=None):
+        self.seed = seed
         self.rs = np.random.RandomState(seed)
         self.entries = [] if entries is None else list(entries)
+        self.bounds = []      # (lo, hi) of every randint draw, in order (for the compact form)
         self.pos = 0
         self.mode = None
 
@@ -40,8 +42,26 @@ class Tape:
             d[f'{prefix}_{i}_val'] = arr
         return d
 
+    def to_compact_npz_dict(self, prefix='tape'):
+        """Seed + the (kind, shape, bounds) sequence only: the values are regenerated from the seed on
+        load (the recording draws them from one numpy RandomState in this order)."""
+        kinds = np.array([k for k, _ in self.entries])
+        shapes = np.array(repr([tuple(a.shape) for _, a in self.entries]))
+        return {f'{prefix}_seed': np.array(self.seed), f'{prefix}_kinds': kinds, f'{prefix}_shapes': shapes,
+                f'{prefix}_bounds': np.array(self.bounds, dtype=np.int64).reshape(-1, 2)}
+
     @classmethod
     def from_npz(cls, z, prefix='tape'):
+        if f'{prefix}_seed' in z:
+            import ast
+            t = cls(seed=int(z[f'{prefix}_seed']))
+            t.mode = 'record'
+            bounds = iter(z[f'{prefix}_bounds'].tolist())
+            for kind, shape in zip(z[f'{prefix}_kinds'].tolist(), ast.literal_eval(str(z[f'{prefix}_shapes']))):
+                lo, hi = next(bounds) if kind == 'randint' else (None, None)
+                t._draw(str(kind), tuple(shape), lo, hi)
+            t.mode = None
+            return t
         n = int(z[f'{prefix}_n'])
         ents = [(str(z[f'{prefix}_{i}_kind']), z[f'{prefix}_{i}_val']) for i in range(n)]
         return cls(entries=ents)
@@ -55,6 +75,7 @@ class Tape:
                 arr = self.rs.random_sample(shape).astype(np.float32)
             else:
                 arr = np.array(self.rs.randint(lo, hi), dtype=np.int64)
+                self.bounds.append((lo, hi))
             self.entries.append((kind, arr))
             return arr
         kind0, arr = self.entries[self.pos]
@@ -67,6 +88,8 @@ class Tape:
     def _mk(self, kind, shape, dtype=None, device=None):
         arr = self._draw(kind, shape)
         t = torch.from_numpy(np.array(arr))
+        if dtype is None and t.is_floating_point():
+            dtype = torch.get_default_dtype()      # as torch.randn / torch.rand without a dtype
         if dtype is not None:
             t = t.to(dtype)
         if device is not None:

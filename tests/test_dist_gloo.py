@@ -1,4 +1,4 @@
-"""Data-parallel gradient exchange (training/trainer.py GradReducer) with world_size 2 on CPU/gloo.
+"""Data-parallel gradient exchange (training/trainer.py GradExchange) with world_size 2 on CPU/gloo.
 
 The product's trainer is driven with the CPU oracle networks (the trainer is device-agnostic host
 logic; the HIP ops need a GPU).  Checked: bucketed, backward-overlapped all_reduce gives exactly
@@ -86,7 +86,7 @@ def _worker(rank, world, port, paths, result_q):
             worst = max(worst, float((reduced[k] - plain[k]).abs().max() / (plain[k].abs().max() + 1e-12)))
         misc.check_ddp_consistency(G, ignore_regex=r'.*\.[^.]+_(avg|ema)')
         misc.check_ddp_consistency(D)
-        nbuckets = len(tr.phases[0].reducer._buckets([p for p in G.parameters()]))
+        nbuckets = len(tr.phases[0].exchange.buckets)
         result_q.put((rank, worst, len(local), nbuckets))
     finally:
         dist.destroy_process_group()

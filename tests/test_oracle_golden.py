@@ -184,3 +184,18 @@ def test_train_iteration(tag):
     compare_state(G, z, 'G1', 1e-4)
     compare_state(D, z, 'D1', 1e-4)
     compare_state(G_ema, z, 'Gema1', 1e-4)
+
+
+# ------------------------------------------------------------------------------- BASELINE configs[0] width
+def test_train_iteration_c1_width():
+    """The oracle's full iteration at the Claro job's real widths (64^2, cbase 16384 -> 512 channels at
+    4^2-32^2, map depth 8, z/w 512, c_dim 2, batch 8) against the reference-generated fixture: per tensor
+    against the float64 answer, as close as the reference's own f32 result (config_parity.judge_f32)."""
+    from config_parity import load_fixture, run_oracle, judge_f32, judge_stats_f32, judge_pl_mean
+    cfg, inp, tape, fix = load_fixture(load('train_c1.npz'))
+    got, stats = run_oracle(cfg, inp, tape)
+    assert tape.pos == len(tape.entries)
+    worst = judge_f32(got, fix)
+    judge_stats_f32(stats, fix)
+    judge_pl_mean(got, fix)
+    print({k: tuple(f'{x:.2g}' for x in v[:4]) for k, v in worst.items()})
