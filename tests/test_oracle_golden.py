@@ -195,7 +195,7 @@ def test_train_iteration_c1_width():
     cfg, inp, tape, fix = load_fixture(load('train_c1.npz'))
     got, stats = run_oracle(cfg, inp, tape)
     assert tape.pos == len(tape.entries)
-    worst = judge_f32(got, fix)
+    worst, _ = judge_f32(got, fix)
     judge_stats_f32(stats, fix)
     judge_pl_mean(got, fix)
     print({k: tuple(f'{x:.2g}' for x in v[:4]) for k, v in worst.items()})
