@@ -183,57 +183,90 @@ def _tensor_errs(a, b, k):
 F32_FLOORS = {'grad': (1e-4, 1e-3), 'param': (1e-3, 1e-1)}
 
 
-def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True):
-    """f32 results against the float64 answer (fixture keys 'f64/...'), per tensor:
+def _group(k):
+    return 'grad/' + k.split('/')[1] if k.startswith('grad/') else k.split('/')[0]
 
-        err(got, f64) <= max(floor, factor * err(reference f32, f64))
 
-    i.e. well-conditioned tensors are held to the floor (1e-4 on a gradient's norm), and a tensor whose
-    value is a near-cancelling sum (noise-strength gradients, R1 bias gradients through the minibatch-std
-    second derivative: the reference's own f32 result is off by percent there) to a multiple of the
-    reference's own f32 deviation.  Returns ({group: (worst norm err, worst sample err, worst reference
-    norm err, worst ratio to the bound, its tensor)}, sorted ratios); raises on the first violation
-    (after computing everything) when `check`."""
+def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
+              groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True):
+    """f32 results against the float64 answer (fixture keys 'f64/...'), per tensor k of group g (a phase's
+    gradients, or a network after the step):
+
+        err(got_k, f64) <= max(floor, factor * err(ref_k, f64), group_factor * max_{j in g} err(ref_j, f64))
+
+    Well-conditioned tensors are held to the floor (1e-4 on a gradient's norm).  Near-cancelling sums are
+    not: the reference's own f32 result is off by up to percents there (noise-strength gradients, R1 bias
+    gradients through the minibatch-std second derivative, and -- through lrelu masks that rounding flips
+    -- the path-length pass: the oracle's f32 J^T y is 7e-4 from float64 at C2, tools/f32_diag.py).  Which
+    tensor of a phase draws the short straw is chance, so the bound also admits the reference's worst
+    error in the same phase.  Returns ({group: (worst norm err, worst sample err, worst reference norm
+    err, worst ratio to the bound, its tensor)}, sorted ratios); raises after computing everything when
+    `check` and any tensor is out of bounds."""
     truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
     kw, kg = _keys(truth, groups), _keys(got, groups)
     _one_sided_zero(got, truth, kg, kw)
+    keys = sorted(set(kw) & set(kg))
+    errs = {k: (_tensor_errs(got, truth, k), _tensor_errs(fix, truth, k)) for k in keys}
+    gmax = {}
+    for k, (_, (rn, rs_)) in errs.items():
+        m = gmax.get(_group(k), (0.0, 0.0))
+        gmax[_group(k)] = (max(m[0], rn), max(m[1], rs_))
     worst, ratios, fails = {}, [], []
-    for k in sorted(set(kw) & set(kg)):
-        gn, gs = _tensor_errs(got, truth, k)
-        rn, rs_ = _tensor_errs(fix, truth, k)
+    for k in keys:
+        (gn, gs), (rn, rs_) = errs[k]
+        g = _group(k)
         floor = floors['grad' if k.startswith('grad/') else 'param']
-        bn, bs = max(floor[0], factor * rn), max(floor[1], factor * rs_)
-        g = 'grad/' + k.split('/')[1] if k.startswith('grad/') else k.split('/')[0]
+        bn = max(floor[0], factor * rn, group_factor * gmax[g][0])
+        bs = max(floor[1], factor * rs_, group_factor * gmax[g][1])
         w = worst.get(g, (0.0, 0.0, 0.0, 0.0, ''))
         ratio = max(gn / bn, gs / bs)
         ratios.append(ratio)
         worst[g] = (max(w[0], gn), max(w[1], gs), max(w[2], rn), max(w[3], ratio), k if ratio > w[3] else w[4])
         if gn > bn:
-            fails.append(f'{k}: norm err vs f64 {gn:.3g} > max({floor[0]}, {factor} x reference f32 err {rn:.3g})')
+            fails.append(f'{k}: norm err vs f64 {gn:.3g} > bound {bn:.3g} (reference f32 {rn:.3g}, phase max {gmax[g][0]:.3g})')
         if gs > bs:
-            fails.append(f'{k}: sampled-entry err vs f64 {gs:.3g} > max({floor[1]}, {factor} x reference {rs_:.3g})')
+            fails.append(f'{k}: sampled-entry err vs f64 {gs:.3g} > bound {bs:.3g} (reference {rs_:.3g})')
     if check:
         assert not fails, f'{len(fails)} tensors out of bounds; first: {fails[0]}'
     return worst, sorted(ratios)
 
 
-def judge_stats_f32(got, fix, floor=1e-4, factor=4.0, check=True):
+def judge_flat(got_flat, ref_flat, floor, factor=3.0):
+    """Per group: the estimated whole-vector error vs f64 (compare_flat) within max(floor, factor x the
+    reference f32's)."""
+    for g, (en, es) in got_flat.items():
+        t = max(floor, factor * max(ref_flat[g]))
+        assert en <= t and es <= t, f'{g}: norm-vector err {en:.3g}, flat err {es:.3g} (bound {t:.3g})'
+
+
+# The regulariser statistics inherit the conditioning of the gradients they are built from: J^T y of the
+# path-length pass carries ~7e-4 of inherent f32 error (the oracle's own f32 vs float64 at C2), and the
+# penalty squares (|J^T y| - a).
+REG_STATS = ('Loss/pl_penalty', 'Loss/G/reg', 'Loss/r1_penalty', 'Loss/D/reg')
+
+
+def judge_stats_f32(got, fix, floor=1e-4, reg_floor=3e-3, factor=4.0, group_factor=3.0, check=True):
+    """Reported loss statistics against f64: each within max(floor, factor x the reference f32's error on it,
+    group_factor x the reference's worst statistic error) -- the same chance argument as judge_f32."""
     names, ref_vals = fixture_stats(fix)
     assert [n for n, _ in got] == names, 'reported statistics differ in name or order'
-    worst = 0.0
+    rows = []
     for j, ((n, v), r) in enumerate(zip(got, ref_vals)):
         if 'signs' in n:
             continue
         t = np.asarray(fix[f'f64/stats/{j}'], np.float64)
         den = max(np.linalg.norm(t), 1e-30)
-        e = np.linalg.norm(np.asarray(v, np.float64) - t) / den
-        er = np.linalg.norm(np.asarray(r, np.float64) - t) / den
-        worst = max(worst, e)
-        assert not check or e <= max(floor, factor * er), f'stat {n}: rel err vs f64 {e:.3g} (reference f32 {er:.3g})'
-    return worst
+        rows.append((n, np.linalg.norm(np.asarray(v, np.float64) - t) / den,
+                     np.linalg.norm(np.asarray(r, np.float64) - t) / den))
+    gmax = max(er for _, _, er in rows)
+    for n, e, er in rows:
+        fl = reg_floor if n in REG_STATS else floor
+        assert not check or e <= max(fl, factor * er, group_factor * gmax), \
+            f'stat {n}: rel err vs f64 {e:.3g} (reference f32 {er:.3g}, worst reference stat {gmax:.3g})'
+    return max(e for _, e, _ in rows)
 
 
-def judge_pl_mean(got, fix, floor=1e-4, factor=4.0, check=True):
+def judge_pl_mean(got, fix, floor=3e-3, factor=4.0, check=True):
     t = float(fix['f64/pl_mean'])
     e = abs(float(got['pl_mean']) - t) / abs(t)
     er = abs(float(fix['pl_mean']) - t) / abs(t)

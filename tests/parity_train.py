@@ -2,8 +2,9 @@
 golden vectors, on identical weights, inputs and RNG draws (tests/golden/rngtape.py).
 
 Test infrastructure (used by tests/test_train_gpu.py and __graft_entry__.smoke()).
-Tolerances: fp32 path (num_fp16_res=0) 2e-3 relative L2 on every gradient / parameter, 1e-3 on
-losses; mixed precision (float16 at the top resolutions, the reference's GPU default) 6e-2.
+Tolerances: fp32 path (num_fp16_res=0) 1e-4 relative L2 on every gradient / parameter and on
+losses (measured worst 3.8e-6); mixed precision (float16 at the top resolutions, the reference's GPU default) 3e-2
+on each phase's flat gradient and each network's parameter vector.
 """
 import ast
 import copy
@@ -113,7 +114,7 @@ def run_train_parity(golden='train_claro.npz', fp16=False):
     """Returns the worst relative error; raises AssertionError beyond tolerance."""
     z = load(golden)
     dev = torch.device('cuda', 0)
-    tol = 6e-2 if fp16 else 2e-3
+    tol = 3e-2 if fp16 else 1e-4
     Gp, Dp, Ep, lp, gp, sp = run_product_iteration(z, dev, fp16)
     Go, Do, Eo, lo, go, so = run_oracle_iteration(z)
     worst = 0.0

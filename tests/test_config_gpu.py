@@ -9,8 +9,10 @@ oracle's float64 evaluation of the same state, inputs and random draws):
   configs[4]    C5  train_c5.npz  1024^2 3-ch, cbase 32768, ADA, batch 2 of 8
 plus full-batch runs of C4 (bs16, fp16) and C5 (bs8, bf16): every statistic / norm finite.
 
-f32 product (num_fp16_res=0: the reference's CPU arithmetic): per tensor, error against the float64
-answer <= max(1e-4, 4 x the reference's own f32 error) (config_parity.judge_f32).
+f32 product (num_fp16_res=0: the reference's CPU arithmetic), against the float64 answer: per tensor
+within max(1e-4, 4 x the reference's own f32 error on it, 3 x the reference's worst error in the same
+phase) (config_parity.judge_f32), and per phase / network the whole-vector error within 3 x the
+reference's (floor 1e-4 for gradients, 1e-5 for parameters).
 16-bit product (num_fp16_res=4, the reference's GPU default, float16 or bfloat16 with f32 accumulate):
 per phase / network, the relative error of the flat vector against the float64 answer
 (config_parity.compare_flat), tolerances set from the measured errors (profiles/r02_config_parity.jsonl).
@@ -32,7 +34,7 @@ GROUPS = ['grad/Gmain', 'grad/Greg', 'grad/Dmain', 'grad/Dreg', 'G1', 'D1', 'Gem
 # (profiles/r02_config_parity.jsonl) with ~1.5x margin.
 FLOOR16 = {
     'fp16': {'grad/Gmain': 0.03, 'grad/Greg': 0.08, 'grad/Dmain': 0.05, 'grad/Dreg': 0.17, 'param': 1e-3},
-    'bf16': {'grad/Gmain': 0.06, 'grad/Greg': 0.08, 'grad/Dmain': 0.06, 'grad/Dreg': 0.15, 'param': 2e-3},
+    'bf16': {'grad/Gmain': 0.06, 'grad/Greg': 0.2, 'grad/Dmain': 0.06, 'grad/Dreg': 0.15, 'param': 2e-3},
 }
 
 
@@ -66,8 +68,8 @@ def test_f32_iteration_vs_reference(tag):
     cp.judge_f32(got, fix, factor=F32_FACTOR)
     cp.judge_stats_f32(stats, fix)
     cp.judge_pl_mean(got, fix)
-    for g in ('G1', 'D1', 'Gema1'):       # whole networks after the step
-        assert max(flat[g]) <= max(1e-5, 4 * max(ref_flat[g])), (g, flat[g], ref_flat[g])
+    cp.judge_flat({g: v for g, v in flat.items() if g.startswith('grad/')}, ref_flat, floor=1e-4)
+    cp.judge_flat({g: v for g, v in flat.items() if not g.startswith('grad/')}, ref_flat, floor=1e-5)
 
 
 @pytest.mark.timeout(240)

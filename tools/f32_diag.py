@@ -101,3 +101,14 @@ from torch_utils.ops import conv2d_gradfix  # noqa: E402
 with conv2d_gradfix.no_weight_gradients():
     g, = torch.autograd.grad((img * y).sum(), [ws], create_graph=True, retain_graph=True)
 print('J^T y create_graph + no_weight_gradients', rel(g, outs[1][0]))
+
+# the oracle itself in f32 (the reference's CPU arithmetic) against f64: the conditioning of J^T y
+O.REAL = torch.float32
+Go32, _ = cp._nets(O, cfg, 4)
+ws = ws_o.detach().float().clone().requires_grad_(True)
+img32 = Go32.synthesis(ws, noise_mode='const')
+y32 = torch.from_numpy(np.random.RandomState(3).standard_normal(tuple(img32.shape))).float()
+g32, = torch.autograd.grad((img32 * y32).sum(), [ws])
+print('oracle f32 J^T y vs f64', rel(g32, outs[1][0]))
+print('   per ws index', ' '.join(f'{rel(g32[:, i], outs[1][0][:, i]):.1e}' for i in range(g32.shape[1])))
+print('product vs oracle f32 J^T y', rel(outs[0][0], g32))
