@@ -158,8 +158,8 @@ def _measured_traffic(key):
 
 
 def roofline(device, res, cbase, dtype):
-    """Roofline of the dominant kernel, the LDS-halo MFMA 3x3 conv (sg2_conv3x3 = conv3x3_halo_kernel,
-    ~the largest kernel family of the step), on the 256^2 synthesis layer the north star names.  Its
+    """Roofline of the dominant kernel, the LDS-halo MFMA 3x3 conv (sg2_conv3x3; at C = 64 its persistent
+    form conv3x3_c64p_kernel), on the 256^2 synthesis layer the north star names.  Its
     arithmetic intensity (~286 FLOP/B at C = 64, 16-bit) is below the MI355X ridge (2500 TFLOP/s / 8 TB/s
     = 312 FLOP/B), so the bound is HBM: achieved = algorithmic bytes / measured launch time.  The MFMA
     view of the same launch and of the MFMA-bound 32^2 / C = 512 layer are reported beside it."""
@@ -170,7 +170,8 @@ def roofline(device, res, cbase, dtype):
     key = f'sg2_conv3x3 fused {res}^2 C={C} N=32 {str(dtype).split(".")[-1]}'
     gbps = byts / (ms * 1e-3) / 1e9
     tflops = flops / (ms * 1e-3) / 1e12
-    out = {'kernel': f'conv3x3_halo_kernel ({key}: modulation + demod/noise/bias/lrelu/clamp epilogue)'}
+    kname = 'conv3x3_c64p_kernel (persistent, weights in LDS)' if C == 64 else 'conv3x3_halo_kernel'
+    out = {'kernel': f'{kname} ({key}: modulation + demod/noise/bias/lrelu/clamp epilogue)'}
     if ai < ridge:
         out.update({'bound': 'hbm', 'achieved': round(gbps, 1), 'peak': HBM_PEAK, 'unit': 'GB/s',
                     'frac': round(gbps / HBM_PEAK, 4)})

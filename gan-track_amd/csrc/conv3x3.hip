@@ -143,9 +143,9 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
         for (int i = 0; i < NH; ++i) {
             if (h_dst[i] < 0) continue;
             vec8 v = rh[i];
-            if (SCALE_IN) {
+            if (SCALE_IN) {   // x * s.to(x.dtype) (networks_stylegan2.py:69): s rounded first, one rounding after
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = (T)((float)v[j] * scl[j]);
+                for (int j = 0; j < 8; ++j) v[j] = (T)((float)v[j] * (float)(T)scl[j]);
             }
             *(vec8*)(hb + h_dst[i]) = v;
         }
@@ -306,6 +306,282 @@ int launch3(const Conv3Args& a, hipStream_t s) {
     return launch_status("sg2_conv3x3");
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Persistent, weights-resident variant for the 64 -> 64 channel layers (the 256^2 layer of the Claro
+// network, 512^2 at cbase 32768; forward and dgrad).  The generic halo kernel above restages the 9 x 64 x 64
+// weights (74 KB) for every 256-pixel tile, and its per-tile prologue (first chunk's loads) and epilogue
+// (noise / demod loads, LDS transpose) are exposed: with Cin = 64 a tile is only two chunks of MFMAs.
+// Here one workgroup of 8 waves per CU keeps all weights in LDS for the whole launch and walks a
+// contiguous run of tiles (neighbouring tiles share halo rows in the same XCD's L2):
+//   * wave w owns pixels 64*(w%4) .. +63 of the 256-pixel tile and output channels 32*(w/4) .. +31
+//     (2 waves per SIMD: one's LDS reads / epilogue overlap the other's MFMAs);
+//   * the tile's two 32-channel chunks live in a double buffer: the next chunk's global loads (the next
+//     tile's first chunk, during the current tile's second) are issued before the current chunk's MFMAs,
+//     one barrier per chunk, no per-tile prologue;
+//   * the epilogue's operands (noise, demod scales, dot source) are loaded before the tile's last chunk of
+//     MFMAs, and the MFMA operands are swapped (weights as A, pixels as B) so a lane's accumulator holds 4
+//     consecutive output channels of one pixel: 8-byte stores straight from registers, no LDS transpose;
+//   * the modulation x * s is applied at the LDS store as a 16-bit multiply by s rounded to the
+//     activation dtype -- the reference's `x * styles.to(x.dtype)` (networks_stylegan2.py:69) bit for bit.
+constexpr int P_TW = 32, P_TH = 8, P_C = 64;
+constexpr int P_HW = P_TW + 2, P_HH = P_TH + 2, P_HP = P_HW * P_HH;      // 34 x 10 halo
+constexpr int P_HALO = P_HP * PX;                                         // elements per halo chunk buffer
+constexpr int P_WCH = 9 * P_C * PX;                                       // elements per weight chunk
+constexpr size_t P_LDS = (size_t)(2 * P_WCH + 2 * P_HALO) * 2;            // 146,560 B
+
+template <typename T, bool SCALE_IN, bool EPI, bool DOT>
+__global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int tiles_total) {
+    constexpr int NT = 512;
+    constexpr int NH = (P_HP * 4 + NT - 1) / NT;         // halo 16-B loads per thread per chunk (3)
+    constexpr int NW = (9 * P_C * 4) / NT;               // weight 16-B loads per thread per chunk (4.5 -> see below)
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    typedef T vec4 __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    T* wlds = (T*)smem_raw;                              // [2 chunks][9][64][PX]
+    T* hlds = wlds + 2 * P_WCH;                          // [2 chunks][HP][PX]
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int pg = wave & 3, half = wave >> 2;           // pixel group, channel half
+    const int tiles_x = a.W / P_TW, tiles_y = a.H / P_TH;
+    const int per_n = tiles_x * tiles_y;
+    const int t_begin = (int)((int64_t)blockIdx.x * tiles_total / gridDim.x);
+    const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles_total / gridDim.x);
+    if (t_begin >= t_end) return;
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(a.x, (int64_t)a.N * a.H * a.W * P_C * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rwb = make_rsrc(a.w, (int64_t)P_C * 9 * P_C * (int64_t)sizeof(T));
+
+    // ---- weights: both chunks, once (2 x 2304 16-B rows over 512 threads) ----
+    for (int idx = tid; idx < 2 * 9 * P_C * 4; idx += NT) {
+        const int c = idx / (9 * P_C * 4), rem = idx - c * 9 * P_C * 4;
+        const int r = rem >> 2, tap = r / P_C, o = r - tap * P_C;
+        const vec8 v = buf_load16<vec8>(rwb, ((o * 9 + tap) * P_C + c * CK + (rem & 3) * 8) * (int)sizeof(T));
+        *(vec8*)(wlds + c * P_WCH + (tap * P_C + o) * PX + (rem & 3) * 8) = v;
+    }
+    (void)NW;
+
+    // ---- halo staging geometry (fixed per thread; the tile origin varies) ----
+    int h_dy[NH], h_dx[NH], h_dst[NH];
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+        const int idx = tid + i * NT, p = idx >> 2, q = idx & 3;
+        h_dy[i] = p / P_HW - 1;
+        h_dx[i] = p % P_HW - 1;
+        h_dst[i] = p < P_HP ? p * PX + q * 8 : -1;
+    }
+    const int hq = (tid & 3) * 8;
+    vec8 rh[NH];
+    vec8 sv8;                                            // the chunk's 8 style scales, rounded to T
+    auto tile_of = [&](int t, int& n, int& ty0, int& tx0) {
+        n = t / per_n;
+        const int tr = t - n * per_n;
+        ty0 = (tr / tiles_x) * P_TH;
+        tx0 = (tr % tiles_x) * P_TW;
+    };
+    auto gload = [&](int t, int c) {
+        int n, ty0, tx0;
+        tile_of(t, n, ty0, tx0);
+#pragma unroll
+        for (int i = 0; i < NH; ++i) {
+            const int iy = ty0 + h_dy[i], ix = tx0 + h_dx[i];
+            const bool ok = h_dst[i] >= 0 && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            rh[i] = buf_load16<vec8>(rxb, ok ? (((n * a.H + iy) * a.W + ix) * P_C + c * CK + hq) * (int)sizeof(T) : -1);
+        }
+        if (SCALE_IN) {
+            const float* sc = a.in_scale + (int64_t)n * P_C + c * CK + hq;
+            const float4 s0 = *(const float4*)sc, s1 = *(const float4*)(sc + 4);
+            sv8 = vec8{(T)s0.x, (T)s0.y, (T)s0.z, (T)s0.w, (T)s1.x, (T)s1.y, (T)s1.z, (T)s1.w};
+        }
+    };
+    auto sstore = [&](int buf) {
+        T* hb = hlds + buf * P_HALO;
+#pragma unroll
+        for (int i = 0; i < NH; ++i) {
+            if (h_dst[i] < 0) continue;
+            vec8 v = rh[i];
+            if (SCALE_IN) {
+                if constexpr (std::is_same<T, f16_t>::value) {
+                    v = v * sv8;                         // v_pk_mul_f16: round(x * round(s)), as the reference
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] = (T)((float)v[j] * (float)sv8[j]);
+                }
+            }
+            *(vec8*)(hb + h_dst[i]) = v;
+        }
+    };
+
+    const int ko = 8 * (lane >> 4);
+    int a_base[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = pg * 64 + i * 16 + (lane & 15);
+        a_base[i] = ((m / P_TW) * P_HW + (m % P_TW)) * PX + ko;
+    }
+    const int b_base = (half * 32 + (lane & 15)) * PX + ko;
+    const int oq = half * 32 + 4 * (lane >> 4);          // channel of acc[.][j][0] is oq + 16 * j
+    float bsc[2][4];                                     // gain * bias (rounded to T first, as the reference)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            bsc[j][r] = (EPI && a.bias) ? (float)(T)a.bias[oq + j * 16 + r] * a.gain : 0.f;
+    const float lr_alpha = (EPI && a.act == 1) ? a.alpha : 1.f;   // lrelu as max(v, alpha v), 0 <= alpha <= 1
+    const float clampv = (EPI && a.clamp >= 0.f) ? a.clamp : __builtin_inff();
+
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    T* y = (T*)a.y;
+    T* yr = (T*)a.y_raw;
+    const int64_t npix = (int64_t)a.N * a.H * a.W;
+    const __amdgpu_buffer_rsrc_t rnz = make_rsrc(a.noise, a.noise ? npix * (int64_t)sizeof(T) : 0);
+    const __amdgpu_buffer_rsrc_t ros = make_rsrc(a.out_scale, a.out_scale ? (int64_t)a.N * P_C * 4 : 0);
+    const __amdgpu_buffer_rsrc_t rds = make_rsrc(a.dot_src, a.dot_src ? npix * P_C * (int64_t)sizeof(T) : 0);
+    gload(t_begin, 0);
+    __syncthreads();                                     // weights in LDS
+    sstore(0);
+    __syncthreads();
+    for (int t = t_begin; t < t_end; ++t) {
+        int n, ty0, tx0;
+        tile_of(t, n, ty0, tx0);
+        T nraw[4];
+        float4 draw[2];
+        vec4 dv[4][2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {                   // chunk c of tile t lives in halo buffer c
+            // no branch around a load (hipcc would drain vmcnt right after it): the last tile's "next
+            // chunk" re-reads the tile itself, and absent epilogue operands read zeros (empty buffers)
+            gload(c == 0 ? t : min(t + 1, t_end - 1), c ^ 1);
+            if (c == 1) {
+                // the epilogue's operands, in flight during the last chunk's MFMAs
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m = pg * 64 + i * 16 + (lane & 15);
+                    const int pix = (n * a.H + ty0 + m / P_TW) * a.W + tx0 + m % P_TW;
+                    if (EPI) nraw[i] = buf_load2<T>(rnz, pix * (int)sizeof(T));
+                    if (DOT) {
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) dv[i][j] = buf_load8<vec4>(rds, (pix * P_C + oq + j * 16) * (int)sizeof(T));
+                    }
+                }
+                if (EPI) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) draw[j] = buf_load16<float4>(ros, (n * P_C + oq + j * 16) * 4);
+                }
+            }
+            const T* hb = hlds + c * P_HALO;
+            const T* wb = wlds + c * P_WCH;
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    const int toff = (ky * P_HW + kx) * PX;
+                    const int tap = ky * 3 + kx;
+                    v8<T> af[4], bfr[2];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) af[i] = *(const v8<T>*)(hb + a_base[i] + toff);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) bfr[j] = *(const v8<T>*)(wb + tap * P_C * PX + j * 16 * PX + b_base);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) acc[i][j] = mma<T>(bfr[j], af[i], acc[i][j]);
+                }
+            }
+            if (c == 1) {
+                // ---- epilogue of tile t from the accumulators: lane = 4 channels x 1 pixel ----
+                // the gain folded in: gain * lrelu(z) = lrelu(gain * z) for gain > 0 (host-checked)
+                float nv[4], dsc[2][4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) nv[i] = EPI ? (float)nraw[i] * (a.noise_gain * a.gain) : 0.f;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const float d4[4] = {draw[j].x, draw[j].y, draw[j].z, draw[j].w};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dsc[j][r] = EPI ? (a.out_scale ? d4[r] * a.gain : a.gain) : 1.f;
+                }
+                float dacc[2][4];
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dacc[j][r] = 0.f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m = pg * 64 + i * 16 + (lane & 15);
+                    const int64_t pix = ((int64_t)n * a.H + ty0 + m / P_TW) * a.W + tx0 + m % P_TW;
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int64_t dst = pix * P_C + oq + j * 16;
+                        vec4 yv, rv;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float cv = acc[i][j][r];
+                            rv[r] = (T)cv;
+                            float v = cv;
+                            if (EPI) {
+                                v = fmaf(v, dsc[j][r], nv[i] + bsc[j][r]);
+                                v = fmaxf(v, v * lr_alpha);
+                                v = __builtin_amdgcn_fmed3f(v, -clampv, clampv);
+                            }
+                            yv[r] = (T)v;
+                            if (DOT) dacc[j][r] += (float)rv[r] * (float)dv[i][j][r];
+                        }
+                        *(vec4*)(y + dst) = yv;
+                        if (yr) *(vec4*)(yr + dst) = rv;
+                        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    }
+                }
+                if (DOT) {
+                    // sum over the 16 lanes holding the same channels (lane % 16 = pixel), one atomic each
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float v = dacc[j][r];
+                            v += __shfl_xor(v, 1);
+                            v += __shfl_xor(v, 2);
+                            v += __shfl_xor(v, 4);
+                            v += __shfl_xor(v, 8);
+                            if ((lane & 15) == 0) atomicAdd(&a.dot_out[(int64_t)n * P_C + oq + j * 16 + r], v);
+                        }
+                }
+            }
+            sstore(c ^ 1);
+            __syncthreads();
+        }
+    }
+}
+
+template <typename T, bool SI, bool EPI, bool DOT>
+int launch_c64p(const Conv3Args& a, hipStream_t s, int tiles, int grid) {
+    auto kern = conv3x3_c64p_kernel<T, SI, EPI, DOT>;
+    static bool attr_set = false;   // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P_LDS);
+        attr_set = true;
+    }
+    kern<<<grid, 512, P_LDS, s>>>(a, tiles);
+    return launch_status("sg2_conv3x3 (c64 persistent)");
+}
+
+template <typename T, bool SI, bool EPI>
+int launch_c64p_dot(const Conv3Args& a, hipStream_t s, int tiles, int grid) {
+    return a.dot_out ? launch_c64p<T, SI, EPI, true>(a, s, tiles, grid) : launch_c64p<T, SI, EPI, false>(a, s, tiles, grid);
+}
+
+int num_cus() {
+    static const int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 256;
+        return v > 0 ? v : 256;
+    }();
+    return n;
+}
+
 template <typename T>
 int dispatch(Conv3Args& a, hipStream_t s) {
     const bool si = a.in_scale != nullptr;
@@ -313,6 +589,19 @@ int dispatch(Conv3Args& a, hipStream_t s) {
     if (a.dot_out) {
         hipError_t e = hipMemsetAsync(a.dot_out, 0, (size_t)a.N * a.Cout * sizeof(float), s);
         if (e != hipSuccess) { set_error("sg2_conv3x3: memset failed"); return (int)e; }
+    }
+    static const bool persist = [] { const char* e = getenv("SG2_HALO_PERSIST"); return !e || atoi(e) != 0; }();
+    // (the persistent kernel's epilogue folds the gain into the demod / noise / bias terms and evaluates lrelu
+    // as max(v, alpha v): it needs gain > 0 and 0 <= alpha <= 1, the StyleGAN2 settings)
+    if (persist && a.Cin == P_C && a.Cout == P_C && a.H % P_TH == 0 && a.W % P_TW == 0 &&
+        (!epi || (a.gain > 0.f && (a.act == 0 || (a.alpha >= 0.f && a.alpha <= 1.f))))) {
+        const int tiles = a.N * (a.H / P_TH) * (a.W / P_TW);
+        if (tiles >= 4 * num_cus()) {
+            const int grid = num_cus();
+            if (si) { if (epi) return launch_c64p_dot<T, true, true>(a, s, tiles, grid); return launch_c64p_dot<T, true, false>(a, s, tiles, grid); }
+            if (epi) return launch_c64p_dot<T, false, true>(a, s, tiles, grid);
+            return launch_c64p_dot<T, false, false>(a, s, tiles, grid);
+        }
     }
     const int TW = a.W >= 32 ? 32 : 16;
     a.tiles_x = (a.W + TW - 1) / TW;

@@ -47,6 +47,15 @@ __device__ __forceinline__ vecT buf_load16(__amdgpu_buffer_rsrc_t r, int byte_of
     return __builtin_bit_cast(vecT, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
 }
 
+template <typename T>
+__device__ __forceinline__ T buf_load2(__amdgpu_buffer_rsrc_t r, int byte_off) {   // one 16-bit element
+    return __builtin_bit_cast(T, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(r, byte_off, 0, 0));
+}
+template <typename vecT>
+__device__ __forceinline__ vecT buf_load8(__amdgpu_buffer_rsrc_t r, int byte_off) {   // 8 bytes
+    return __builtin_bit_cast(vecT, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
+}
+
 template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T)v; }
 

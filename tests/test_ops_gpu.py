@@ -356,7 +356,8 @@ def test_augment_golden(name):
 
 # ------------------------------------------------------------------ LDS-halo 3x3 conv with fused epilogue
 @pytest.mark.parametrize('shape', [(2, 64, 32, 32, 64), (2, 64, 20, 37, 96), (1, 512, 32, 32, 512), (2, 128, 16, 16, 128),
-                                   (2, 40, 16, 24, 8)])
+                                   (2, 40, 16, 24, 8),
+                                   (4, 64, 256, 256, 64), (9, 64, 128, 256, 64)])   # persistent c64 kernel
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
 def test_conv3x3_fused(shape, dtype):
     from torch_utils.ops import conv2d_gradfix as cg
@@ -489,10 +490,11 @@ def test_layer_bwd(dtype, shape):
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
-def test_conv3x3_dot_and_scaled_wgrad(dtype):
+@pytest.mark.parametrize('shape', [(2, 64, 20, 33, 96), (5, 64, 128, 256, 64)])   # generic / persistent c64
+def test_conv3x3_dot_and_scaled_wgrad(dtype, shape):
     from torch_utils.ops import conv2d_gradfix as cg
     torch.manual_seed(4)
-    N, Cin, H, W, Cout = 2, 64, 20, 33, 96
+    N, Cin, H, W, Cout = shape
     x = torch.randn(N, Cin, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(Cout, Cin, 3, 3, device=DEV) / np.sqrt(Cin * 9)).to(dtype)
     src = torch.randn(N, Cout, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)

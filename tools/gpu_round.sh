@@ -48,7 +48,7 @@ if step pmc; then
     # HBM bytes of the roofline kernel: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots).
     for c in FETCH_SIZE WRITE_SIZE; do
         echo "== pmc $c"
-        timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex conv3x3_halo -d "$O/pmc_$c" -o run \
+        timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex 'conv3x3_(halo|c64p)' -d "$O/pmc_$c" -o run \
             --output-format csv -- python3 "$R/tools/roofline_only.py" > "$O/pmc_$c.log" 2>&1
         rc=$?; tail -1 "$O/pmc_$c.log"; [ $rc -eq 0 ] || exit $rc
     done
@@ -58,7 +58,7 @@ if step diag; then
     # where the halo conv waves wait (one pass, 8 SQ counters; MI355X_MICROARCH.md rocprofv3 PMC slots)
     echo "== pmc diag halo"
     timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
-        SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-include-regex 'conv3x3_halo|conv_fwd|wgrad' \
+        SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-include-regex 'conv3x3|conv_fwd|wgrad' \
         -d "$O/diag" -o run --output-format csv -- python3 "$R/tools/conv_micro.py" --reps 3 > "$O/diag.log" 2>&1
     rc=$?; tail -5 "$O/diag.log"; [ $rc -eq 0 ] || exit $rc
 fi
