@@ -55,7 +55,10 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--phase-timing', action='store_true')
-    ap.add_argument('--no-graphs', action='store_true', help='eager PyTorch dispatch instead of HIP-graph replay')
+    ap.add_argument('--graphs', default='auto', choices=['auto', 'on', 'off'],
+                    help='HIP-graph replay of each phase (auto: on for one GPU; with several GPUs the eager path, '
+                         'whose bucketed all_reduces overlap the backward from post-accumulate hooks)')
+    ap.add_argument('--no-graphs', action='store_true', help='same as --graphs off')
     return ap.parse_args()
 
 
@@ -194,7 +197,9 @@ def cpu_baseline(args):
     the host cores: one Gmain, Greg, Dmain and Dreg phase at the bench resolution with batch 4
     (bounded sample), combined with the reference's phase frequencies (1, 1/4, 1, 1/16)."""
     from oracle import sg2_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    # the host cores this process may use: its CPU affinity, or the share the GPU box grants it
+    # (OMP_NUM_THREADS; os.cpu_count() there reports the whole machine)
+    threads = int(os.environ.get('OMP_NUM_THREADS') or len(os.sched_getaffinity(0)))
     torch.set_num_threads(threads)
     B = 4
     torch.manual_seed(0)
@@ -243,9 +248,11 @@ def main():
     real, real_c = make_inputs(args, device, rank)
     for _ in range(args.warmup):
         one_step(tr, args, device, real, real_c)
-    if not args.no_graphs:
+    graphs = (args.graphs == 'on' or (args.graphs == 'auto' and num_gpus == 1)) and not args.no_graphs
+    if graphs:
         # capture: one untimed step at batch_idx 0 runs (and captures) all four phases; afterwards every
-        # phase is a single HIP-graph replay (trainer.py Trainer.graphs)
+        # phase is a single HIP-graph replay (trainer.py Trainer.graphs; with several GPUs the bucket
+        # all_reduces are captured into the phase graphs)
         tr.graphs = True
         tr.batch_idx = 0
         one_step(tr, args, device, real, real_c)
@@ -283,6 +290,7 @@ def main():
             'metric': 'imgs/sec at 256^2 bs32/GPU StyleGAN2-ADA training (+ sec/kimg)',
             'value': round(value, 3), 'unit': 'imgs/s', 'n_gpus': num_gpus, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
+            'graphs': graphs,
             'scaling': 'weak', 'vs_baseline': None,
             'dtype': f'{args.fp16_dtype}+fp32 (fp16 at the 4 highest resolutions, fp32 below; f32 accumulate)',
             'data': 'synthetic (U(-1,1) reals resident in HBM, device-drawn z, random one-hot c; random-init weights)',

@@ -64,7 +64,7 @@ class InfiniteSampler(torch.utils.data.Sampler):
 
     def __init__(self, dataset, rank=0, num_replicas=1, shuffle=True, seed=0, window_size=0.5):
         assert len(dataset) > 0 and num_replicas > 0 and 0 <= rank < num_replicas and 0 <= window_size <= 1
-        super().__init__(dataset)
+        super().__init__()
         self.dataset, self.rank, self.num_replicas = dataset, rank, num_replicas
         self.shuffle, self.seed, self.window_size = shuffle, seed, window_size
 
@@ -97,10 +97,11 @@ def named_params_and_buffers(module):
 
 def copy_params_and_buffers(src_module, dst_module, require_all=False):
     src = dict(named_params_and_buffers(src_module))
-    for name, t in named_params_and_buffers(dst_module):
-        assert (name in src) or (not require_all)
-        if name in src:
-            t.copy_(src[name].detach()).requires_grad_(t.requires_grad)
+    with torch.no_grad():
+        for name, t in named_params_and_buffers(dst_module):
+            assert (name in src) or (not require_all)
+            if name in src:
+                t.copy_(src[name].detach())
 
 
 @contextlib.contextmanager
