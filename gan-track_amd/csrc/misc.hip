@@ -172,15 +172,18 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(Tout* __restrict__ out
 // Row-wise infinity-norm pre-normalisation of the fp16 modulated layers (networks_stylegan2.py:52-54):
 // n = max_i |t[r,i]|; mode 0: y = t * ((1/n) * c) (the weight: torch's scalar / tensor is a reciprocal and a
 // scale), mode 1: y = t / n (the styles).  One workgroup per row, the row reread from L2 for the store.
+// max that propagates NaN (torch's amax / norm(inf) does; fmaxf would drop it)
+__device__ __forceinline__ float nanmax(float a, float b) { return (a != a || b != b) ? __builtin_nanf("") : fmaxf(a, b); }
+
 __device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
     for (int off = 32; off > 0; off >>= 1) {
         const float o = __shfl_xor(v, off);
-        v = is_max ? fmaxf(v, o) : v + o;
+        v = is_max ? nanmax(v, o) : v + o;
     }
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
-    return is_max ? fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])) : (red[0] + red[1]) + (red[2] + red[3]);
+    return is_max ? nanmax(nanmax(red[0], red[1]), nanmax(red[2], red[3])) : (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 __global__ __launch_bounds__(256) void infnorm_fwd_kernel(float* __restrict__ y, float* __restrict__ nrm,
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(256) void infnorm_fwd_kernel(float* __restrict__ y,
     __shared__ float red[4];
     const float* tr = t + (int64_t)blockIdx.x * L;
     float m = 0.f;
-    for (int i = threadIdx.x; i < L; i += 256) m = fmaxf(m, fabsf(tr[i]));
+    for (int i = threadIdx.x; i < L; i += 256) m = nanmax(m, fabsf(tr[i]));
     m = block_reduce(m, red, true);
     if (threadIdx.x == 0) nrm[blockIdx.x] = m;
     float* yr = y + (int64_t)blockIdx.x * L;
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(256) void infnorm_bwd_kernel(float* __restrict__ dt
     for (int i = threadIdx.x; i < L; i += 256) {
         const float tv = t[base + i];
         s1 += dy[base + i] * tv;
-        cnt += fabsf(tv) == n ? 1.f : 0.f;
+        cnt += (fabsf(tv) == n || tv != tv) ? 1.f : 0.f;
     }
     s1 = block_reduce(s1, red, false);
     cnt = block_reduce(cnt, red, false);
@@ -218,7 +221,7 @@ __global__ __launch_bounds__(256) void infnorm_bwd_kernel(float* __restrict__ dt
     for (int i = threadIdx.x; i < L; i += 256) {
         const float tv = t[base + i], g = dy[base + i];
         float d = mode == 0 ? g * k : g / n;
-        if (fabsf(tv) == n) d += (tv > 0.f ? gm : (tv < 0.f ? -gm : 0.f));
+        if (fabsf(tv) == n || tv != tv) d += (tv > 0.f ? gm : (tv < 0.f ? -gm : (tv != tv ? tv : 0.f)));
         dt[base + i] = d;
     }
 }

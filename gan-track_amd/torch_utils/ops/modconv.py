@@ -61,6 +61,7 @@ def _mul(a, s):
 class FusedConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, styles, weight, dcoefs, noise, bias, residual, stride, pad, act, alpha, gain, clamp):
+        x_in = x                       # saved as given: a create_graph backward differentiates through it
         x = _cg._nhwc(x)
         n, cin, h, w = x.shape
         cout, _, kh, kw = weight.shape
@@ -82,7 +83,7 @@ class FusedConv(torch.autograd.Function):
                                     in_scale=_f32(styles), out_scale=_f32(dcoefs), noise=nz, noise_gain=1.0,
                                     bias=b32, act=act, alpha=alpha, gain=gain, clamp=clamp, residual=residual,
                                     aux_mode=1 if want_c else (2 if want_z else 0))
-        ctx.save_for_backward(x, styles, weight, dcoefs, noise, bias, y, aux)
+        ctx.save_for_backward(x_in, styles, weight, dcoefs, noise, bias, y, aux)
         ctx.cfg = (stride, pad, act, alpha, gain, clamp, residual is not None)
         return y
 
@@ -95,8 +96,8 @@ class FusedConv(torch.autograd.Function):
         zsrc = aux if has_res else y
         c = aux if (dcoefs is not None and not has_res) else None
         if not torch.is_grad_enabled() and fast_backward:
-            g = _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain,
-                               clamp)
+            g = _fast_backward(need, dy, _cg._nhwc(x), styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act,
+                               alpha, gain, clamp)
         else:
             g = _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha,
                                    gain, clamp)
@@ -141,13 +142,13 @@ class _ScaledConvT(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, dz, d, weight, stride, pad, out_hw):
-        dz = _cg._nhwc(dz)
+        dzk = _cg._nhwc(dz)            # the kernels' layout; the input itself is saved (third-order fallback)
         cin, kh, kw = weight.shape[1], weight.shape[2], weight.shape[3]
         dt = dz.dtype
-        if _halo(dz, kh, kw, stride, pad):
-            y, _ = _cg.conv3x3_fused(dz, _cg._pack_convT(weight, dt, flip=True), cin, in_scale=_f32(d))
+        if _halo(dzk, kh, kw, stride, pad):
+            y, _ = _cg.conv3x3_fused(dzk, _cg._pack_convT(weight, dt, flip=True), cin, in_scale=_f32(d))
         else:
-            y, _ = _cg.conv_fused(dz, _cg._pack_convT(weight, dt), cin, out_hw[0], out_hw[1], kh, kw, stride,
+            y, _ = _cg.conv_fused(dzk, _cg._pack_convT(weight, dt), cin, out_hw[0], out_hw[1], kh, kw, stride,
                                   (pad, pad), transpose=True, in_scale=_f32(d))
         ctx.save_for_backward(dz, d, weight)
         ctx.cfg = (stride, pad, tuple(out_hw))
@@ -167,6 +168,7 @@ class _ScaledConvT(torch.autograd.Function):
             gs = iter(torch.autograd.grad(y, ins, g, create_graph=True, allow_unused=True))
             return tuple(next(gs) if nd else None for nd in need[:3]) + (None, None, None)
         g = _cg._nhwc(g.to(dt))
+        dz = _cg._nhwc(dz)
         d32 = _f32(d)
         gdz = gd = gw = None
         if need[0] or need[1]:
@@ -210,7 +212,7 @@ class _SavedRaw(torch.autograd.Function):
                                    (oh, ow))
             gs = iter(torch.autograd.grad(cc, ins, dc, create_graph=True, allow_unused=True))
             return tuple(next(gs) if nd else None for nd in need[:3]) + (None, None, None)
-        dx, ds, dw = _scaled_input_grads(_cg._nhwc(dc.to(x.dtype)), x, styles,
+        dx, ds, dw = _scaled_input_grads(_cg._nhwc(dc.to(x.dtype)), _cg._nhwc(x), styles,
                                          weight, need[0], need[1], need[2], stride, pad)
         return dx, ds, dw, None, None, None
 

@@ -430,6 +430,52 @@ def test_fused_synthesis_layer_matches_composed(dtype):
         assert rel_err(a_, b_) < 4 * tol
 
 
+@pytest.mark.parametrize('dtype,res', [(torch.float16, 16), (torch.bfloat16, 16), (torch.float32, 16),
+                                       (torch.float16, 4), (torch.float32, 8)])
+def test_fused_synthesis_layer_pl_pass(dtype, res):
+    """The path-length pass as loss.py runs it: the create_graph gradient w.r.t. ws under
+    conv2d_gradfix.no_weight_gradients() (where the dgrad goes through _ScaledConvT, the demodulation scale
+    on the operand staging), then the penalty's backward with weight gradients enabled (_ScaledConvT's
+    backward: conv(G, W) * d with the dd dot epilogue, and the d-scaled wgrad).  Fused path vs the composed
+    one (x*s, conv, fma, bias_act kernels); 16-bit at 16^2 runs the halo kernels, f32 and 4^2 the generic."""
+    from training import networks_stylegan2 as net
+    from torch_utils.ops import conv2d_gradfix, modconv
+    torch.manual_seed(13)
+    layer = net.SynthesisLayer(32, 48, w_dim=16, resolution=res, conv_clamp=256).to(DEV)
+    with torch.no_grad():
+        layer.noise_strength.fill_(0.3)
+        layer.bias.copy_(torch.randn(48) * 0.2)
+    x0 = torch.randn(4, 32, res, res, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    w0 = torch.randn(4, 16, device=DEV)
+    noise = torch.randn(4, 1, res, res, device=DEV)
+    pl = torch.randn(4, 48, res, res, device=DEV)
+    params = [layer.weight, layer.bias, layer.noise_strength, layer.affine.weight, layer.affine.bias]
+    out = []
+    for fused in [True, False]:
+        modconv.enabled = fused
+        x = x0.clone().requires_grad_(True)
+        wv = w0.clone().requires_grad_(True)
+        orig = torch.randn
+        torch.randn = lambda *a, **k: noise.clone()
+        try:
+            y = layer(x, wv)
+        finally:
+            torch.randn = orig
+        with conv2d_gradfix.no_weight_gradients():
+            g_w, = torch.autograd.grad((y.float() * pl).sum(), [wv], create_graph=True)
+        g2 = torch.autograd.grad(g_w.square().sum(), params + [x, wv], allow_unused=True)
+        out.append((g_w.float(), [g if g is None else g.float() for g in g2]))
+    modconv.enabled = True
+    tol = {torch.float16: 2e-2, torch.bfloat16: 5e-2, torch.float32: 1e-4}[dtype]
+    (gw1, g21), (gw2, g22) = out
+    assert rel_err(gw1, gw2) < tol
+    for a_, b_ in zip(g21, g22):
+        if b_ is None:
+            continue
+        assert a_ is not None
+        assert rel_err(a_, b_) < 4 * tol
+
+
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize('shape', [(4, 32, 16, 16, 48), (2, 64, 32, 32, 64), (2, 512, 16, 16, 256)])
 def test_fused_synthesis_layer_fast_backward(dtype, shape):
@@ -894,3 +940,34 @@ def test_infnorm_prenorm():
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     for a, b in zip(out[0][2:], out[1][2:]):
         assert rel_err(a.double().cpu(), b.double().cpu()) < 1e-6
+
+
+def test_infnorm_prenorm_nan_rows():
+    """A NaN in a row makes that row's norm(inf) NaN (torch's amax propagates it) -- the fused reduction
+    must not drop it as fmaxf would; forward and gradient NaN patterns match the reference expression and
+    the finite rows are unaffected."""
+    from training import networks_stylegan2 as net
+    torch.manual_seed(6)
+    w = torch.randn(8, 16, 3, 3, device=DEV)
+    w[2, 3, 1, 0] = float('nan')
+    s = torch.randn(4, 16, device=DEV)
+    s[1, 7] = float('nan')
+    gy_w, gy_s = torch.randn_like(w), torch.randn_like(s)
+
+    def ref(w_, s_):
+        return (w_ * (1 / np.sqrt(16 * 9) / w_.norm(float('inf'), dim=[1, 2, 3], keepdim=True)),
+                s_ / s_.norm(float('inf'), dim=1, keepdim=True))
+
+    out = []
+    for fn in (net._prenorm, ref):
+        wd, sd = w.clone().requires_grad_(True), s.clone().requires_grad_(True)
+        yw, ys = fn(wd, sd)
+        gw, gs = torch.autograd.grad((yw * gy_w).sum() + (ys * gy_s).sum(), [wd, sd])
+        out.append([yw.detach(), ys.detach(), gw, gs])
+    assert torch.isnan(out[0][0][2]).all() and torch.isnan(out[0][1][1]).all()
+    for a, b in zip(out[0][:2], out[1][:2]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+    for a, b in zip(out[0][2:], out[1][2:]):
+        assert torch.equal(torch.isnan(a), torch.isnan(b))
+        fin = ~torch.isnan(a)
+        assert rel_err(a[fin].double().cpu(), b[fin].double().cpu()) < 1e-6
