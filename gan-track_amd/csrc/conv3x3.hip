@@ -309,39 +309,65 @@ int launch3(const Conv3Args& a, hipStream_t s) {
 // ---------------------------------------------------------------------------------------------------
 // Persistent, weights-resident variant for the 64 -> 64 channel layers (the 256^2 layer of the Claro
 // network, 512^2 at cbase 32768; forward and dgrad).  The generic halo kernel above restages the 9 x 64 x 64
-// weights (74 KB) for every 256-pixel tile, and its per-tile prologue (first chunk's loads) and epilogue
-// (noise / demod loads, LDS transpose) are exposed: with Cin = 64 a tile is only two chunks of MFMAs.
-// Here one workgroup of 8 waves per CU keeps all weights in LDS for the whole launch and walks a
-// contiguous run of tiles (neighbouring tiles share halo rows in the same XCD's L2):
-//   * wave w owns pixels 64*(w%4) .. +63 of the 256-pixel tile and output channels 32*(w/4) .. +31
-//     (2 waves per SIMD: one's LDS reads / epilogue overlap the other's MFMAs);
+// weights (74 KB) for every 256-pixel tile, and its per-tile prologue / epilogue are exposed: with Cin = 64
+// a tile is only two chunks of MFMAs.  Here one workgroup of 8 waves per CU keeps all weights in LDS for
+// the whole launch and walks a contiguous run of 32 x 16 pixel tiles (vertically neighbouring tiles share
+// halo rows through the CU's L2):
+//   * wave w owns tile rows 2w, 2w+1 (64 pixels) x all 64 output channels: per tap and chunk 4 pixel and
+//     4 weight fragments feed 16 MFMAs (0.5 ds_read_b128 per MFMA; 2 waves per SIMD, so one wave's LDS
+//     reads and epilogue overlap the other's MFMAs);
+//   * LDS is unpadded and XOR-swizzled: the 16-byte piece q of position p (a halo pixel or a weight row,
+//     64 B per 32-channel chunk) sits at p * 64 + ((q ^ ((p >> 1) & 2)) << 4).  A fragment read (16
+//     consecutive positions, 4 pieces) then hits 16 distinct 16-byte bank slots in each of ds_read_b128's
+//     four lane groups ({0-3,12-15,20-27}, ...) for ANY starting position -- the tap shifts included --
+//     where the 80-byte padded rows of the halo kernel conflict 2-way (SQ_LDS_BANK_CONFLICT = half the
+//     LDS cycles, profiles/r02_v1_pmc_diag.txt).  The staging stores (8 lanes = 2 positions) stay
+//     contiguous 128-byte blocks;
 //   * the tile's two 32-channel chunks live in a double buffer: the next chunk's global loads (the next
 //     tile's first chunk, during the current tile's second) are issued before the current chunk's MFMAs,
 //     one barrier per chunk, no per-tile prologue;
 //   * the epilogue's operands (noise, demod scales, dot source) are loaded before the tile's last chunk of
 //     MFMAs, and the MFMA operands are swapped (weights as A, pixels as B) so a lane's accumulator holds 4
 //     consecutive output channels of one pixel: 8-byte stores straight from registers, no LDS transpose;
+//     the dot epilogue (dgrad's ds = sum_p c * x) keeps its per-(n, channel) partial sums in registers
+//     across the run's tiles of one sample and flushes them once per sample;
 //   * the modulation x * s is applied at the LDS store as a 16-bit multiply by s rounded to the
 //     activation dtype -- the reference's `x * styles.to(x.dtype)` (networks_stylegan2.py:69) bit for bit.
-constexpr int P_TW = 32, P_TH = 8, P_C = 64;
-constexpr int P_HW = P_TW + 2, P_HH = P_TH + 2, P_HP = P_HW * P_HH;      // 34 x 10 halo
-constexpr int P_HALO = P_HP * PX;                                         // elements per halo chunk buffer
-constexpr int P_WCH = 9 * P_C * PX;                                       // elements per weight chunk
-constexpr size_t P_LDS = (size_t)(2 * P_WCH + 2 * P_HALO) * 2;            // 146,560 B
+#ifndef SG2_DIAG
+#define SG2_DIAG 0          // timing-only builds (tools/c64p_diag.sh): 1 no MFMA, 2 no output stores, 4 no halo loads,
+                            // 8 both chunks load the first 64 B of each pixel line
+#endif
+constexpr int P_TW = 32, P_TH = 16, P_C = 64;
+constexpr int P_HW = P_TW + 2, P_HH = P_TH + 2, P_HP = P_HW * P_HH;      // 34 x 18 halo positions
+constexpr int P_POS = CK * 2;                                             // bytes per position and chunk
+constexpr int P_WB = 2 * 9 * P_C * P_POS;                                 // weights: 73,728 B
+constexpr int P_HB = P_HP * P_POS;                                        // one halo buffer: 39,168 B
+constexpr int P_EB = (2 * P_C + P_TW * P_TH) * 4 + 16;                     // epilogue tables (f32), a dummy slot
+constexpr size_t P_LDS = (size_t)P_WB + 2 * P_HB + P_EB;                  // 154,624 B
+static_assert(P_WB % 256 == 0 && P_HB % 256 == 0, "swizzle assumes 256-byte aligned regions");
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Output channel of MFMA row m (0..15) of channel tile j (A-operand row P = 16 j + m): tiles 2jj, 2jj+1 give
+// lane group q the 8 consecutive channels 32 jj + 8 q .. +7 (rows 4q..4q+3 of each), so the epilogue stores
+// 16 bytes per lane and pixel instead of 8 (a store-issue-bound tail: MI355X_MICROARCH.md latency table).
+__device__ __forceinline__ int p_chan(int P) { return (P >> 5) * 32 + 8 * ((P & 15) >> 2) + 4 * ((P >> 4) & 1) + (P & 3); }
+__device__ __forceinline__ int swz(int pos, int q) { return pos * P_POS + ((q ^ ((pos >> 1) & 2)) << 4); }
 
 template <typename T, bool SCALE_IN, bool EPI, bool DOT>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int tiles_total) {
     constexpr int NT = 512;
-    constexpr int NH = (P_HP * 4 + NT - 1) / NT;         // halo 16-B loads per thread per chunk (3)
-    constexpr int NW = (9 * P_C * 4) / NT;               // weight 16-B loads per thread per chunk (4.5 -> see below)
+    constexpr int NH = (P_HP * 4 + NT - 1) / NT;         // halo 16-B loads per thread per chunk (5)
+    constexpr int NWL = 2 * 9 * P_C * 4 / NT;            // weight 16-B loads per thread (9)
     typedef T vec8 __attribute__((ext_vector_type(8)));
     typedef T vec4 __attribute__((ext_vector_type(4)));
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    T* wlds = (T*)smem_raw;                              // [2 chunks][9][64][PX]
-    T* hlds = wlds + 2 * P_WCH;                          // [2 chunks][HP][PX]
+    char* wlds = smem_raw;                               // [2 chunks][9 taps][64 rows] x 64 B, swizzled
+    char* hlds = smem_raw + P_WB;                        // [2 buffers][612 positions] x 64 B, swizzled
+    float* blds = (float*)(smem_raw + P_WB + 2 * P_HB);  // gain * bias[64]
+    float* dlds = blds + P_C;                            // the tile's gain * demod[n, 64]
+    float* nlds = dlds + P_C;                            // the tile's gain * noise_gain * noise[512 pixels]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int pg = wave & 3, half = wave >> 2;           // pixel group, channel half
     const int tiles_x = a.W / P_TW, tiles_y = a.H / P_TH;
     const int per_n = tiles_x * tiles_y;
     const int t_begin = (int)((int64_t)blockIdx.x * tiles_total / gridDim.x);
@@ -350,14 +376,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
     const __amdgpu_buffer_rsrc_t rxb = make_rsrc(a.x, (int64_t)a.N * a.H * a.W * P_C * (int64_t)sizeof(T));
     const __amdgpu_buffer_rsrc_t rwb = make_rsrc(a.w, (int64_t)P_C * 9 * P_C * (int64_t)sizeof(T));
 
-    // ---- weights: both chunks, once (2 x 2304 16-B rows over 512 threads) ----
-    for (int idx = tid; idx < 2 * 9 * P_C * 4; idx += NT) {
+    // ---- weights: both chunks, once; bias ----
+#pragma unroll
+    for (int k = 0; k < NWL; ++k) {
+        const int idx = tid + k * NT;
         const int c = idx / (9 * P_C * 4), rem = idx - c * 9 * P_C * 4;
-        const int r = rem >> 2, tap = r / P_C, o = r - tap * P_C;
-        const vec8 v = buf_load16<vec8>(rwb, ((o * 9 + tap) * P_C + c * CK + (rem & 3) * 8) * (int)sizeof(T));
-        *(vec8*)(wlds + c * P_WCH + (tap * P_C + o) * PX + (rem & 3) * 8) = v;
+        const int r = rem >> 2, q = rem & 3, tap = r / P_C, row = r - tap * P_C;
+        const int o = p_chan(row);
+        const vec8 v = buf_load16<vec8>(rwb, ((o * 9 + tap) * P_C + c * CK + q * 8) * (int)sizeof(T));
+        *(vec8*)(wlds + swz((c * 9 + tap) * P_C + row, q)) = v;
     }
-    (void)NW;
+    if (tid < P_C) blds[tid] = (EPI && a.bias) ? (float)(T)a.bias[tid] * a.gain : 0.f;
 
     // ---- halo staging geometry (fixed per thread; the tile origin varies) ----
     int h_dy[NH], h_dx[NH], h_dst[NH];
@@ -366,11 +395,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
         const int idx = tid + i * NT, p = idx >> 2, q = idx & 3;
         h_dy[i] = p / P_HW - 1;
         h_dx[i] = p % P_HW - 1;
-        h_dst[i] = p < P_HP ? p * PX + q * 8 : -1;
+        h_dst[i] = p < P_HP ? swz(p, q) : -1;
     }
     const int hq = (tid & 3) * 8;
     vec8 rh[NH];
-    vec8 sv8;                                            // the chunk's 8 style scales, rounded to T
+    float4 s0, s1;                                       // the chunk's 8 style scales (rounded to T at the store)
+    const __amdgpu_buffer_rsrc_t rsc = make_rsrc(a.in_scale, SCALE_IN ? (int64_t)a.N * P_C * 4 : 0);
     auto tile_of = [&](int t, int& n, int& ty0, int& tx0) {
         n = t / per_n;
         const int tr = t - n * per_n;
@@ -383,20 +413,21 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
 #pragma unroll
         for (int i = 0; i < NH; ++i) {
             const int iy = ty0 + h_dy[i], ix = tx0 + h_dx[i];
-            const bool ok = h_dst[i] >= 0 && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-            rh[i] = buf_load16<vec8>(rxb, ok ? (((n * a.H + iy) * a.W + ix) * P_C + c * CK + hq) * (int)sizeof(T) : -1);
+            // bitwise &: no short-circuit branches (each would split the load sequence)
+            const bool ok = (tid + i * NT < P_HP * 4) & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W);
+            if (!(SG2_DIAG & 4)) rh[i] = buf_load16<vec8>(rxb, ok ? (((n * a.H + iy) * a.W + ix) * P_C + ((SG2_DIAG & 8) ? 0 : c) * CK + hq) * (int)sizeof(T) : -1);
+            else rh[i] = vec8{};
         }
         if (SCALE_IN) {
-            const float* sc = a.in_scale + (int64_t)n * P_C + c * CK + hq;
-            const float4 s0 = *(const float4*)sc, s1 = *(const float4*)(sc + 4);
-            sv8 = vec8{(T)s0.x, (T)s0.y, (T)s0.z, (T)s0.w, (T)s1.x, (T)s1.y, (T)s1.z, (T)s1.w};
+            s0 = buf_load16<float4>(rsc, (n * P_C + c * CK + hq) * 4);
+            s1 = buf_load16<float4>(rsc, (n * P_C + c * CK + hq + 4) * 4);
         }
     };
     auto sstore = [&](int buf) {
-        T* hb = hlds + buf * P_HALO;
+        char* hb = hlds + buf * P_HB;
+        const vec8 sv8 = vec8{(T)s0.x, (T)s0.y, (T)s0.z, (T)s0.w, (T)s1.x, (T)s1.y, (T)s1.z, (T)s1.w};
 #pragma unroll
         for (int i = 0; i < NH; ++i) {
-            if (h_dst[i] < 0) continue;
             vec8 v = rh[i];
             if (SCALE_IN) {
                 if constexpr (std::is_same<T, f16_t>::value) {
@@ -406,39 +437,45 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
                     for (int j = 0; j < 8; ++j) v[j] = (T)((float)v[j] * (float)sv8[j]);
                 }
             }
-            *(vec8*)(hb + h_dst[i]) = v;
+            // the ragged last round writes a dummy slot instead of branching round the store (a branch
+            // leaves the skipped load pending for the waitcnt pass, which then drains vmcnt at the loop top)
+            char* dst = h_dst[i] >= 0 ? hb + h_dst[i] : smem_raw + P_LDS - 16;
+            *(vec8*)dst = v;
         }
     };
 
-    const int ko = 8 * (lane >> 4);
-    int a_base[4];
+    // MFMA operand addressing (lane: row / pixel = lane & 15, 16-byte piece q = lane >> 4)
+    const int l16 = lane & 15, q = lane >> 4;
+    const int w_lane = swz(l16, q);                      // + (chunk * 9 + tap) * 4096 + j * 1024 (same swizzle)
+    int hp[4];                                           // halo position of pixel fragment i at tap (0, 0)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int m = pg * 64 + i * 16 + (lane & 15);
-        a_base[i] = ((m / P_TW) * P_HW + (m % P_TW)) * PX + ko;
-    }
-    const int b_base = (half * 32 + (lane & 15)) * PX + ko;
-    const int oq = half * 32 + 4 * (lane >> 4);          // channel of acc[.][j][0] is oq + 16 * j
-    float bsc[2][4];                                     // gain * bias (rounded to T first, as the reference)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            bsc[j][r] = (EPI && a.bias) ? (float)(T)a.bias[oq + j * 16 + r] * a.gain : 0.f;
+    for (int i = 0; i < 4; ++i) hp[i] = (2 * wave + (i >> 1)) * P_HW + (i & 1) * 16 + l16;
+    const int oq8 = 8 * q;                               // channel of acc[.][j][r] is 32 (j / 2) + oq8 + 4 (j % 2) + r
     const float lr_alpha = (EPI && a.act == 1) ? a.alpha : 1.f;   // lrelu as max(v, alpha v), 0 <= alpha <= 1
     const float clampv = (EPI && a.clamp >= 0.f) ? a.clamp : __builtin_inff();
+    const float ngain = a.noise_gain * a.gain;
+    const float dgain = a.gain;
+    T e_noise;                                           // this thread's pixel of the tile's noise
+    float e_d;                                           // this thread's (tid < 64) demodulation scale
 
-    f32x4 acc[4][2];
+    f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dacc[2][8];                                    // dot partial sums of the current sample
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dacc[jj][e] = 0.f;
 
-    T* y = (T*)a.y;
-    T* yr = (T*)a.y_raw;
     const int64_t npix = (int64_t)a.N * a.H * a.W;
+    const __amdgpu_buffer_rsrc_t ryb = make_rsrc(a.y, npix * P_C * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t ryr = make_rsrc(a.y_raw, a.y_raw ? npix * P_C * (int64_t)sizeof(T) : 0);
+    const bool has_raw = __builtin_amdgcn_readfirstlane(a.y_raw != nullptr);
     const __amdgpu_buffer_rsrc_t rnz = make_rsrc(a.noise, a.noise ? npix * (int64_t)sizeof(T) : 0);
     const __amdgpu_buffer_rsrc_t ros = make_rsrc(a.out_scale, a.out_scale ? (int64_t)a.N * P_C * 4 : 0);
+    const int e_row = tid / P_TW, e_col = tid % P_TW;
     const __amdgpu_buffer_rsrc_t rds = make_rsrc(a.dot_src, a.dot_src ? npix * P_C * (int64_t)sizeof(T) : 0);
     gload(t_begin, 0);
     __syncthreads();                                     // weights in LDS
@@ -447,109 +484,125 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
     for (int t = t_begin; t < t_end; ++t) {
         int n, ty0, tx0;
         tile_of(t, n, ty0, tx0);
-        T nraw[4];
-        float4 draw[2];
-        vec4 dv[4][2];
+        vec8 dv[4][2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {                   // chunk c of tile t lives in halo buffer c
             // no branch around a load (hipcc would drain vmcnt right after it): the last tile's "next
             // chunk" re-reads the tile itself, and absent epilogue operands read zeros (empty buffers)
             gload(c == 0 ? t : min(t + 1, t_end - 1), c ^ 1);
-            if (c == 1) {
-                // the epilogue's operands, in flight during the last chunk's MFMAs
+            if (c == 0 && EPI) {
+                // the tile's noise and demodulation scales: into LDS with the chunk's halo store
+                e_noise = buf_load2<T>(rnz, ((n * a.H + ty0 + e_row) * a.W + tx0 + e_col) * (int)sizeof(T));
+                e_d = buf_load4f(ros, (n * P_C + (tid & (P_C - 1))) * 4);
+            }
+            if (c == 1 && DOT) {
+                // the dot source of pixel fragments 0, 1 in flight during the last chunk's MFMAs (2, 3 are
+                // loaded at the epilogue's start: the registers for all four would spill)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int m = pg * 64 + i * 16 + (lane & 15);
-                    const int pix = (n * a.H + ty0 + m / P_TW) * a.W + tx0 + m % P_TW;
-                    if (EPI) nraw[i] = buf_load2<T>(rnz, pix * (int)sizeof(T));
-                    if (DOT) {
+                for (int i = 0; i < 2; ++i) {
+                    const int pix = (n * a.H + ty0 + 2 * wave + (i >> 1)) * a.W + tx0 + (i & 1) * 16 + l16;
 #pragma unroll
-                        for (int j = 0; j < 2; ++j) dv[i][j] = buf_load8<vec4>(rds, (pix * P_C + oq + j * 16) * (int)sizeof(T));
-                    }
-                }
-                if (EPI) {
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) draw[j] = buf_load16<float4>(ros, (n * P_C + oq + j * 16) * 4);
+                    for (int jj = 0; jj < 2; ++jj) dv[i][jj] = buf_load16<vec8>(rds, (pix * P_C + jj * 32 + oq8) * (int)sizeof(T));
                 }
             }
-            const T* hb = hlds + c * P_HALO;
-            const T* wb = wlds + c * P_WCH;
+            __builtin_amdgcn_sched_barrier(0);         // all loads issued before the MFMAs
+            const char* hb = hlds + c * P_HB;
+            const char* wb = wlds + c * 9 * P_C * P_POS + w_lane;
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky) {
 #pragma unroll
                 for (int kx = 0; kx < 3; ++kx) {
-                    const int toff = (ky * P_HW + kx) * PX;
                     const int tap = ky * 3 + kx;
-                    v8<T> af[4], bfr[2];
+                    v8<T> pf[4], wf[4];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) af[i] = *(const v8<T>*)(hb + a_base[i] + toff);
+                    for (int j = 0; j < 4; ++j) wf[j] = *(const v8<T>*)(wb + (tap * P_C + j * 16) * P_POS);
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) bfr[j] = *(const v8<T>*)(wb + tap * P_C * PX + j * 16 * PX + b_base);
+                    for (int i = 0; i < 4; ++i) pf[i] = *(const v8<T>*)(hb + swz(hp[i] + ky * P_HW + kx, q));
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
 #pragma unroll
-                        for (int j = 0; j < 2; ++j) acc[i][j] = mma<T>(bfr[j], af[i], acc[i][j]);
+                        for (int j = 0; j < 4; ++j) {
+                            if (!(SG2_DIAG & 1)) acc[i][j] = mma<T>(wf[j], pf[i], acc[i][j]);
+                            else acc[i][j][0] += (float)wf[j][0] * (float)pf[i][0];
+                        }
                 }
             }
+            // keep the scheduler from hoisting the staging store's math (which waits for the in-flight halo
+            // loads) or the epilogue above the MFMAs
+            __builtin_amdgcn_sched_barrier(0);
             if (c == 1) {
                 // ---- epilogue of tile t from the accumulators: lane = 4 channels x 1 pixel ----
                 // the gain folded in: gain * lrelu(z) = lrelu(gain * z) for gain > 0 (host-checked)
-                float nv[4], dsc[2][4];
+                if (DOT) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) nv[i] = EPI ? (float)nraw[i] * (a.noise_gain * a.gain) : 0.f;
+                    for (int i = 2; i < 4; ++i) {
+                        const int pix = (n * a.H + ty0 + 2 * wave + (i >> 1)) * a.W + tx0 + (i & 1) * 16 + l16;
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const float d4[4] = {draw[j].x, draw[j].y, draw[j].z, draw[j].w};
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) dsc[j][r] = EPI ? (a.out_scale ? d4[r] * a.gain : a.gain) : 1.f;
+                        for (int jj = 0; jj < 2; ++jj) dv[i][jj] = buf_load16<vec8>(rds, (pix * P_C + jj * 32 + oq8) * (int)sizeof(T));
+                    }
                 }
-                float dacc[2][4];
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) dacc[j][r] = 0.f;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int m = pg * 64 + i * 16 + (lane & 15);
-                    const int64_t pix = ((int64_t)n * a.H + ty0 + m / P_TW) * a.W + tx0 + m % P_TW;
+                    const int64_t pix = ((int64_t)n * a.H + ty0 + 2 * wave + (i >> 1)) * a.W + tx0 + (i & 1) * 16 + l16;
+                    const float nv = EPI ? nlds[(2 * wave + (i >> 1)) * P_TW + (i & 1) * 16 + l16] : 0.f;
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const int64_t dst = pix * P_C + oq + j * 16;
-                        vec4 yv, rv;
+                    for (int jj = 0; jj < 2; ++jj) {
+                        const int ch = jj * 32 + oq8;            // channels ch .. ch + 7: acc[i][2jj][.], acc[i][2jj+1][.]
+                        const int64_t dst = pix * P_C + ch;
+                        float bb[8], dd[8];
+                        if (EPI) {
+                            const float4 b0 = *(const float4*)(blds + ch), b1 = *(const float4*)(blds + ch + 4);
+                            const float4 d0 = *(const float4*)(dlds + ch), d1 = *(const float4*)(dlds + ch + 4);
+                            bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+                            dd[0] = d0.x; dd[1] = d0.y; dd[2] = d0.z; dd[3] = d0.w; dd[4] = d1.x; dd[5] = d1.y; dd[6] = d1.z; dd[7] = d1.w;
+                        }
+                        vec8 yv, rv;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const float cv = acc[i][j][r];
-                            rv[r] = (T)cv;
+                        for (int e = 0; e < 8; ++e) {
+                            const float cv = acc[i][2 * jj + (e >> 2)][e & 3];
+                            rv[e] = (T)cv;
                             float v = cv;
                             if (EPI) {
-                                v = fmaf(v, dsc[j][r], nv[i] + bsc[j][r]);
+                                v = fmaf(v, dd[e], nv + bb[e]);
                                 v = fmaxf(v, v * lr_alpha);
                                 v = __builtin_amdgcn_fmed3f(v, -clampv, clampv);
                             }
-                            yv[r] = (T)v;
-                            if (DOT) dacc[j][r] += (float)rv[r] * (float)dv[i][j][r];
+                            yv[e] = (T)v;
+                            if (DOT) dacc[jj][e] += (float)rv[e] * (float)dv[i][jj][e];
                         }
-                        *(vec4*)(y + dst) = yv;
-                        if (yr) *(vec4*)(yr + dst) = rv;
-                        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                        if (!(SG2_DIAG & 2)) {
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, (int)(dst * sizeof(T)), 0, 0);
+                            // a uniform (scalar) branch: a dropped store still costs its issue slot
+                            if (has_raw) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, (int)(dst * sizeof(T)), 0, 0);
+                        } else if (yv[0] == (T)12345.f && rv[1] == (T)-7.f) {
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, (int)(dst * sizeof(T)), 0, 0);
+                        }
                     }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
                 }
-                if (DOT) {
-                    // sum over the 16 lanes holding the same channels (lane % 16 = pixel), one atomic each
+                if (DOT && (t + 1 == t_end || (t + 1) / per_n != n)) {
+                    // this run is done with sample n: sum over the 16 lanes holding the same channels
+                    // (lane % 16 = pixel), one atomic per channel and wave
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
+                    for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            float v = dacc[j][r];
+                        for (int e = 0; e < 8; ++e) {
+                            float v = dacc[jj][e];
                             v += __shfl_xor(v, 1);
                             v += __shfl_xor(v, 2);
                             v += __shfl_xor(v, 4);
                             v += __shfl_xor(v, 8);
-                            if ((lane & 15) == 0) atomicAdd(&a.dot_out[(int64_t)n * P_C + oq + j * 16 + r], v);
+                            if (l16 == 0) atomicAdd(&a.dot_out[(int64_t)n * P_C + jj * 32 + oq8 + e], v);
+                            dacc[jj][e] = 0.f;
                         }
                 }
             }
             sstore(c ^ 1);
+            if (c == 0 && EPI) {
+                nlds[tid] = (float)e_noise * ngain;
+                if (tid < P_C) dlds[tid] = a.out_scale ? e_d * dgain : dgain;
+            }
             __syncthreads();
         }
     }
@@ -596,7 +649,7 @@ int dispatch(Conv3Args& a, hipStream_t s) {
     if (persist && a.Cin == P_C && a.Cout == P_C && a.H % P_TH == 0 && a.W % P_TW == 0 &&
         (!epi || (a.gain > 0.f && (a.act == 0 || (a.alpha >= 0.f && a.alpha <= 1.f))))) {
         const int tiles = a.N * (a.H / P_TH) * (a.W / P_TW);
-        if (tiles >= 4 * num_cus()) {
+        if (tiles >= 2 * num_cus()) {
             const int grid = num_cus();
             if (si) { if (epi) return launch_c64p_dot<T, true, true>(a, s, tiles, grid); return launch_c64p_dot<T, true, false>(a, s, tiles, grid); }
             if (epi) return launch_c64p_dot<T, false, true>(a, s, tiles, grid);

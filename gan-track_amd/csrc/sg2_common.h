@@ -51,6 +51,9 @@ template <typename T>
 __device__ __forceinline__ T buf_load2(__amdgpu_buffer_rsrc_t r, int byte_off) {   // one 16-bit element
     return __builtin_bit_cast(T, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(r, byte_off, 0, 0));
 }
+__device__ __forceinline__ float buf_load4f(__amdgpu_buffer_rsrc_t r, int byte_off) {   // one f32
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
 template <typename vecT>
 __device__ __forceinline__ vecT buf_load8(__amdgpu_buffer_rsrc_t r, int byte_off) {   // 8 bytes
     return __builtin_bit_cast(vecT, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
