@@ -27,7 +27,12 @@ namespace {
 
 constexpr int CK = 32;              // input channels per chunk (= MFMA K)
 constexpr int BN = 64;              // output channels per workgroup
-constexpr int PX = CK + 8;          // LDS pixel / weight-row stride in elements (80 B)
+constexpr int PX = CK;              // LDS pixel / weight-row stride in elements (64 B, XOR-swizzled: swz64)
+
+// 16-byte piece q of LDS row p (a halo pixel or a weight row of one 32-channel chunk): a fragment read of
+// 16 consecutive rows then hits 16 distinct bank slots in each of ds_read_b128's lane groups for any
+// starting row (tools/lds_swizzle_check.py; the 80-byte padded rows used before conflicted 2-way).
+__device__ __forceinline__ int swz64(int p, int q) { return p * 64 + ((q ^ ((p >> 1) & 2)) << 4); }
 
 struct Conv3Args {
     const void* x;
@@ -61,7 +66,7 @@ __device__ __forceinline__ f32x4 mma(v8<T> a, v8<T> b, f32x4 c) {
 // NBUF = 2: double-buffered chunks (1 workgroup / CU); NBUF = 1: single buffer, 2 workgroups / CU
 // overlap each other's staging (better when Cin spans only a couple of chunks).
 template <typename T, int TW, bool SCALE_IN, bool EPI, int NBUF>
-__global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
+__global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a) {   // NBUF = 1: two workgroups per CU
     constexpr int TH = 256 / TW;
     constexpr int HW_ = TW + 2, HH = TH + 2, HP = HW_ * HH;          // halo pixels
     constexpr int HALO = HP * PX;                                      // elements per halo buffer
@@ -94,8 +99,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
         const int iy = ty0 - 1 + hy, ix = tx0 - 1 + hx;
         h_ok[i] = p < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
         h_src[i] = h_ok[i] ? ((n * a.H + iy) * a.W + ix) : 0;     // pixel index
-        h_dst[i] = (p < HP ? p : 0) * PX + q * 8;
-        if (p >= HP) h_dst[i] = -1;
+        h_dst[i] = p < HP ? swz64(p, q) : -1;      // byte offset
     }
     const int hq = (tid & 3) * 8;
     int w_src[NW], w_dst[NW];
@@ -107,7 +111,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
         const int tap = r / BN, o = r - tap * BN;
         w_ok[i] = o0 + o < a.Cout;
         w_src[i] = (w_ok[i] ? (o0 + o) : 0) * 9 + tap;              // row index in [Cout*9]
-        w_dst[i] = (tap * BN + o) * PX + (idx & 3) * 8;
+        w_dst[i] = swz64(tap * BN + o, idx & 3);   // byte offset
     }
 
     // Loads are unconditional (out-of-image / out-of-range lanes read a valid dummy address) and the
@@ -147,22 +151,22 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) v[j] = (T)((float)v[j] * (float)(T)scl[j]);
             }
-            *(vec8*)(hb + h_dst[i]) = v;
+            *(vec8*)((char*)hb + h_dst[i]) = v;
         }
 #pragma unroll
-        for (int i = 0; i < NW; ++i) *(vec8*)(wb + w_dst[i]) = rw[i];
+        for (int i = 0; i < NW; ++i) *(vec8*)((char*)wb + w_dst[i]) = rw[i];
     };
 
     // ---- per-lane fragment bases ----
-    const int ko = 8 * (lane >> 4);
-    int a_base[4];
+    const int lq = lane >> 4, l16 = lane & 15;
+    int a_pos[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int m = wave * 64 + i * 16 + (lane & 15);
+        const int m = wave * 64 + i * 16 + l16;
         const int py = m / TW, px = m - py * TW;
-        a_base[i] = (py * HW_ + px) * PX + ko;     // halo position of tap (0,0)
+        a_pos[i] = py * HW_ + px;                  // halo row of tap (0,0)
     }
-    const int b_base = (lane & 15) * PX + ko;
+    const int b_lane = swz64(l16, lq);             // + (tap * BN + j * 16) * 64: the same swizzle
 
     f32x4 acc[4][4];
 #pragma unroll
@@ -177,19 +181,18 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(Conv3Args a) {
         const int cur = NBUF == 2 ? (ch & 1) : 0;
         const bool more = ch + 1 < nchunks;
         if (more) gload(ch + 1);
-        const T* hb = smem + cur * (HALO + WTS);
-        const T* wb = hb + HALO;
+        const char* hb = (const char*)(smem + cur * (HALO + WTS));
+        const char* wb = hb + HALO * sizeof(T) + b_lane;
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
-                const int toff = (ky * HW_ + kx) * PX;
                 const int tap = ky * 3 + kx;
                 v8<T> af[4], bfr[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) af[i] = *(const v8<T>*)(hb + a_base[i] + toff);
+                for (int i = 0; i < 4; ++i) af[i] = *(const v8<T>*)(hb + swz64(a_pos[i] + ky * HW_ + kx, lq));
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bfr[j] = *(const v8<T>*)(wb + tap * BN * PX + j * 16 * PX + b_base);
+                for (int j = 0; j < 4; ++j) bfr[j] = *(const v8<T>*)(wb + (tap * BN + j * 16) * 64);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll

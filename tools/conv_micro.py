@@ -56,6 +56,8 @@ for sh in args.shapes.split(','):
         out.append(f'halo+mod {ms:.3f}ms')
         ms = timeit(lambda: cg.conv3x3_fused(x, wp, C, out_scale=d_, noise=nz_, noise_gain=0.1, bias=b_, act=1, gain=1.41, clamp=256.0), args.reps)
         out.append(f'halo+epi {ms:.3f}ms')
+        ms = timeit(lambda: cg.conv3x3_fused(x, wp, C, out_scale=d_, dot_src=x), args.reps)
+        out.append(f'halo+scale+dot {ms:.3f}ms')
     if 'generic' in args.which:
         ms = timeit(lambda: cg._conv_raw(x, wp, C, res, res, 3, 3, 1, (1, 1), False), args.reps)
         out.append(f'generic {ms:.3f}ms {flops / ms / 1e9:.0f}TF')
