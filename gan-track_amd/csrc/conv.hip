@@ -85,7 +85,13 @@ template <> struct Traits<float> {
 template <typename T, bool S3> struct KStage { static constexpr int BK = Traits<T>::BK; };
 template <> struct KStage<float, true> { static constexpr int BK = 32; };
 
-constexpr int S3LD = 32 + 8;          // bf16 plane row pitch (elements, 80 B: conflict-free b128 reads)
+constexpr int S3LD = 32;              // bf16 plane row pitch (elements, 64 B rows, XOR-swizzled: swz64)
+
+// 16-byte piece q of a 64-byte LDS row r (one 32-element K slice of an A or B tile row): fragment reads of
+// 16 consecutive rows hit 16 distinct bank slots in each of ds_read_b128's lane groups
+// (tools/lds_swizzle_check.py; the 80-byte padded rows used before conflicted 2-way, SQ_LDS_BANK_CONFLICT
+// ~45% of LDS cycles, profiles/r02_v2_pmc_diag.txt).
+__device__ __forceinline__ int swz64(int r, int q) { return r * 64 + ((q ^ ((r >> 1) & 2)) << 4); }
 
 // x = h + m + l, three bf16 pieces (exact for normal f32; round-to-nearest at each step)
 __device__ __forceinline__ void split3(float x, bf16_t& h, bf16_t& m, bf16_t& l) {
@@ -321,7 +327,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
     constexpr int LPR = BK / V;          // lanes per tile row
     constexpr int RPP = 256 / LPR;       // rows per load pass
     constexpr int PA = BM / RPP, PB = BN / RPP;
-    constexpr int LDK = BK + V;          // padded LDS row (16 B pad)
+    constexpr int LDK = sizeof(T) == 2 ? BK : BK + V;   // 16-bit: 64-byte swizzled rows; f32: padded rows
     constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
     typedef typename Loader<T, VEC>::vecT vecT;
 
@@ -424,7 +430,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
     auto store3 = [&](int buf, int r, const vecT& v) {
         bf16x4_t h, m, l;
         split3x4((float)v[0], (float)v[1], (float)v[2], (float)v[3], h, m, l);
-        bf16_t* p = lds3 + buf * BUF3 + r * S3LD + lcol;
+        bf16_t* p = (bf16_t*)((char*)(lds3 + buf * BUF3) + swz64(r, lcol >> 3) + (lcol & 7) * 2);
         *(bf16x4_t*)p = h;
         *(bf16x4_t*)(p + PLANE) = m;
         *(bf16x4_t*)(p + 2 * PLANE) = l;
@@ -440,12 +446,14 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
                 for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * rsc[i][j]);
             }
             if constexpr (S3) store3(buf, lrow + i * RPP, v);
+            else if constexpr (sizeof(T) == 2) *(vecT*)((char*)As + swz64(lrow + i * RPP, lcol >> 3)) = v;
             else *(vecT*)(As + (lrow + i * RPP) * LDK + lcol) = v;
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
             const vecT v = VEC ? rb[i] : Loader<T, VEC>::mask(rb[i], cur_c, a.Cin, rb_ok[i]);
             if constexpr (S3) store3(buf, BM + lrow + i * RPP, v);
+            else if constexpr (sizeof(T) == 2) *(vecT*)((char*)Bs + swz64(lrow + i * RPP, lcol >> 3)) = v;
             else *(vecT*)(Bs + (lrow + i * RPP) * LDK + lcol) = v;
         }
     };
@@ -460,17 +468,17 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
         const T* As = lds + cur * BUF + (wm * WM) * LDK;
         const T* Bs = lds + cur * BUF + BM * LDK + (wn * WN) * LDK;
         if constexpr (S3) {
-            const bf16_t* P = lds3 + cur * BUF3;
-            const int ko = 8 * (lane >> 4);
+            const char* P = (const char*)(lds3 + cur * BUF3);
+            const int fl = swz64(lane & 15, lane >> 4);          // + 64 * (16-aligned row): the same swizzle
             bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
-                    af[i][q] = *(const bf16x8*)(P + q * PLANE + (wm * WM + i * 16 + (lane & 15)) * S3LD + ko);
+                    af[i][q] = *(const bf16x8*)(P + q * PLANE * 2 + (wm * WM + i * 16) * 64 + fl);
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    bfr[j][q] = *(const bf16x8*)(P + q * PLANE + (BM + wn * WN + j * 16 + (lane & 15)) * S3LD + ko);
+                    bfr[j][q] = *(const bf16x8*)(P + q * PLANE * 2 + (BM + wn * WN + j * 16) * 64 + fl);
             }
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -491,13 +499,13 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
             }
         } else {
-            const int ko = 8 * (lane >> 4);
+            const int fl = swz64(lane & 15, lane >> 4);          // rows 16-aligned: the same swizzle
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = mfma16<T>(As + (i * 16 + (lane & 15)) * LDK + ko,
-                                          Bs + (j * 16 + (lane & 15)) * LDK + ko, acc[i][j]);
+                    acc[i][j] = mfma16<T>((const T*)((const char*)As + i * 16 * 64 + fl),
+                                          (const T*)((const char*)Bs + j * 16 * 64 + fl), acc[i][j]);
         }
     };
     if (k_begin < k_end) {
@@ -705,7 +713,7 @@ template <typename T, int BM, int BN, bool S3>
 size_t fwd_lds_bytes() {
     constexpr int BK = Traits<T>::BK, V = Traits<T>::V;
     if (S3) return 3 * (size_t)(BM + BN) * S3LD * sizeof(bf16_t);   // one buffer (conv_fwd_kernel S3 loop)
-    const size_t main = 2 * (size_t)(BM + BN) * (BK + V) * sizeof(T);
+    const size_t main = 2 * (size_t)(BM + BN) * (sizeof(T) == 2 ? BK : BK + V) * sizeof(T);
     const size_t epi = std::is_same<T, float>::value ? 0 : 2 * (size_t)BM * (64 + 8) * sizeof(T) + 64 * sizeof(float);
     return std::max(main, epi);
 }

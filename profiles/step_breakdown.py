@@ -6,19 +6,25 @@ from collections import defaultdict
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
 ms = float(sys.argv[2])
+# the roofline measures 23 launches of the 256^2 layer (the persistent C=64 kernel since r02; the halo
+# kernel before) then 23 of the 32^2 layer (halo kernel) at the end of the run
+c64 = [r for r in rows if 'conv3x3_c64p' in r['Kernel_Name']]
 halo = [r for r in rows if 'conv3x3_halo' in r['Kernel_Name']]
-t_end = int(halo[-23 - 23]['Start_Timestamp']) if len(halo) > 46 else int(halo[0]['Start_Timestamp'])
-# the roofline measures 23 launches of the 256^2 layer then 23 of the 32^2 layer at the end of the run
+if len(c64) > 23:
+    t_end = int(c64[-23]['Start_Timestamp'])
+else:
+    t_end = int(halo[-23 - 23]['Start_Timestamp']) if len(halo) > 46 else int(halo[0]['Start_Timestamp'])
 t0 = t_end - int(16 * ms * 1e6)
 win = [r for r in rows if t0 <= int(r['Start_Timestamp']) < t_end]
 
 
 def cat(n):
-    for key, name in [('conv3x3_halo', 'halo conv 16-bit'), ('wgrad3x3', 'halo wgrad 16-bit'),
+    for key, name in [('conv3x3_c64p', 'halo conv 16-bit C=64 persistent'), ('conv3x3_halo', 'halo conv 16-bit'), ('wgrad3x3', 'halo wgrad 16-bit'),
                       ('conv_fwd_kernel<float', 'generic conv f32'), ('conv_fwd_kernel', 'generic conv 16-bit'),
                       ('conv_wgrad_kernel<float', 'generic wgrad f32'), ('conv_wgrad_kernel', 'generic wgrad 16-bit'),
                       ('layer_bwd', 'layer_bwd'), ('bias_act', 'bias_act'), ('demod', 'demod'), ('Cijk', 'GEMM'),
                       ('conv_finalize', 'conv finalize'), ('rocclr', 'memset/copy'), ('multi_tensor', 'optimizer'),
+                      ('adam_multi', 'optimizer'), ('lerp_multi', 'optimizer'),
                       ('pack_weight', 'weight pack'), ('infnorm', 'fp16 pre-normalisation')]:
         if key in n:
             return name
