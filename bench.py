@@ -287,7 +287,7 @@ def main():
         cpu = cpu_baseline(args)
     if rank == 0:
         line = {
-            'metric': 'imgs/sec at 256^2 bs32/GPU StyleGAN2-ADA training (+ sec/kimg)',
+            'metric': f'imgs/sec at {args.res}^2 bs{args.batch_gpu}/GPU StyleGAN2-ADA training (+ sec/kimg)',
             'value': round(value, 3), 'unit': 'imgs/s', 'n_gpus': num_gpus, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
             'graphs': graphs,
