@@ -765,6 +765,7 @@ struct WgradArgs {
     int M;           // N*OH*OW
     int kper;        // pixels per split (multiple of BK)
     int splits;
+    float alpha;     // dw += alpha * (partial sums): a layer's weight gain folded in
 };
 
 template <typename T>
@@ -826,7 +827,7 @@ __global__ __launch_bounds__(256) void wgrad1x1_smallb_kernel(WgradArgs a) {
         for (int k = 0; k < 4; ++k)
             if (k < a.B) atomicAdd(&red[(a0 + j) * a.B + k], acc[j][k]);
     __syncthreads();
-    for (int i = threadIdx.x; i < a.A * a.B; i += 256) atomicAdd(a.dw + i, red[i]);
+    for (int i = threadIdx.x; i < a.A * a.B; i += 256) atomicAdd(a.dw + i, red[i] * a.alpha);
 }
 
 // Mirror for a tiny output depth (A <= 4, toRGB): the lane owns 8 input channels b of the wide x.
@@ -873,7 +874,7 @@ __global__ __launch_bounds__(256) void wgrad1x1_smalla_kernel(WgradArgs a) {
         for (int j = 0; j < 8; ++j)
             if (k < a.A) atomicAdd(&red[k * a.B + b0 + j], acc[k][j]);
     __syncthreads();
-    for (int i = threadIdx.x; i < a.A * a.B; i += 256) atomicAdd(a.dw + i, red[i]);
+    for (int i = threadIdx.x; i < a.A * a.B; i += 256) atomicAdd(a.dw + i, red[i] * a.alpha);
 }
 
 template <typename T, int BM, int BN, bool VEC, bool S3>
@@ -1117,7 +1118,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int bc = b0 + wn * WN + j * 16 + (lane & 15);
-                if (bc < a.B) atomicAdd(a.dw + ((int64_t)ar * KK + tap) * a.B + bc, acc[i][j][r]);
+                if (bc < a.B) atomicAdd(a.dw + ((int64_t)ar * KK + tap) * a.B + bc, acc[i][j][r] * a.alpha);
             }
         }
 }
@@ -1152,7 +1153,7 @@ int floordiv_h(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 bool wgrad_halo_ok(int dtype, int KH, int KW, int stride, int pad_y, int pad_x, int OW, int A, int B);
 int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale, const float* xscale, int dtype,
                     int N, int A, int OH, int OW, int B, int H, int W, int KH, int KW, int stride, int pad_y,
-                    int pad_x, hipStream_t s);
+                    int pad_x, float alpha, hipStream_t s);
 }  // namespace sg2
 
 extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
@@ -1313,7 +1314,7 @@ extern "C" int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int 
 
 extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
                                 int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* g_scale,
-                                const float* x_scale, void* stream) {
+                                const float* x_scale, float alpha, void* stream) {
     using namespace sg2;
     SG2_CHECK(dw && g && x, "sg2_conv2d_wgrad: null pointer");
     SG2_CHECK(N > 0 && A > 0 && B > 0 && OH > 0 && OW > 0 && H > 0 && W > 0, "sg2_conv2d_wgrad: empty shape");
@@ -1326,7 +1327,7 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     WgradArgs a{};
     a.g = g; a.x = x; a.dw = dw; a.b_scale = x_scale; a.a_scale = g_scale;
     a.N = N; a.A = A; a.OH = OH; a.OW = OW; a.B = B; a.H = H; a.W = W; a.KH = KH; a.KW = KW;
-    a.stride = stride; a.pady = pad_y; a.padx = pad_x;
+    a.stride = stride; a.pady = pad_y; a.padx = pad_x; a.alpha = alpha;
     a.M = N * OH * OW;
     if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W && B <= 4 &&
         A % 8 == 0 && 256 % (A / 8) == 0 && A * B <= 2048 && (uintptr_t)g % 16 == 0) {
@@ -1343,7 +1344,7 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     const bool halo = wgrad_halo_ok(dtype, KH, KW, stride, pad_y, pad_x, OW, A, B) && (uintptr_t)x % 16 == 0 &&
                       (uintptr_t)g % 16 == 0;
     if (halo) return wgrad3x3_launch(dw, g, x, g_scale, x_scale, dtype, N, A, OH, OW, B, H, W, KH, KW, stride, pad_y,
-                                     pad_x, s);
+                                     pad_x, alpha, s);
     int rc = 0;
     SG2_DISPATCH(dtype, T, {
         constexpr int V = Traits<T>::V;

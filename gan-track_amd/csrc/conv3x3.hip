@@ -678,6 +678,172 @@ int dispatch(Conv3Args& a, hipStream_t s) {
 #undef L3
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Stride-2 transposed 3x3 convolution, padding 0 (conv2d_resample's up-2 plan, conv2d_resample.py:112-129:
+// the G up layers' conv_transpose2d, and the input gradient of the D down layers' stride-2 conv):
+//   y[n, 2i + ky, 2j + kx, o] += sum_c x[n, i, j, c] (* s[n, c]) W[o][ky][kx][c],   y: (2H+1) x (2W+1)
+// The generic implicit GEMM runs this as four output phases, each a separate GEMM of 1, 2, 2 or 4 taps:
+// the input is fetched once per phase and a phase's K is only taps x Cin, so its workgroups are bound by
+// prologue and epilogue.  Here a workgroup owns a 16 x 8 tile of output CELLS (cell (i, j) = the 2 x 2
+// output pixels 2i + py, 2j + px) x 64 output channels: per 32-channel chunk it stages the 17 x 9 input
+// halo (cell (i, j) reads inputs (i - 1 .. i, j - 1 .. j)) and the chunk's 9 x 64 x 32 weights once, and
+// every wave accumulates all nine taps into the four phase accumulators of its 2 x 16 cells:
+//   per tap: 2 pixel and 4 weight fragments, 8 MFMAs into phase (ky & 1, kx & 1).
+// LDS rows are the swizzled 64-byte rows of swz64.  The epilogue transposes each phase through LDS and
+// stores whole 128-byte pixel lines (64 channels).  Two workgroups per CU, single-buffered LDS (the same
+// staging discipline as conv3x3_halo_kernel NBUF = 1).
+constexpr int U_TW = 16, U_TH = 8, U_CELLS = U_TW * U_TH;              // 128 cells
+constexpr int U_HW = U_TW + 1, U_HH = U_TH + 1, U_HP = U_HW * U_HH;   // 17 x 9 = 153 input positions
+constexpr int U_HB = ((U_HP * 64 + 255) / 256) * 256;                  // halo bytes (256-aligned: swz64)
+constexpr int U_WB = 9 * BN * 64;                                      // weight bytes per chunk
+constexpr int U_OS = BN + 8;                                           // epilogue tile row (elements)
+constexpr size_t U_LDS = (size_t)U_HB + U_WB;                          // 46,848 B
+static_assert((size_t)U_CELLS * U_OS * 2 <= U_LDS, "epilogue tile fits the staging buffer");
+
+template <typename T, bool SCALE_IN>
+__global__ __launch_bounds__(256, 2) void conv3x3_up2_kernel(Conv3Args a) {
+    constexpr int NH = (U_HP * 4 + 255) / 256;                // halo 16-B loads per thread (3)
+    constexpr int NW = (9 * BN * 4) / 256;                    // weight 16-B loads per thread (9)
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    char* hl = smem_raw;                                      // [153 rows] x 64 B
+    char* wl = smem_raw + U_HB;                               // [9 taps][64 rows] x 64 B
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int per_n = a.tiles_x * a.tiles_y;
+    const int n = blockIdx.x / per_n, tr = blockIdx.x - n * per_n;
+    const int i0 = (tr / a.tiles_x) * U_TH, j0 = (tr % a.tiles_x) * U_TW;   // first cell of the tile
+    const int o0 = blockIdx.y * BN;
+    const int OH = 2 * a.H + 1, OW = 2 * a.W + 1;
+    const int nchunks = a.Cin / CK;
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(a.x, (int64_t)a.N * a.H * a.W * a.Cin * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rwb = make_rsrc(a.w, (int64_t)a.Cout * 9 * a.Cin * (int64_t)sizeof(T));
+    const int hq = (tid & 3) * 8;
+
+    vec8 rh[NH], rw[NW];
+    float4 sc0, sc1;
+    auto gload = [&](int chunk) {
+        const int c = chunk * CK + hq;
+#pragma unroll
+        for (int k = 0; k < NH; ++k) {
+            const int p = (tid + k * 256) >> 2;
+            const int iy = i0 - 1 + p / U_HW, ix = j0 - 1 + p % U_HW;
+            const bool ok = (p < U_HP) & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W);
+            rh[k] = buf_load16<vec8>(rxb, ok ? (((n * a.H + iy) * a.W + ix) * a.Cin + c) * (int)sizeof(T) : -1);
+        }
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const int r = (tid + k * 256) >> 2, tap = r / BN, o = r - tap * BN;
+            rw[k] = buf_load16<vec8>(rwb, o0 + o < a.Cout ? (((o0 + o) * 9 + tap) * a.Cin + c) * (int)sizeof(T) : -1);
+        }
+        if (SCALE_IN) {
+            const float* sc = a.in_scale + (int64_t)n * a.Cin + c;
+            sc0 = *(const float4*)sc;
+            sc1 = *(const float4*)(sc + 4);
+        }
+    };
+    auto sstore = [&]() {
+        const float scl[8] = {sc0.x, sc0.y, sc0.z, sc0.w, sc1.x, sc1.y, sc1.z, sc1.w};
+#pragma unroll
+        for (int k = 0; k < NH; ++k) {
+            const int p = (tid + k * 256) >> 2;
+            if (k * 256 + 256 > U_HP * 4 && p >= U_HP) continue;   // the ragged last round only
+            vec8 v = rh[k];
+            if (SCALE_IN) {   // x * s.to(x.dtype) (networks_stylegan2.py:69): s rounded first, one rounding after
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = (T)((float)v[e] * (float)(T)scl[e]);
+            }
+            *(vec8*)(hl + swz64(p, tid & 3)) = v;
+        }
+#pragma unroll
+        for (int k = 0; k < NW; ++k) *(vec8*)(wl + swz64((tid + k * 256) >> 2, tid & 3)) = rw[k];
+    };
+
+    const int lq = lane >> 4, l16 = lane & 15;
+    const int b_lane = swz64(l16, lq);                        // + (tap * 64 + j * 16) * 64: the same swizzle
+    f32x4 acc[4][2][4];                                       // [phase (ky & 1) * 2 + (kx & 1)][cell row][co tile]
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[f][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    gload(0);
+    sstore();
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const bool more = ch + 1 < nchunks;
+        if (more) gload(ch + 1);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const int tap = ky * 3 + kx, ph = (ky & 1) * 2 + (kx & 1);
+                v8<T> af[2], bfr[4];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    // cell row 2w + i reads input row (cell row + 1 - ky / 2) of the halo
+                    const int pos = (2 * wave + i + 1 - (ky >> 1)) * U_HW + l16 + 1 - (kx >> 1);
+                    af[i] = *(const v8<T>*)(hl + swz64(pos, lq));
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bfr[j] = *(const v8<T>*)(wl + b_lane + (tap * BN + j * 16) * 64);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[ph][i][j] = mma<T>(af[i], bfr[j], acc[ph][i][j]);
+            }
+        }
+        if (more) {
+            __syncthreads();                                  // everyone done reading before the overwrite
+            sstore();
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: per phase, the 128 x 64 tile through LDS, whole 128-byte pixel lines out ----
+    T* ot = (T*)smem_raw;                                     // [128 cells][U_OS]
+    T* y = (T*)a.y;
+    const int c8 = (tid & 7) * 8;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+        const int py = ph >> 1, px = ph & 1;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = (2 * wave + i) * U_TW + 4 * lq + r;     // cell of accumulator row 4 lq + r
+#pragma unroll
+                for (int j = 0; j < 4; ++j) ot[m * U_OS + j * 16 + l16] = (T)acc[ph][i][j][r];
+            }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {                         // 128 cells x 8 channel vectors / 256 threads
+            const int m = (tid >> 3) + k * 32;
+            const int oy = 2 * (i0 + m / U_TW) + py, ox = 2 * (j0 + m % U_TW) + px;
+            if (oy < OH && ox < OW && o0 + c8 < a.Cout)
+                *(vec8*)(y + (((int64_t)n * OH + oy) * OW + ox) * a.Cout + o0 + c8) = *(const vec8*)(ot + m * U_OS + c8);
+        }
+        __syncthreads();
+    }
+}
+
+template <typename T, bool SI>
+int launch_up2(Conv3Args& a, hipStream_t s) {
+    auto kern = conv3x3_up2_kernel<T, SI>;
+    static bool attr_set = false;   // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)U_LDS);
+        attr_set = true;
+    }
+    a.tiles_x = (a.W + 1 + U_TW - 1) / U_TW;
+    a.tiles_y = (a.H + 1 + U_TH - 1) / U_TH;
+    dim3 grid(a.N * a.tiles_x * a.tiles_y, (a.Cout + BN - 1) / BN);
+    kern<<<grid, 256, U_LDS, s>>>(a);
+    return launch_status("sg2_conv3x3_up2");
+}
+
 }  // namespace
 }  // namespace sg2
 
@@ -702,4 +868,23 @@ extern "C" int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, i
     hipStream_t s = as_stream(stream);
     if (dtype == SG2_F16) return dispatch<f16_t>(a, s);
     return dispatch<bf16_t>(a, s);
+}
+
+extern "C" int sg2_conv3x3_up2(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W, int Cout,
+                               const float* in_scale, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(y && x && w, "sg2_conv3x3_up2: null pointer");
+    SG2_CHECK(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "sg2_conv3x3_up2: empty shape");
+    SG2_CHECK(dtype == SG2_F16 || dtype == SG2_BF16, "sg2_conv3x3_up2: f16/bf16 only");
+    SG2_CHECK(Cin % CK == 0 && Cout % 8 == 0, "sg2_conv3x3_up2: Cin must be a multiple of 32, Cout of 8");
+    SG2_CHECK(((uintptr_t)x % 16) == 0 && ((uintptr_t)w % 16) == 0 && ((uintptr_t)y % 16) == 0,
+              "sg2_conv3x3_up2: 16-byte alignment required");
+    SG2_CHECK((int64_t)N * H * W * Cin * 2 < INT32_MAX && (int64_t)Cout * 9 * Cin * 2 < INT32_MAX,
+              "sg2_conv3x3_up2: tensor too large (32-bit byte offsets of the buffer loads)");
+    Conv3Args a{};
+    a.x = x; a.w = w; a.y = y; a.in_scale = in_scale;
+    a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
+    hipStream_t s = as_stream(stream);
+    if (dtype == SG2_F16) return in_scale ? launch_up2<f16_t, true>(a, s) : launch_up2<f16_t, false>(a, s);
+    return in_scale ? launch_up2<bf16_t, true>(a, s) : launch_up2<bf16_t, false>(a, s);
 }

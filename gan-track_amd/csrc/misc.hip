@@ -160,13 +160,19 @@ __global__ __launch_bounds__(256) void lerp_multi_kernel(const int64_t* __restri
 // latency-bound.  Replaces the strided-permute copy of _pack_conv / _pack_convT.
 template <typename Tin, typename Tout>
 __global__ __launch_bounds__(256) void pack_weight_kernel(Tout* __restrict__ out, const Tin* __restrict__ in, int A,
-                                                          int B, int K, int64_t sa, int64_t sb, int64_t sk, int flip) {
+                                                          int B, int K, int64_t sa, int64_t sb, int64_t sk, int flip,
+                                                          float scale) {
     const unsigned e = blockIdx.x * 256u + threadIdx.x;      // 32-bit index math (A*B*K < 2^31, host-checked)
     if (e >= (unsigned)A * B * K) return;
     const unsigned r = e / (unsigned)B, b = e - r * B;
     const unsigned a = r / (unsigned)K, k = r - a * K;
     const int kk = flip ? K - 1 - (int)k : (int)k;
-    out[e] = from_f32<Tout>(to_f32(in[(int64_t)a * sa + (int64_t)b * sb + kk * sk]));
+    // (weight * gain).to(dtype): one f32 product, one rounding -- as the reference's `self.weight * self.weight_gain`
+    // (the empty asm keeps the f32 product: fmul + fptrunc would otherwise become one v_fma_mix with a
+    // single rounding, not torch's f32 product then cast)
+    float v = to_f32(in[(int64_t)a * sa + (int64_t)b * sb + kk * sk]) * scale;
+    asm volatile("" : "+v"(v));
+    out[e] = from_f32<Tout>(v);
 }
 
 // Row-wise infinity-norm pre-normalisation of the fp16 modulated layers (networks_stylegan2.py:52-54):
@@ -280,7 +286,7 @@ extern "C" int sg2_lerp_multi(const int64_t* seg, const int64_t* blocks, int nbl
 }
 
 extern "C" int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_dtype, int A, int B, int K,
-                               int64_t sa, int64_t sb, int64_t sk, int flip, void* stream) {
+                               int64_t sa, int64_t sb, int64_t sk, int flip, float scale, void* stream) {
     using namespace sg2;
     SG2_CHECK(out && in, "sg2_pack_weight: null pointer");
     SG2_CHECK(A > 0 && B > 0 && K >= 1 && K <= 9 && (int64_t)A * B * K < (1LL << 31),
@@ -288,7 +294,7 @@ extern "C" int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_
     const unsigned grid = (unsigned)cdiv((int64_t)A * B * K, 256);
     hipStream_t s = as_stream(stream);
     SG2_DISPATCH(in_dtype, Tin, SG2_DISPATCH(out_dtype, Tout,
-        pack_weight_kernel<Tin, Tout><<<grid, 256, 0, s>>>((Tout*)out, (const Tin*)in, A, B, K, sa, sb, sk, flip)));
+        pack_weight_kernel<Tin, Tout><<<grid, 256, 0, s>>>((Tout*)out, (const Tin*)in, A, B, K, sa, sb, sk, flip, scale)));
     return launch_status("sg2_pack_weight");
 }
 

@@ -54,6 +54,7 @@ struct W3Args {
     int S, PY, PX;        // stride and phase: x coordinate = (g coordinate + shift) * S + phase
     int tiles_x, tiles_y, tiles;
     int tiles_per_block;
+    float alpha;          // dw += alpha * partial sums (a layer's weight gain)
     PTap taps[9];
 };
 
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
             if (ar >= a.A) continue;
 #pragma unroll
             for (int t = 0; t < NT; ++t)
-                atomicAdd(a.dw + ((int64_t)ar * a.KK + a.taps[t].out) * a.B + b, acc[t][j]);
+                atomicAdd(a.dw + ((int64_t)ar * a.KK + a.taps[t].out) * a.B + b, acc[t][j] * a.alpha);
         }
     }
 }
@@ -242,9 +243,9 @@ bool wgrad_halo_ok(int dtype, int KH, int KW, int stride, int pad_y, int pad_x, 
 // dw already zeroed.  One launch per output phase that has taps.
 int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale, const float* xscale, int dtype,
                     int N, int A, int OH, int OW, int B, int H, int W, int KH, int KW, int stride, int pad_y,
-                    int pad_x, hipStream_t s) {
+                    int pad_x, float alpha, hipStream_t s) {
     W3Args a{};
-    a.g = g; a.x = x; a.gscale = gscale; a.xscale = xscale; a.dw = dw;
+    a.g = g; a.x = x; a.gscale = gscale; a.xscale = xscale; a.dw = dw; a.alpha = alpha;
     a.N = N; a.GH = OH; a.GW = OW; a.XH = H; a.XW = W; a.A = A; a.B = B; a.KK = KH * KW; a.S = stride;
     const int TW = OW >= 32 ? 32 : 16;
     a.tiles_x = (int)cdiv(OW, TW);

@@ -55,8 +55,30 @@ def _nhwc(t):
 _WS_LIMIT = 1 << 23  # split-K f32 workspace only for small outputs (low-resolution layers)
 
 
+def _up2_ok(x, cout, oh, ow, kh, kw, stride, pad, transpose):
+    """sg2_conv3x3_up2 serves the 16-bit stride-2 transposed 3x3 convs with padding 0 (output 2H+1) from 64^2
+    inputs up; below, its 16 x 8 cell tiles are mostly empty (17 x 17 cells at 16^2) and the four-phase
+    implicit GEMM is faster (tools/up2_ab.py: 128^2 -> 257^2 C 128 -> 64: 0.168 vs 0.264 ms; 64^2 C 256 -> 128:
+    0.152 vs 0.181 ms; 32^2 C 512 -> 256: 0.163 vs 0.143 ms)."""
+    n, cin, h, w = x.shape
+    return (transpose and stride == 2 and kh == 3 and kw == 3 and tuple(pad) == (0, 0) and oh == 2 * h + 1 and
+            ow == 2 * w + 1 and x.dtype in (torch.float16, torch.bfloat16) and cin % 32 == 0 and cout % 8 == 0 and
+            h >= 64 and w >= 64)
+
+
+def _conv_up2(x, wp, cout, in_scale=None):
+    n, cin, h, w = x.shape
+    y = torch.empty([n, cout, 2 * h + 1, 2 * w + 1], dtype=x.dtype, device=x.device, memory_format=_CL)
+    _hip.check(_hip.lib().sg2_conv3x3_up2(
+        _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, _hip.ptr(in_scale),
+        _hip.stream_ptr(x.device)), 'sg2_conv3x3_up2')
+    return y
+
+
 def _conv_raw(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose):
     """x [N,Cin,H,W] (NHWC memory), wp packed [Cout][kh][kw][Cin] -> y [N,Cout,oh,ow] (NHWC memory)."""
+    if _up2_ok(x, cout, oh, ow, kh, kw, stride, pad, transpose):
+        return _conv_up2(x, wp, cout)
     n, cin, h, w = x.shape
     y = torch.empty([n, cout, oh, ow], dtype=x.dtype, device=x.device, memory_format=_CL)
     total = n * cout * oh * ow
@@ -74,6 +96,9 @@ def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_sca
     """sg2_conv2d_fused: y = round(clamp(act(conv(x * in_scale, w) * out_scale + noise * g + bias) * gain))
     + residual.  Returns (y, aux) with aux = conv result (aux_mode 1) or activation (aux_mode 2); with
     dot_src also dot[n, o] = sum_p conv(...)[n, o, p] * dot_src[n, o, p] -> (y, aux, dot)."""
+    if (out_scale is None and noise is None and bias is None and residual is None and dot_src is None and act == 0 and
+            gain == 1.0 and clamp < 0 and not aux_mode and _up2_ok(x, cout, oh, ow, kh, kw, stride, pad, transpose)):
+        return _conv_up2(x, wp, cout, in_scale), None
     n, cin, h, w = x.shape
     y = torch.empty([n, cout, oh, ow], dtype=x.dtype, device=x.device, memory_format=_CL)
     aux = torch.empty_like(y) if aux_mode else None
@@ -100,25 +125,27 @@ def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_sca
     return (y, aux, dot) if dot_src is not None else (y, aux)
 
 
-def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None):
-    """dw[a, b, ky, kx] = sum g[n,a,oy,ox] (* g_scale[n,a]) x[n,b,oy*s+ky-p,ox*s+kx-p] (* x_scale[n,b]);
-    returns f32 [A,B,kh,kw] (NHWC-packed)."""
+def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None, alpha=1.0):
+    """dw[a, b, ky, kx] = alpha * sum g[n,a,oy,ox] (* g_scale[n,a]) x[n,b,oy*s+ky-p,ox*s+kx-p] (* x_scale[n,b]);
+    returns f32 [A,B,kh,kw] (NHWC-packed).  alpha: a layer's weight gain (the backward of w * gain)."""
     n, a, oh, ow = g.shape
     _, b, h, w = x.shape
     dw = torch.empty([a, kh, kw, b], dtype=torch.float32, device=g.device)
     _hip.check(_hip.lib().sg2_conv2d_wgrad(
         _hip.ptr(dw), _hip.ptr(g), _hip.ptr(x), _hip.dtype_code(g), n, a, oh, ow, b, h, w, kh, kw, stride,
-        pad[0], pad[1], _hip.ptr(g_scale), _hip.ptr(x_scale), _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad')
+        pad[0], pad[1], _hip.ptr(g_scale), _hip.ptr(x_scale), float(alpha), _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad')
     return dw.permute(0, 3, 1, 2)
 
 
-def _pack(w, a_dim, dtype, flip):
-    """out[a][ky][kx][b] = w[.., ky', kx'] with (a, b) = dims (a_dim, 1 - a_dim) of w, cast to dtype, the
-    taps reversed when flip -- one sg2_pack_weight launch (LDS-tiled transpose) instead of a strided copy."""
+def _pack(w, a_dim, dtype, flip, scale=1.0):
+    """out[a][ky][kx][b] = scale * w[.., ky', kx'] with (a, b) = dims (a_dim, 1 - a_dim) of w, cast to dtype,
+    the taps reversed when flip -- one sg2_pack_weight launch instead of a strided copy (and, with scale, of
+    the reference's `weight * weight_gain` multiply)."""
     b_dim = 1 - a_dim
     A, B, kh, kw = w.shape[a_dim], w.shape[b_dim], w.shape[2], w.shape[3]
     if kh * kw > 9:    # no such conv in the networks; layout copy on the device
         w = w.flip([2, 3]) if flip else w
+        w = w * scale if scale != 1.0 else w
         return w.permute(a_dim, 2, 3, b_dim).to(dtype or w.dtype, memory_format=torch.contiguous_format)
     if w.stride(2) != kw * w.stride(3):
         w = w.contiguous()
@@ -126,16 +153,16 @@ def _pack(w, a_dim, dtype, flip):
     _hip.require_device(w)
     _hip.check(_hip.lib().sg2_pack_weight(
         _hip.ptr(out), _hip.dtype_code(out), _hip.ptr(w), _hip.dtype_code(w), A, B, kh * kw, w.stride(a_dim),
-        w.stride(b_dim), w.stride(3), 1 if flip else 0, _hip.stream_ptr(w.device)), 'sg2_pack_weight')
+        w.stride(b_dim), w.stride(3), 1 if flip else 0, float(scale), _hip.stream_ptr(w.device)), 'sg2_pack_weight')
     return out
 
 
-def _pack_conv(w, dtype=None, flip=False):      # [O, I, kh, kw] -> [O][kh][kw][I], cast to dtype in the same pass
-    return _pack(w, 0, dtype, flip)
+def _pack_conv(w, dtype=None, flip=False, scale=1.0):   # [O, I, kh, kw] -> [O][kh][kw][I], cast (and scaled) in one pass
+    return _pack(w, 0, dtype, flip, scale)
 
 
-def _pack_convT(w, dtype=None, flip=False):     # [I, O, kh, kw] -> [O][kh][kw][I]
-    return _pack(w, 1, dtype, flip)
+def _pack_convT(w, dtype=None, flip=False, scale=1.0):  # [I, O, kh, kw] -> [O][kh][kw][I]
+    return _pack(w, 1, dtype, flip, scale)
 
 
 def _halo_ok(x, kh, kw, stride, pad, out_hw):

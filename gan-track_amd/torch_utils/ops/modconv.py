@@ -60,7 +60,9 @@ def _mul(a, s):
 
 class FusedConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, styles, weight, dcoefs, noise, bias, residual, stride, pad, act, alpha, gain, clamp):
+    def forward(ctx, x, styles, weight, dcoefs, noise, bias, residual, stride, pad, act, alpha, gain, clamp, wgain):
+        # wgain: the layer's weight gain (Conv2dLayer's `weight * weight_gain`, networks_stylegan2.py:173), applied
+        # by the weight pack and by the weight-gradient kernel instead of two elementwise launches
         x_in = x                       # saved as given: a create_graph backward differentiates through it
         x = _cg._nhwc(x)
         n, cin, h, w = x.shape
@@ -75,36 +77,36 @@ class FusedConv(torch.autograd.Function):
         assert not (want_c and want_z), 'demodulation and a residual in one layer are not supported'
         b32 = _f32(bias) if bias is not None else None   # the kernels add it rounded to x.dtype, as the reference
         if _halo(x, kh, kw, stride, pad) and residual is None:
-            y, aux = _cg.conv3x3_fused(x, _cg._pack_conv(weight, dt), cout, in_scale=_f32(styles), out_scale=_f32(dcoefs),
+            y, aux = _cg.conv3x3_fused(x, _cg._pack_conv(weight, dt, scale=wgain), cout, in_scale=_f32(styles), out_scale=_f32(dcoefs),
                                        noise=nz, noise_gain=1.0, bias=b32, act=act, alpha=alpha, gain=gain,
                                        clamp=clamp, want_raw=want_c)
         else:
-            y, aux = _cg.conv_fused(x, _cg._pack_conv(weight, dt), cout, oh, ow, kh, kw, stride, (pad, pad),
+            y, aux = _cg.conv_fused(x, _cg._pack_conv(weight, dt, scale=wgain), cout, oh, ow, kh, kw, stride, (pad, pad),
                                     in_scale=_f32(styles), out_scale=_f32(dcoefs), noise=nz, noise_gain=1.0,
                                     bias=b32, act=act, alpha=alpha, gain=gain, clamp=clamp, residual=residual,
                                     aux_mode=1 if want_c else (2 if want_z else 0))
         ctx.save_for_backward(x_in, styles, weight, dcoefs, noise, bias, y, aux)
-        ctx.cfg = (stride, pad, act, alpha, gain, clamp, residual is not None)
+        ctx.cfg = (stride, pad, act, alpha, gain, clamp, residual is not None, wgain)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, styles, weight, dcoefs, noise, bias, y, aux = ctx.saved_tensors
-        stride, pad, act, alpha, gain, clamp, has_res = ctx.cfg
+        stride, pad, act, alpha, gain, clamp, has_res, wgain = ctx.cfg
         need = ctx.needs_input_grad
         dres = dy if need[6] else None
         zsrc = aux if has_res else y
         c = aux if (dcoefs is not None and not has_res) else None
         if not torch.is_grad_enabled() and fast_backward:
             g = _fast_backward(need, dy, _cg._nhwc(x), styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act,
-                               alpha, gain, clamp)
+                               alpha, gain, clamp, wgain)
         else:
             g = _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha,
-                                   gain, clamp)
-        return g + (dres, None, None, None, None, None, None)
+                                   gain, clamp, wgain)
+        return g + (dres, None, None, None, None, None, None, None)
 
 
-def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, pad):
+def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, pad, wgain=1.0):
     """Gradients of c = conv(x * s, W) given dc: dx = convT(dc, W) * s and ds = sum_hw convT(dc, W) * x in
     one dgrad launch (out_scale / dot_src epilogue), dw = the s-scaled weight gradient."""
     n, cin, h, w = x.shape
@@ -115,22 +117,22 @@ def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, p
     want_ds = need_s and styles is not None
     if need_x or want_ds:
         if _halo(dc, kh, kw, stride, pad):
-            wT = _cg._pack_convT(weight, dt, flip=True)
+            wT = _cg._pack_convT(weight, dt, flip=True, scale=wgain)
             if want_ds:
                 dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
             else:
                 dx, _ = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32)
         else:
             if want_ds:
-                dx, _, ds = _cg.conv_fused(dc, _cg._pack_convT(weight, dt), cin, h, w, kh, kw, stride, (pad, pad),
-                                           transpose=True, out_scale=s32, dot_src=x)
+                dx, _, ds = _cg.conv_fused(dc, _cg._pack_convT(weight, dt, scale=wgain), cin, h, w, kh, kw, stride,
+                                           (pad, pad), transpose=True, out_scale=s32, dot_src=x)
             else:
-                dx, _ = _cg.conv_fused(dc, _cg._pack_convT(weight, dt), cin, h, w, kh, kw, stride, (pad, pad),
-                                       transpose=True, out_scale=s32)
+                dx, _ = _cg.conv_fused(dc, _cg._pack_convT(weight, dt, scale=wgain), cin, h, w, kh, kw, stride,
+                                       (pad, pad), transpose=True, out_scale=s32)
         ds = ds.to(styles.dtype) if want_ds else None
         dx = dx if need_x else None
     if need_w and not _cg.weight_gradients_disabled:
-        dw = _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32).to(weight.dtype)
+        dw = _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32, alpha=wgain).to(weight.dtype)
     return dx, ds, dw
 
 
@@ -217,7 +219,8 @@ class _SavedRaw(torch.autograd.Function):
         return dx, ds, dw, None, None, None
 
 
-def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain, clamp):
+def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain, clamp,
+                   wgain=1.0):
     """First order in three kernels: sg2_layer_bwd; dgrad with the *s scale (+ ds); scaled wgrad."""
     n, cin, h, w = x.shape
     cout, _, kh, kw = weight.shape
@@ -234,7 +237,7 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
         dd = (dz * c).sum([2, 3], dtype=torch.float32) if want_dd else None
         dn = dz.sum(1, keepdim=True, dtype=torch.float32) if want_dn else None
         dc = _cg._nhwc(dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None else dz)
-    dx, ds, dw = _scaled_input_grads(dc, x, styles, weight, need[0], need[1], need[2], stride, pad)
+    dx, ds, dw = _scaled_input_grads(dc, x, styles, weight, need[0], need[1], need[2], stride, pad, wgain)
     db = db.to(bias.dtype) if db is not None else None
     dd = dd.to(dcoefs.dtype) if dd is not None else None
     dn = dn.to(noise.dtype) if dn is not None else None
@@ -242,8 +245,10 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
 
 
 def _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain,
-                       clamp):
+                       clamp, wgain=1.0):
     """Differentiable form (used under create_graph)."""
+    if wgain != 1.0:
+        weight = weight * wgain        # (rare path: the R1 double backward) the gain as a differentiable op
     n, cin, h, w = x.shape
     cout, _, kh, kw = weight.shape
     oh, ow = zsrc.shape[2], zsrc.shape[3]
@@ -285,10 +290,12 @@ def _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c
 
 
 def fused_conv(x, weight, styles=None, dcoefs=None, noise=None, bias=None, residual=None, stride=1, padding=0,
-               act='linear', alpha=0.2, gain=1.0, clamp=None):
+               act='linear', alpha=0.2, gain=1.0, clamp=None, wgain=1.0):
+    """wgain: multiplier of `weight` (a Conv2dLayer's weight gain), applied inside the weight pack and the
+    weight-gradient kernel."""
     return FusedConv.apply(x, styles, weight, dcoefs, noise, bias, residual, int(stride), int(padding),
                            1 if act == 'lrelu' else 0, float(alpha), float(gain),
-                           float(clamp if clamp is not None else -1.0))
+                           float(clamp if clamp is not None else -1.0), float(wgain))
 
 
 def modconv_layer(x, styles, weight, dcoefs, noise, bias, alpha, gain, clamp):

@@ -170,9 +170,10 @@ class _Addmm(torch.autograd.Function):
             return ((dy.sum(0) * beta) if nb else None, (dy @ w) * alpha if nx else None,
                     (dy.t() @ x) * alpha if nw else None, None, None)
         z = _zero_scalar(dy)
-        db = dy.sum(0) if nb else None
-        if db is not None and beta != 1:
-            db = db * beta
+        db = None
+        if nb:   # beta * sum_rows(dy) as ONE GEMV (a sum and a scale otherwise)
+            db = torch.addmv(_zero_vec(dy, dy.shape[1]), dy.t(), _ones(dy, dy.shape[0]), beta=0, alpha=beta) \
+                if beta != 1 else dy.sum(0)
         dx = torch.addmm(z, dy, w, beta=0, alpha=alpha) if nx else None
         dw = torch.addmm(z, dy.t(), x, beta=0, alpha=alpha) if nw else None
         return db, dx, dw, None, None
@@ -180,6 +181,21 @@ class _Addmm(torch.autograd.Function):
 
 def _zero_scalar(t):
     return torch.empty((), dtype=t.dtype, device=t.device)   # beta = 0: never read
+
+
+def _zero_vec(t, n):
+    return torch.empty((n,), dtype=t.dtype, device=t.device)  # beta = 0: never read
+
+
+_ONES = {}
+
+
+def _ones(t, n):
+    key = (n, t.dtype, t.device)
+    v = _ONES.get(key)
+    if v is None:
+        v = _ONES[key] = torch.ones(n, dtype=t.dtype, device=t.device)
+    return v
 
 
 @persistence.persistent_class
@@ -240,10 +256,9 @@ class Conv2dLayer(torch.nn.Module):
 
     def forward(self, x, gain=1, residual=None):
         """residual (DiscriminatorBlock's resnet skip, :621-627) is added to the activated output."""
-        w = self.weight * self.weight_gain
         clamp = self.conv_clamp * gain if self.conv_clamp is not None else None
-        kh = w.shape[2]
-        if self.activation in ('lrelu', 'linear') and self.up == 1 and modconv.supported_generic(x, w):
+        kh = self.weight.shape[2]
+        if self.activation in ('lrelu', 'linear') and self.up == 1 and modconv.supported_generic(x, self.weight):
             # conv + bias + act + gain + clamp (+ residual) in one kernel; the FIR of a down-2 layer runs
             # first (conv2d_resample.py:94-97 / :106-109 plans, same padding algebra)
             stride, pad = 1, self.padding
@@ -255,9 +270,12 @@ class Conv2dLayer(torch.nn.Module):
                     x = upfirdn2d.upfirdn2d(x, self.resample_filter, padding=[x0, x1, y0, y1])
                     stride = self.down
                 pad = 0
-            return modconv.fused_conv(x, w, bias=self.bias, residual=residual, stride=stride, padding=pad,
+            # the weight gain (`w = self.weight * self.weight_gain`, :173) rides in the weight pack and the
+            # weight-gradient kernel: no elementwise launch forward or backward
+            return modconv.fused_conv(x, self.weight, bias=self.bias, residual=residual, stride=stride, padding=pad,
                                       act=self.activation, alpha=bias_act.activation_funcs[self.activation].def_alpha or 0.2,
-                                      gain=self.act_gain * gain, clamp=clamp)
+                                      gain=self.act_gain * gain, clamp=clamp, wgain=self.weight_gain)
+        w = self.weight * self.weight_gain
         b = self.bias.to(x.dtype) if self.bias is not None else None
         x = conv2d_resample.conv2d_resample(x=x, w=w.to(x.dtype), f=self.resample_filter, up=self.up, down=self.down,
                                             padding=self.padding, flip_weight=(self.up == 1))

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define SG2_ABI_VERSION 2
+#define SG2_ABI_VERSION 3
 
 enum sg2_dtype { SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2 };
 
@@ -145,14 +145,25 @@ int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, int dtype, i
                 const float* bias, int act, float alpha, float gain, float clamp, const void* dot_src,
                 float* dot_out, void* stream);
 
+/* Stride-2 transposed 3x3 convolution, padding 0, 16-bit (conv2d_resample.py:112-129, the up-2 plan's
+ * conv_transpose2d; also the input gradient of a stride-2 3x3 convolution):
+ *   y[n, 2i+ky, 2j+kx, o] = sum_{c, (i,j) -> (2i+ky, 2j+kx)} x[n, i, j, c] (* s[n, c]) w[o][ky][kx][c]
+ * x [N, H, W, Cin] NHWC, y [N, 2H+1, 2W+1, Cout] NHWC (overwritten), w packed [Cout][3][3][Cin] (the
+ * conv_transpose2d weight [Cin, Cout, 3, 3] read as [Cout][Cin] without a tap flip), in_scale [N, Cin] f32
+ * or NULL (the modulation x * s rounded as the reference's x * s.to(x.dtype)).  Cin % 32 == 0, Cout % 8 == 0. */
+int sg2_conv3x3_up2(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W, int Cout,
+                    const float* in_scale, void* stream);
+
 /* Weight gradient of sg2_conv2d (transpose = 0 form):
  *   dw[a][ky][kx][b] = sum_{n,oy,ox} g[n,oy,ox,a] * u[n,a] * x[n, oy*stride+ky-pad_y, ox*stride+kx-pad_x, b] * s[n,b]
  *   u = g_scale [N, A], s = x_scale [N, B] float32 (a layer's modulation), or NULL for 1.
  *   g [N, OH, OW, A] NHWC, x [N, H, W, B] NHWC; dw is float32 [A][KH][KW][B], overwritten.
- *   The conv_transpose2d weight gradient is the same call with (g, x) = (x_of_convT, dy). */
+ *   The conv_transpose2d weight gradient is the same call with (g, x) = (x_of_convT, dy).
+ *   alpha scales the result (dw = alpha * sum ...): a layer's weight gain, the backward of the reference's
+ *   `self.weight * self.weight_gain` (networks_stylegan2.py:173) folded in (ABI 3). */
 int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
                      int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* g_scale,
-                     const float* x_scale, void* stream);
+                     const float* x_scale, float alpha, void* stream);
 
 /* Fused first-order backward of the layer epilogue z = c*d + noise + b, y = clamp(act(z)*gain):
  *   dc = dz * d;  db[o] = sum dz;  dd[n,o] = sum_p dz*c;  dnoise[n,p] = sum_o dz
@@ -220,9 +231,11 @@ int sg2_demod_bwd(float* gs, float* gw, const float* dd, const float* d, const f
  * conv2d_gradfix.py _pack_conv / _pack_convT; the reference feeds cuDNN the [O,I,kh,kw] weight
  * directly, networks_stylegan2.py:70/176):  out[a][k][b] = in[a*sa + b*sb + k'*sk], k' = K-1-k when
  * flip != 0, else k.  Strides in elements; in/out dtypes SG2_F32/F16/BF16 (cast in the same pass); K <= 9.
- * [O,I,kh,kw] -> [O][kh][kw][I]: A=O, B=I, K=kh*kw, sa=I*K, sb=K, sk=1. */
+ * [O,I,kh,kw] -> [O][kh][kw][I]: A=O, B=I, K=kh*kw, sa=I*K, sb=K, sk=1.
+ * Each element is multiplied by `scale` in f32 before the cast (ABI 3): a layer's weight gain, the
+ * reference's `self.weight * self.weight_gain` (networks_stylegan2.py:173) in the same pass. */
 int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_dtype, int A, int B, int K, int64_t sa,
-                    int64_t sb, int64_t sk, int flip, void* stream);
+                    int64_t sb, int64_t sk, int flip, float scale, void* stream);
 
 /* fp16 range pre-normalisation, row-wise (SG3/training/networks_stylegan2.py:52-54): t [rows, L] f32,
  * n[r] = max_i |t[r,i]| (written to nrm [rows]); mode 0: y = t * ((1/n) * c)  (the weight, c = 1/sqrt(fan_in)),

@@ -971,3 +971,45 @@ def test_infnorm_prenorm_nan_rows():
         assert torch.equal(torch.isnan(a), torch.isnan(b))
         fin = ~torch.isnan(a)
         assert rel_err(a[fin].double().cpu(), b[fin].double().cpu()) < 1e-6
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
+def test_pack_scale_and_wgrad_alpha(dtype):
+    """The weight gain of a Conv2dLayer (`weight * weight_gain`, networks_stylegan2.py:173) folded into
+    sg2_pack_weight (scale: bit-identical to the f32 product cast to the activation dtype) and into
+    sg2_conv2d_wgrad (alpha: the weight gradient times the gain), on the halo, generic and 1x1 paths."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(21)
+    gain = 1 / np.sqrt(64 * 9)
+    w = torch.randn(48, 64, 3, 3, device=DEV)
+    assert torch.equal(cg._pack_conv(w, dtype, scale=gain), cg._pack_conv((w * gain).to(dtype)))
+    assert torch.equal(cg._pack_convT(w, dtype, flip=True, scale=gain), cg._pack_convT((w * gain).to(dtype), flip=True))
+    for (n, a, b, h, k, s, p) in [(2, 48, 64, 20, 3, 1, 1), (2, 48, 64, 20, 3, 2, 0), (2, 40, 24, 9, 1, 1, 0)]:
+        oh = (h + 2 * p - k) // s + 1
+        g = torch.randn(n, a, oh, oh, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+        x = torch.randn(n, b, h, h, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+        ref = cg._wgrad_raw(g, x, k, k, s, (p, p)) * gain
+        got = cg._wgrad_raw(g, x, k, k, s, (p, p), alpha=gain)
+        assert rel_err(got, ref) < 1e-6, (n, a, b, h, k, s, p)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(2, 128, 65, 70, 64), (2, 64, 64, 64, 128), (1, 512, 64, 64, 512), (1, 32, 64, 96, 8)])
+@pytest.mark.parametrize('mod', [False, True])
+def test_conv3x3_up2(dtype, shape, mod):
+    """sg2_conv3x3_up2 (the stride-2 transposed 3x3 conv of the up-2 layers, output 2H+1, with the
+    modulation x * s.to(x.dtype) in its staging) vs F.conv_transpose2d in float64 on the same rounded
+    operands; ragged tiles (H, W not multiples of the 8 x 16 cell tile), Cout below one 64-channel block."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    N, Cin, H, W, Cout = shape
+    torch.manual_seed(31)
+    x = torch.randn(N, Cin, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, 3, 3, device=DEV) / np.sqrt(Cin * 9)).to(dtype)   # the modulated-conv layout
+    s = (torch.rand(N, Cin, device=DEV) + 0.5) if mod else None
+    assert cg._up2_ok(x, Cout, 2 * H + 1, 2 * W + 1, 3, 3, 2, (0, 0), True)
+    y, _ = cg.conv_fused(x, cg._pack_conv(w), Cout, 2 * H + 1, 2 * W + 1, 3, 3, 2, (0, 0), transpose=True, in_scale=s)
+    xs = (x.float() * s.to(dtype).float()[:, :, None, None]).to(dtype) if mod else x
+    ref = F.conv_transpose2d(xs.double(), w.double().transpose(0, 1), stride=2)
+    assert y.shape == ref.shape
+    tol = 5e-3 if dtype == torch.float16 else 2e-2
+    assert rel_err(y.float(), ref) < tol
