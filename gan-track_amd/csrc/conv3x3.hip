@@ -49,6 +49,10 @@ struct Conv3Args {
     int act;                // 0 linear, 1 lrelu
     int N, H, W, Cin, Cout;
     int tiles_x, tiles_y;
+    int OH, OW;             // output size (= H, W at stride 1; the stride-2 pad-0 form: (H - 3) / 2 + 1)
+    const void* residual;   // optional [N,OH,OW,Cout] (dtype T): y = round(act(...)) + residual (the D resnet add)
+    int raw_act;            // y_raw receives the activated value before the residual add (the activation
+                            // gradient's input) instead of the raw conv output
 };
 
 template <typename T>
@@ -65,10 +69,16 @@ __device__ __forceinline__ f32x4 mma(v8<T> a, v8<T> b, f32x4 c) {
 // TW: tile width (pixels); TH = 256 / TW.  4 waves, each owns 64 consecutive tile pixels x 64 channels.
 // NBUF = 2: double-buffered chunks (1 workgroup / CU); NBUF = 1: single buffer, 2 workgroups / CU
 // overlap each other's staging (better when Cin spans only a couple of chunks).
-template <typename T, int TW, bool SCALE_IN, bool EPI, int NBUF>
+// S = 2: the stride-2, padding-0 3x3 conv (conv2d_resample's down-2 plan after its FIR, :94-109; the D
+// blocks' conv1 and the input gradient of the G up layers) on a 32 x 4 output tile: the (2 TW + 1) x
+// (2 TH + 1) input halo is stored column-deinterleaved (a halo row = its even columns, then its odd ones),
+// so a fragment read of 16 output pixels (input columns 2 apart) is 16 consecutive swizzled LDS rows.
+template <typename T, int TW, bool SCALE_IN, bool EPI, int NBUF, int S = 1>
 __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a) {   // NBUF = 1: two workgroups per CU
-    constexpr int TH = 256 / TW;
-    constexpr int HW_ = TW + 2, HH = TH + 2, HP = HW_ * HH;          // halo pixels
+    constexpr int TH = S == 1 ? 256 / TW : 4;
+    constexpr int PXW = TW * TH / 4, NFR = PXW / 16;                 // pixels and 16-pixel fragments per wave
+    constexpr int HW_ = S * (TW - 1) + 3, HH = S * (TH - 1) + 3, HP = HW_ * HH;   // halo pixels
+    constexpr int HEV = (HW_ + 1) / 2;                                // even columns of a halo row (S = 2)
     constexpr int HALO = HP * PX;                                      // elements per halo buffer
     constexpr int WTS = 9 * BN * PX;                                   // elements per weight buffer
     constexpr int NH = (HP * 4 + 255) / 256;                          // halo 16-B loads per thread
@@ -96,10 +106,11 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
         const int idx = tid + i * 256;             // (pixel, 16-byte quarter)
         const int p = idx >> 2, q = idx & 3;
         const int hy = p / HW_, hx = p - hy * HW_;
-        const int iy = ty0 - 1 + hy, ix = tx0 - 1 + hx;
+        const int iy = S == 1 ? ty0 - 1 + hy : 2 * ty0 + hy, ix = S == 1 ? tx0 - 1 + hx : 2 * tx0 + hx;
         h_ok[i] = p < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
         h_src[i] = h_ok[i] ? ((n * a.H + iy) * a.W + ix) : 0;     // pixel index
-        h_dst[i] = p < HP ? swz64(p, q) : -1;      // byte offset
+        const int pl = S == 1 ? p : hy * HW_ + ((hx & 1) ? HEV + (hx >> 1) : (hx >> 1));   // LDS row
+        h_dst[i] = p < HP ? swz64(pl, q) : -1;     // byte offset
     }
     const int hq = (tid & 3) * 8;
     int w_src[NW], w_dst[NW];
@@ -159,18 +170,18 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
 
     // ---- per-lane fragment bases ----
     const int lq = lane >> 4, l16 = lane & 15;
-    int a_pos[4];
+    int a_pos[NFR];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int m = wave * 64 + i * 16 + l16;
+    for (int i = 0; i < NFR; ++i) {
+        const int m = wave * PXW + i * 16 + l16;
         const int py = m / TW, px = m - py * TW;
-        a_pos[i] = py * HW_ + px;                  // halo row of tap (0,0)
+        a_pos[i] = S * py * HW_ + px;              // LDS row of tap (0,0)
     }
     const int b_lane = swz64(l16, lq);             // + (tap * BN + j * 16) * 64: the same swizzle
 
-    f32x4 acc[4][4];
+    f32x4 acc[NFR][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NFR; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -188,13 +199,15 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
                 const int tap = ky * 3 + kx;
-                v8<T> af[4], bfr[4];
+                // S = 2: input column 2 px + kx of the deinterleaved halo row
+                const int toff = ky * HW_ + (S == 1 ? kx : ((kx & 1) ? HEV : (kx >> 1)));
+                v8<T> af[NFR], bfr[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) af[i] = *(const v8<T>*)(hb + swz64(a_pos[i] + ky * HW_ + kx, lq));
+                for (int i = 0; i < NFR; ++i) af[i] = *(const v8<T>*)(hb + swz64(a_pos[i] + toff, lq));
 #pragma unroll
                 for (int j = 0; j < 4; ++j) bfr[j] = *(const v8<T>*)(wb + (tap * BN + j * 16) * 64);
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < NFR; ++i)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) acc[i][j] = mma<T>(af[i], bfr[j], acc[i][j]);
             }
@@ -216,24 +229,25 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
         bsc[j] = (EPI && a.bias) ? (float)(T)a.bias[oc] : 0.f;   // the reference adds the bias rounded to x.dtype
     }
     constexpr int OS = BN + 8;                 // LDS row stride (elements) of the output tile
-    T* ot = smem;                              // y tile  [256][OS]
-    T* rt = smem + 256 * OS;                   // raw tile [256][OS] (y_raw and/or dot)
-    float* red = (float*)(smem + 2 * 256 * OS);   // [BN] dot partial sums
+    constexpr int NPX = 4 * PXW;               // tile pixels
+    T* ot = smem;                              // y tile  [NPX][OS]
+    T* rt = smem + NPX * OS;                   // raw tile [NPX][OS] (y_raw and/or dot)
+    float* red = (float*)(smem + 2 * NPX * OS);   // [BN] dot partial sums
     const T* nz = (const T*)a.noise;
     const bool want_raw = a.y_raw != nullptr;
     const bool want_dot = a.dot_out != nullptr;
     const bool keep_raw = want_raw || want_dot;
     if (want_dot && tid < BN) red[tid] = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NFR; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int m = wave * 64 + i * 16 + 4 * (lane >> 4) + r;
+            const int m = wave * PXW + i * 16 + 4 * (lane >> 4) + r;
             float nv = 0.f;
             if (EPI && nz) {
                 const int py = m / TW, px = m - py * TW;
-                const int oy = min(ty0 + py, a.H - 1), ox = min(tx0 + px, a.W - 1);
-                nv = (float)nz[((int64_t)n * a.H + oy) * a.W + ox] * a.noise_gain;
+                const int oy = min(ty0 + py, a.OH - 1), ox = min(tx0 + px, a.OW - 1);
+                nv = (float)nz[((int64_t)n * a.OH + oy) * a.OW + ox] * a.noise_gain;
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -260,17 +274,24 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
     for (int e = 0; e < 8; ++e) dacc[e] = 0.f;
     const int c8 = (tid & 7) * 8;              // fixed per thread (256 % 8 == 0)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {               // 256 pixels x 8 chunks of 8 channels / 256 threads
+    for (int k = 0; k < NPX / 32; ++k) {        // NPX pixels x 8 chunks of 8 channels / 256 threads
         const int idx = tid + k * 256;
         const int m = idx >> 3;
         const int py = m / TW, px = m - py * TW;
         const int oy = ty0 + py, ox = tx0 + px;
         const int o = o0 + c8;
-        if (oy >= a.H || ox >= a.W || o >= a.Cout) continue;
-        const int64_t dst = (((int64_t)n * a.H + oy) * a.W + ox) * a.Cout + o;
+        if (oy >= a.OH || ox >= a.OW || o >= a.Cout) continue;
+        const int64_t dst = (((int64_t)n * a.OH + oy) * a.OW + ox) * a.Cout + o;
         if (cvec) {
-            *(vec8o*)(y + dst) = *(const vec8o*)(ot + m * OS + c8);
-            if (want_raw) *(vec8o*)(yr + dst) = *(const vec8o*)(rt + m * OS + c8);
+            vec8o yo = *(const vec8o*)(ot + m * OS + c8);
+            if (a.residual) {
+                if (want_raw && a.raw_act) *(vec8o*)(yr + dst) = yo;
+                const vec8o rr = *(const vec8o*)((const T*)a.residual + dst);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) yo[e] = (T)((float)yo[e] + (float)rr[e]);   // round(v) + residual, rounded
+            }
+            *(vec8o*)(y + dst) = yo;
+            if (want_raw && !a.raw_act) *(vec8o*)(yr + dst) = *(const vec8o*)(rt + m * OS + c8);
             if (want_dot) {
                 const vec8o sv = *(const vec8o*)(dsrc + dst);
                 const vec8o rv = *(const vec8o*)(rt + m * OS + c8);
@@ -279,8 +300,10 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
             }
         } else {
             for (int e = 0; e < 8 && o + e < a.Cout; ++e) {
-                y[dst + e] = ot[m * OS + c8 + e];
-                if (want_raw) yr[dst + e] = rt[m * OS + c8 + e];
+                T yo = ot[m * OS + c8 + e];
+                if (want_raw) yr[dst + e] = a.raw_act ? yo : rt[m * OS + c8 + e];
+                if (a.residual) yo = (T)((float)yo + (float)((const T*)a.residual)[dst + e]);
+                y[dst + e] = yo;
                 if (want_dot) dacc[e] += (float)rt[m * OS + c8 + e] * (float)dsrc[dst + e];
             }
         }
@@ -293,12 +316,12 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
     }
 }
 
-template <typename T, int TW, bool SI, bool EPI, int NBUF>
+template <typename T, int TW, bool SI, bool EPI, int NBUF, int S = 1>
 int launch3(const Conv3Args& a, hipStream_t s) {
-    constexpr int TH = 256 / TW;
-    size_t lds = NBUF * (size_t)((TW + 2) * (TH + 2) * PX + 9 * BN * PX) * sizeof(T);
-    lds = std::max(lds, (size_t)2 * 256 * (BN + 8) * sizeof(T) + BN * sizeof(float));   // epilogue tiles
-    auto kern = conv3x3_halo_kernel<T, TW, SI, EPI, NBUF>;
+    constexpr int TH = S == 1 ? 256 / TW : 4;
+    size_t lds = NBUF * (size_t)((S * (TW - 1) + 3) * (S * (TH - 1) + 3) * PX + 9 * BN * PX) * sizeof(T);
+    lds = std::max(lds, (size_t)2 * TW * TH * (BN + 8) * sizeof(T) + BN * sizeof(float));   // epilogue tiles
+    auto kern = conv3x3_halo_kernel<T, TW, SI, EPI, NBUF, S>;
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -639,12 +662,19 @@ int num_cus() {
 }
 
 template <typename T>
-int dispatch(Conv3Args& a, hipStream_t s) {
+int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     const bool si = a.in_scale != nullptr;
     const bool epi = a.out_scale || a.noise || a.bias || a.act != 0 || a.gain != 1.f || a.clamp >= 0.f;
     if (a.dot_out) {
         hipError_t e = hipMemsetAsync(a.dot_out, 0, (size_t)a.N * a.Cout * sizeof(float), s);
         if (e != hipSuccess) { set_error("sg2_conv3x3: memset failed"); return (int)e; }
+    }
+    if (stride == 2) {   // 32 x 4 output tiles, two workgroups per CU
+        a.tiles_x = (a.OW + 31) / 32;
+        a.tiles_y = (a.OH + 3) / 4;
+        if (si) { if (epi) return launch3<T, 32, true, true, 1, 2>(a, s); return launch3<T, 32, true, false, 1, 2>(a, s); }
+        if (epi) return launch3<T, 32, false, true, 1, 2>(a, s);
+        return launch3<T, 32, false, false, 1, 2>(a, s);
     }
     static const bool persist = [] { const char* e = getenv("SG2_HALO_PERSIST"); return !e || atoi(e) != 0; }();
     // (the persistent kernel's epilogue folds the gain into the demod / noise / bias terms and evaluates lrelu
@@ -847,11 +877,40 @@ int launch_up2(Conv3Args& a, hipStream_t s) {
 }  // namespace
 }  // namespace sg2
 
+namespace sg2 {
+namespace {
+int conv3x3_entry(void* y, void* y_raw, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
+                  int Cout, const float* in_scale, const float* out_scale, const void* noise, float noise_gain,
+                  const float* bias, int act, float alpha, float gain, float clamp, const void* dot_src,
+                  float* dot_out, void* stream, int stride, const void* residual = nullptr, int raw_act = 0);
+}
+}
+
 extern "C" int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
                            int Cout, const float* in_scale, const float* out_scale, const void* noise, float noise_gain,
                            const float* bias, int act, float alpha, float gain, float clamp, const void* dot_src,
                            float* dot_out, void* stream) {
+    return sg2::conv3x3_entry(y, y_raw, x, w, dtype, N, Cin, H, W, Cout, in_scale, out_scale, noise, noise_gain, bias,
+                              act, alpha, gain, clamp, dot_src, dot_out, stream, 1);
+}
+
+extern "C" int sg2_conv3x3_s2(void* y, void* y_raw, const void* x, const void* w, int dtype, int N, int Cin, int H,
+                              int W, int Cout, const float* in_scale, const float* out_scale, const void* noise,
+                              float noise_gain, const float* bias, int act, float alpha, float gain, float clamp,
+                              const void* residual, int raw_act, const void* dot_src, float* dot_out, void* stream) {
     using namespace sg2;
+    SG2_CHECK(H >= 3 && W >= 3, "sg2_conv3x3_s2: input smaller than the kernel");
+    SG2_CHECK(residual == nullptr || ((uintptr_t)residual % 16) == 0, "sg2_conv3x3_s2: 16-byte alignment required");
+    return sg2::conv3x3_entry(y, y_raw, x, w, dtype, N, Cin, H, W, Cout, in_scale, out_scale, noise, noise_gain, bias,
+                              act, alpha, gain, clamp, dot_src, dot_out, stream, 2, residual, raw_act);
+}
+
+namespace sg2 {
+namespace {
+int conv3x3_entry(void* y, void* y_raw, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
+                  int Cout, const float* in_scale, const float* out_scale, const void* noise, float noise_gain,
+                  const float* bias, int act, float alpha, float gain, float clamp, const void* dot_src,
+                  float* dot_out, void* stream, int stride, const void* residual, int raw_act) {
     SG2_CHECK(y && x && w, "sg2_conv3x3: null pointer");
     SG2_CHECK(N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0, "sg2_conv3x3: empty shape");
     SG2_CHECK(dtype == SG2_F16 || dtype == SG2_BF16, "sg2_conv3x3: f16/bf16 only");
@@ -865,10 +924,15 @@ extern "C" int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, i
     a.x = x; a.w = w; a.y = y; a.y_raw = y_raw; a.in_scale = in_scale; a.out_scale = out_scale; a.noise = noise;
     a.bias = bias; a.dot_src = dot_src; a.dot_out = dot_out; a.noise_gain = noise_gain; a.alpha = alpha; a.gain = gain; a.clamp = clamp; a.act = act;
     a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
+    a.residual = residual; a.raw_act = raw_act;
+    a.OH = stride == 1 ? H : (H - 3) / 2 + 1;
+    a.OW = stride == 1 ? W : (W - 3) / 2 + 1;
     hipStream_t s = as_stream(stream);
-    if (dtype == SG2_F16) return dispatch<f16_t>(a, s);
-    return dispatch<bf16_t>(a, s);
+    if (dtype == SG2_F16) return dispatch<f16_t>(a, s, stride);
+    return dispatch<bf16_t>(a, s, stride);
 }
+}  // namespace
+}  // namespace sg2
 
 extern "C" int sg2_conv3x3_up2(void* y, const void* x, const void* w, int dtype, int N, int Cin, int H, int W, int Cout,
                                const float* in_scale, void* stream) {

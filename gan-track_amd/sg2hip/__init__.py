@@ -42,6 +42,8 @@ SIGNATURES = {
                          ctypes.POINTER(Epilogue), _vp, _i64, _vp],
     'sg2_conv3x3': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _f, _f, _f, _vp, _vp,
                     _vp],
+    'sg2_conv3x3_s2': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _f, _f, _f, _vp, _i,
+                       _vp, _vp, _vp],
     'sg2_conv3x3_up2': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp],
     'sg2_conv2d_wgrad': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _f, _vp],
     'sg2_upfirdn2d_lim': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i,

@@ -172,22 +172,51 @@ def _halo_ok(x, kh, kw, stride, pad, out_hw):
             x.dtype in (torch.float16, torch.bfloat16) and c % 8 == 0 and h >= 16 and w >= 16)
 
 
+def _halo_s2_ok(x, kh, kw, stride, pad, dot=False):
+    """The stride-2 / pad-0 form of the halo kernel (sg2_conv3x3_s2, 32x4 output tiles) for 16-bit 3x3
+    layers.  Measured against the implicit GEMM (tools/s2_ab.py, profiles/r02_s2_ab.log): it wins for
+    outputs <= 16 wide in every form (the discriminator's 32^2 / 16^2 down layers), and in the out_scale +
+    dot form (the up layers' input gradient, where the implicit GEMM's dot epilogue is slow) also for
+    inputs of <= 128 channels; wide outputs with many channels stay on the implicit GEMM."""
+    n, c, h, w = x.shape
+    p = tuple(pad) if isinstance(pad, (tuple, list)) else (pad, pad)
+    if not (kh == 3 and kw == 3 and stride == 2 and p == (0, 0) and x.dtype in (torch.float16, torch.bfloat16) and
+            c % 8 == 0 and h >= 17 and w >= 17):
+        return False
+    return (w - 3) // 2 + 1 <= 16 or (dot and c <= 128)
+
+
 def conv3x3_fused(x, wp, cout, in_scale=None, out_scale=None, noise=None, noise_gain=0.0, bias=None, act=0,
-                  alpha=0.2, gain=1.0, clamp=-1.0, want_raw=False, dot_src=None):
-    """sg2_conv3x3 launch.  x NHWC 16-bit, wp packed [Cout][3][3][Cin].
-    Returns (y, raw or None, dot or None) with dot[n,o] = sum_p conv(x)[n,o,p] * dot_src[n,o,p]."""
+                  alpha=0.2, gain=1.0, clamp=-1.0, want_raw=False, dot_src=None, stride=1, residual=None,
+                  raw_act=False):
+    """sg2_conv3x3 (stride 1, pad 1) / sg2_conv3x3_s2 (stride 2, pad 0) launch.  x NHWC 16-bit, wp packed
+    [Cout][3][3][Cin].  Returns (y, raw or None, dot or None) with dot[n,o] = sum_p conv(x)[n,o,p] *
+    dot_src[n,o,p]; with stride 2 an optional residual is added after the epilogue and raw_act makes raw
+    the pre-residual epilogue value."""
     n, cin, h, w = x.shape
-    y = torch.empty([n, cout, h, w], dtype=x.dtype, device=x.device, memory_format=_CL)
+    oh, ow = (h, w) if stride == 1 else ((h - 3) // 2 + 1, (w - 3) // 2 + 1)
+    y = torch.empty([n, cout, oh, ow], dtype=x.dtype, device=x.device, memory_format=_CL)
     raw = torch.empty_like(y) if want_raw else None
     dot = None
     if dot_src is not None:
         dot_src = _nhwc(dot_src)
+        assert dot_src.shape == y.shape and dot_src.dtype == y.dtype
         dot = torch.empty([n, cout], dtype=torch.float32, device=x.device)
-    _hip.check(_hip.lib().sg2_conv3x3(
-        _hip.ptr(y), _hip.ptr(raw), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout,
-        _hip.ptr(in_scale), _hip.ptr(out_scale), _hip.ptr(noise), float(noise_gain), _hip.ptr(bias), int(act),
-        float(alpha), float(gain), float(clamp), _hip.ptr(dot_src), _hip.ptr(dot), _hip.stream_ptr(x.device)),
-        'sg2_conv3x3')
+    lib = _hip.lib()
+    common = (_hip.ptr(y), _hip.ptr(raw), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout,
+              _hip.ptr(in_scale), _hip.ptr(out_scale), _hip.ptr(noise), float(noise_gain), _hip.ptr(bias), int(act),
+              float(alpha), float(gain), float(clamp))
+    if stride == 1:
+        assert residual is None
+        _hip.check(lib.sg2_conv3x3(*common, _hip.ptr(dot_src), _hip.ptr(dot), _hip.stream_ptr(x.device)),
+                   'sg2_conv3x3')
+    else:
+        assert stride == 2
+        if residual is not None:
+            residual = _nhwc(residual)
+            assert residual.shape == y.shape and residual.dtype == y.dtype
+        _hip.check(lib.sg2_conv3x3_s2(*common, _hip.ptr(residual), int(bool(raw_act)), _hip.ptr(dot_src),
+                                      _hip.ptr(dot), _hip.stream_ptr(x.device)), 'sg2_conv3x3_s2')
     return (y, raw, dot) if dot_src is not None else (y, raw)
 
 
@@ -253,6 +282,8 @@ class _Conv2d(torch.autograd.Function):
         oh, ow = out_hw
         if _halo_ok(x, kh, kw, stride, pad, out_hw):
             y = conv3x3_fused(x, _pack_conv(w), o)[0]
+        elif _halo_s2_ok(x, kh, kw, stride, pad):
+            y = conv3x3_fused(x, _pack_conv(w), o, stride=2)[0]
         else:
             y = _conv_raw(x, _pack_conv(w), o, oh, ow, kh, kw, stride, pad, False)
         ctx.save_for_backward(x, w)

@@ -8,8 +8,9 @@ DiscriminatorBlock :621-627):
     z = clamp(act(c * d[n, co] + noise + b) * gain, +-clamp)
     y = z + residual                               (optional)
 where the reference runs x*s, conv, fma(x, d, noise), bias_act and add as separate HBM passes.
-The 3x3 / stride-1 16-bit layers run on the LDS-halo kernel (sg2_conv3x3); every other geometry and
-f32 runs on the implicit-GEMM kernel with the same epilogue (sg2_conv2d_fused).
+The 3x3 / stride-1 16-bit layers run on the LDS-halo kernel (sg2_conv3x3), the 3x3 / stride-2 / pad-0
+ones from 65^2 inputs on its stride-2 form (sg2_conv3x3_s2, with the resnet residual in its epilogue);
+every other geometry and f32 runs on the implicit-GEMM kernel with the same epilogue (sg2_conv2d_fused).
 
 Backward:
   * first order (no create_graph): sg2_layer_bwd (dz, dc = dz*d, db, dd, dnoise in one pass), then
@@ -80,6 +81,11 @@ class FusedConv(torch.autograd.Function):
             y, aux = _cg.conv3x3_fused(x, _cg._pack_conv(weight, dt, scale=wgain), cout, in_scale=_f32(styles), out_scale=_f32(dcoefs),
                                        noise=nz, noise_gain=1.0, bias=b32, act=act, alpha=alpha, gain=gain,
                                        clamp=clamp, want_raw=want_c)
+        elif _cg._halo_s2_ok(x, kh, kw, stride, pad):
+            y, aux = _cg.conv3x3_fused(x, _cg._pack_conv(weight, dt, scale=wgain), cout, in_scale=_f32(styles),
+                                       out_scale=_f32(dcoefs), noise=nz, noise_gain=1.0, bias=b32, act=act,
+                                       alpha=alpha, gain=gain, clamp=clamp, want_raw=want_c or want_z, stride=2,
+                                       residual=residual, raw_act=want_z)
         else:
             y, aux = _cg.conv_fused(x, _cg._pack_conv(weight, dt, scale=wgain), cout, oh, ow, kh, kw, stride, (pad, pad),
                                     in_scale=_f32(styles), out_scale=_f32(dcoefs), noise=nz, noise_gain=1.0,
@@ -371,7 +377,12 @@ class UpModConv(torch.autograd.Function):
                                            clamp=clamp, want_db=need[5] and bias is not None, want_dd=want_dd,
                                            want_dnoise=need[4] and noise is not None)
             dt_ = _up.upfirdn2d(dc, f, up=aup, down=adown, padding=apad, flip_filter=aflip, gain=4)
-            if need[0] or need[1]:
+            if (need[0] or need[1]) and _cg._halo_s2_ok(dt_, kh, kw, 2, tpad, dot=need[1]):
+                res = _cg.conv3x3_fused(dt_, _cg._pack_conv(weight.transpose(0, 1), dt), cin, out_scale=s32,
+                                        dot_src=x if need[1] else None, stride=2)
+                dx = res[0] if need[0] else None
+                ds = res[2] if need[1] else None
+            elif need[0] or need[1]:
                 if need[1]:
                     dx, _, ds = _cg.conv_fused(dt_, _cg._pack_conv(weight.transpose(0, 1), dt), cin, h, w, kh, kw, 2, tpad, out_scale=s32,
                                                dot_src=x)

@@ -145,6 +145,18 @@ int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, int dtype, i
                 const float* bias, int act, float alpha, float gain, float clamp, const void* dot_src,
                 float* dot_out, void* stream);
 
+/* Stride-2 / pad-0 form of sg2_conv3x3 (conv2d_resample.py:139-142 with down = 2: the discriminator's
+ * down-2 3x3 layers after their FIR pre-filter, and the input gradient of the up-2 synthesis layers):
+ * x [N, H, W, Cin] -> y [N, (H-3)/2+1, (W-3)/2+1, Cout]; same epilogue and dot as sg2_conv3x3, plus
+ *   residual  [N, OH, OW, Cout] (dtype, NULL = off): y = round(epilogue) + residual, rounded
+ *             (the resnet add of DiscriminatorBlock, networks_stylegan2.py:621-627)
+ *   raw_act   1: y_raw receives the epilogue value before the residual add (the activation gradient's
+ *             input) instead of the raw conv. */
+int sg2_conv3x3_s2(void* y, void* y_raw, const void* x, const void* w, int dtype, int N, int Cin, int H, int W,
+                   int Cout, const float* in_scale, const float* out_scale, const void* noise, float noise_gain,
+                   const float* bias, int act, float alpha, float gain, float clamp, const void* residual,
+                   int raw_act, const void* dot_src, float* dot_out, void* stream);
+
 /* Stride-2 transposed 3x3 convolution, padding 0, 16-bit (conv2d_resample.py:112-129, the up-2 plan's
  * conv_transpose2d; also the input gradient of a stride-2 3x3 convolution):
  *   y[n, 2i+ky, 2j+kx, o] = sum_{c, (i,j) -> (2i+ky, 2j+kx)} x[n, i, j, c] (* s[n, c]) w[o][ky][kx][c]

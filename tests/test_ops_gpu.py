@@ -1013,3 +1013,86 @@ def test_conv3x3_up2(dtype, shape, mod):
     assert y.shape == ref.shape
     tol = 5e-3 if dtype == torch.float16 else 2e-2
     assert rel_err(y.float(), ref) < tol
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(2, 64, 65, 65, 128), (2, 128, 69, 133, 64), (1, 512, 65, 65, 512),
+                                   (2, 40, 67, 71, 8), (1, 64, 257, 257, 128), (2, 512, 33, 33, 512),
+                                   (3, 256, 17, 19, 512)])
+def test_conv3x3_s2(dtype, shape):
+    """sg2_conv3x3_s2 (stride 2, pad 0: the discriminator's down-2 3x3 layers and the up-2 layers' input
+    gradient) vs F.conv2d in float64 on the same rounded operands: the full layer epilogue with the raw
+    output, the resnet residual with the pre-residual epilogue value, and the out_scale + dot form;
+    ragged 32 x 4 output tiles, Cin = 40 (one partial K chunk), Cout below one block."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    N, Cin, H, W, Cout = shape
+    OH, OW = (H - 3) // 2 + 1, (W - 3) // 2 + 1
+    torch.manual_seed(41)
+    x = torch.randn(N, Cin, H, W)
+    w = torch.randn(Cout, Cin, 3, 3) / np.sqrt(Cin * 9)
+    s = torch.rand(N, Cin) + 0.5
+    d = torch.rand(N, Cout) + 0.5
+    noise = torch.randn(N, 1, OH, OW)
+    b = torch.randn(Cout) * 0.1
+    res = torch.randn(N, Cout, OH, OW)
+    xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    wp = cg._pack_conv(w.to(DEV, dtype))
+    tol = 5e-3 if dtype == torch.float16 else 2e-2
+    xs = (x.to(dtype).float() * s[:, :, None, None]).to(dtype).double()
+    c = F.conv2d(xs, w.to(dtype).double(), stride=2)
+    # (1) modulated conv + demod + noise + bias + lrelu + clamp, raw output
+    y, raw = cg.conv3x3_fused(xd, wp, Cout, in_scale=s.to(DEV), out_scale=d.to(DEV),
+                              noise=noise.to(DEV, dtype).reshape(N, OH, OW).contiguous(), noise_gain=0.3,
+                              bias=b.to(DEV), act=1, alpha=0.2, gain=np.sqrt(2), clamp=1.5, want_raw=True, stride=2)
+    z = c * d[:, :, None, None] + noise.to(dtype).double() * 0.3 + b[None, :, None, None]
+    yr = (F.leaky_relu(z, 0.2) * np.sqrt(2)).clamp(-1.5, 1.5)
+    assert y.shape == (N, Cout, OH, OW)
+    assert rel_err(raw.float(), c) < tol
+    assert rel_err(y.float(), yr) < tol
+    # (2) bias + lrelu + residual (DiscriminatorBlock conv1), raw = the activation before the add
+    rd = res.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    y, za = cg.conv3x3_fused(xd, wp, Cout, bias=b.to(DEV), act=1, alpha=0.2, gain=np.sqrt(0.5), clamp=256.0,
+                             want_raw=True, stride=2, residual=rd, raw_act=True)
+    c0 = F.conv2d(x.to(dtype).double(), w.to(dtype).double(), stride=2)
+    zr = F.leaky_relu(c0 + b[None, :, None, None], 0.2) * np.sqrt(0.5)
+    assert rel_err(za.float(), zr) < tol
+    assert rel_err(y.float(), zr + res.to(dtype).double()) < tol
+    assert torch.equal(y, (za.float() + rd.float()).to(dtype))     # round(z) + residual, rounded once more
+    # (3) out_scale + dot (the up-2 layer's dgrad: dx and ds in one launch)
+    src = torch.randn(N, Cout, OH, OW).to(dtype)
+    y, _, dot = cg.conv3x3_fused(xd, wp, Cout, out_scale=d.to(DEV), dot_src=src.to(DEV).contiguous(
+        memory_format=torch.channels_last), stride=2)
+    cd = F.conv2d(x.to(dtype).double(), w.to(dtype).double(), stride=2)
+    assert rel_err(y.float(), cd * d[:, :, None, None]) < tol
+    assert rel_err(dot, (cd * src.double()).sum([2, 3])) < tol
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_down_layer_s2_route_matches_generic(dtype, monkeypatch):
+    """A discriminator down-2 Conv2dLayer with the resnet residual (networks_stylegan2.py:621-627) through
+    the stride-2 halo kernel vs the same layer forced onto the generic implicit-GEMM kernel: output and
+    first-order gradients (x, weight, bias, residual)."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    from torch_utils.ops import modconv
+    torch.manual_seed(43)
+    N, Cin, H, Cout = 4, 64, 33, 128
+    x0 = torch.randn(N, Cin, H, H, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    w0 = torch.randn(Cout, Cin, 3, 3, device=DEV)
+    b0 = torch.randn(Cout, device=DEV) * 0.1
+    r0 = torch.randn(N, Cout, 16, 16, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(N, Cout, 16, 16, device=DEV).to(dtype)
+    assert cg._halo_s2_ok(x0, 3, 3, 2, (0, 0))
+
+    def run():
+        x, w, b, r = (t.detach().clone().requires_grad_(True) for t in (x0, w0, b0, r0))
+        y = modconv.fused_conv(x, w.to(dtype), bias=b, residual=r, stride=2, padding=0, act='lrelu',
+                               gain=np.sqrt(0.5), clamp=256.0, wgain=1 / np.sqrt(Cin * 9))
+        y.backward(g)
+        return [t.float() for t in (y, x.grad, w.grad, b.grad, r.grad)]
+
+    fast = run()
+    monkeypatch.setattr(cg, '_halo_s2_ok', lambda *a, **k: False)
+    slow = run()
+    tol = 5e-3 if dtype == torch.float16 else 2e-2
+    for name, a_, b_ in zip(('y', 'dx', 'dw', 'db', 'dres'), fast, slow):
+        assert rel_err(a_, b_) < tol, name
