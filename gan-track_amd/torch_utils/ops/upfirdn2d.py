@@ -155,6 +155,63 @@ def fir_fused(x, f2, padding, gain=1.0, flip_filter=False, out_scale=None, noise
     return y, aux
 
 
+class _ForkFIR(torch.autograd.Function):
+    """(x, upfirdn2d(x, f, down=down, padding)) for a tensor that feeds both a FIR-downsampled branch and an
+    unfiltered one (DiscriminatorBlock's resnet skip and conv0, networks_stylegan2.py:621-627).  The
+    backward fuses the add of the two branch gradients into the adjoint FIR (its epilogue's residual
+    term): dx = round(FIR^T(g_down)) + g_x, the sum autograd would form, without an activation-sized add
+    pass.  Under create_graph the same gradient is built from differentiable ops."""
+
+    @staticmethod
+    def forward(ctx, x, f, down, padding):
+        px0, px1, py0, py1 = padding
+        y = _raw(x, f, 1, 1, down, down, px0, px1, py0, py1, False, 1.0)
+        ctx.save_for_backward(f)
+        ctx.cfg = (down, padding, x.shape)
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, gx, gy):
+        f, = ctx.saved_tensors
+        down, padding, xs = ctx.cfg
+        if gy is None:
+            return gx, None, None, None
+        aup, adown, p, aflip = adjoint_params(f, (xs[2], xs[3]), (gy.shape[2], gy.shape[3]), [1, 1], [down, down],
+                                              list(padding), False)
+        if torch.is_grad_enabled() or gx is None:
+            dx = _upfirdn2d_fn(up=aup, down=adown, padding=p, flip_filter=aflip).apply(gy, f)
+            return (dx + gx if gx is not None else dx), None, None, None
+        cl = torch.channels_last
+        gy = gy.contiguous(memory_format=cl)
+        gx = gx.to(gy.dtype).contiguous(memory_format=cl)
+        dx = torch.empty_like(gx)
+        epi = _hip.Epilogue(None, None, None, _hip.ptr(gx), None, 1.0, 0.2, 1.0, -1.0, 0, 0)
+        fh, fw = f.shape
+        _hip.check(_hip.lib().sg2_upfirdn2d_fused(
+            _hip.ptr(dx), _hip.ptr(gy), _hip.ptr(f), _hip.dtype_code(gy), _hip.i64arr(gy.shape),
+            _hip.i64arr(gy.stride()), _hip.i64arr(dx.shape), _hip.i64arr(dx.stride()), fw, fh, aup[0], aup[1],
+            adown[0], adown[1], p[0], p[1], p[2], p[3], int(bool(aflip)), 1.0, ctypes.byref(epi),
+            _hip.stream_ptr(gy.device)), 'sg2_upfirdn2d_fused')
+        return dx, None, None, None
+
+
+def fork_fir(x, f, down, padding):
+    """(x, upfirdn2d(x, f, down=down, padding=padding)) with the branch-gradient add fused into the
+    backward (_ForkFIR).  f: a 2-D float32 filter on x's device; x channels-last with C % 8 == 0 (16-bit)
+    or C % 4 == 0 (f32), as the fused epilogue requires."""
+    _hip.require_device(x)
+    px0, px1, py0, py1 = _parse_padding(padding)
+    f = f.to(device=x.device, dtype=torch.float32).contiguous()
+    return _ForkFIR.apply(x, f, int(down), (px0, px1, py0, py1))
+
+
+def fork_fir_ok(x, f):
+    """Whether fork_fir's fused backward applies (else the caller runs the plain two-branch graph)."""
+    v = 8 if x.dtype in (torch.float16, torch.bfloat16) else 4
+    return (x.is_cuda and f is not None and f.ndim == 2 and x.ndim == 4 and x.shape[1] % v == 0 and
+            x.is_contiguous(memory_format=torch.channels_last))
+
+
 def adjoint_params(f, x_hw, y_hw, up, down, padding, flip_filter):
     """(up, down, padding, flip) of the adjoint upfirdn2d (reference upfirdn2d.py:250-269)."""
     upx, upy = _parse_scaling(up)

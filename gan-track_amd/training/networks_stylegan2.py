@@ -254,8 +254,9 @@ class Conv2dLayer(torch.nn.Module):
             else:
                 self.bias = None
 
-    def forward(self, x, gain=1, residual=None):
-        """residual (DiscriminatorBlock's resnet skip, :621-627) is added to the activated output."""
+    def forward(self, x, gain=1, residual=None, prefiltered=False):
+        """residual (DiscriminatorBlock's resnet skip, :621-627) is added to the activated output.
+        prefiltered: a 1x1 down-2 layer's input already went through its FIR (upfirdn2d.fork_fir)."""
         clamp = self.conv_clamp * gain if self.conv_clamp is not None else None
         kh = self.weight.shape[2]
         if self.activation in ('lrelu', 'linear') and self.up == 1 and modconv.supported_generic(x, self.weight):
@@ -265,7 +266,8 @@ class Conv2dLayer(torch.nn.Module):
             if self.down > 1:
                 x0, x1, y0, y1 = conv2d_resample._frame_padding(self.padding, self.resample_filter, 1, self.down)
                 if kh == 1:
-                    x = upfirdn2d.upfirdn2d(x, self.resample_filter, down=self.down, padding=[x0, x1, y0, y1])
+                    if not prefiltered:
+                        x = upfirdn2d.upfirdn2d(x, self.resample_filter, down=self.down, padding=[x0, x1, y0, y1])
                 else:
                     x = upfirdn2d.upfirdn2d(x, self.resample_filter, padding=[x0, x1, y0, y1])
                     stride = self.down
@@ -277,8 +279,10 @@ class Conv2dLayer(torch.nn.Module):
                                       gain=self.act_gain * gain, clamp=clamp, wgain=self.weight_gain)
         w = self.weight * self.weight_gain
         b = self.bias.to(x.dtype) if self.bias is not None else None
-        x = conv2d_resample.conv2d_resample(x=x, w=w.to(x.dtype), f=self.resample_filter, up=self.up, down=self.down,
-                                            padding=self.padding, flip_weight=(self.up == 1))
+        pre = prefiltered and self.down > 1 and kh == 1
+        x = conv2d_resample.conv2d_resample(x=x, w=w.to(x.dtype), f=None if pre else self.resample_filter, up=self.up,
+                                            down=1 if pre else self.down, padding=self.padding,
+                                            flip_weight=(self.up == 1))
         x = bias_act.bias_act(x, b, act=self.activation, gain=self.act_gain * gain, clamp=clamp)
         return x if residual is None else residual.add_(x)
 
@@ -598,7 +602,14 @@ class DiscriminatorBlock(torch.nn.Module):
             x = x + y if x is not None else y
             img = upfirdn2d.downsample2d(img, self.resample_filter) if self.architecture == 'skip' else None
         if self.architecture == 'resnet':
-            y = self.skip(x, gain=np.sqrt(0.5))
+            sk = self.skip
+            if sk.down > 1 and sk.weight.shape[2] == 1 and upfirdn2d.fork_fir_ok(x, sk.resample_filter):
+                # the skip's FIR taken off x with the two branches' gradient add fused into its backward
+                pad = conv2d_resample._frame_padding(sk.padding, sk.resample_filter, 1, sk.down)
+                x, xd = upfirdn2d.fork_fir(x, sk.resample_filter, sk.down, pad)
+                y = sk(xd, gain=np.sqrt(0.5), prefiltered=True)
+            else:
+                y = self.skip(x, gain=np.sqrt(0.5))
             x = self.conv0(x)
             x = self.conv1(x, gain=np.sqrt(0.5), residual=y)   # y + conv1(x), the add fused into conv1
         else:

@@ -1096,3 +1096,46 @@ def test_down_layer_s2_route_matches_generic(dtype, monkeypatch):
     tol = 5e-3 if dtype == torch.float16 else 2e-2
     for name, a_, b_ in zip(('y', 'dx', 'dw', 'db', 'dres'), fast, slow):
         assert rel_err(a_, b_) < tol, name
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16])
+def test_fork_fir_discriminator_block(dtype, monkeypatch):
+    """DiscriminatorBlock with the skip's FIR forked off its input (upfirdn2d.fork_fir: the skip / conv0
+    gradient add fused into the adjoint FIR's epilogue, rounding FIR^T(g) and the sum as the separate
+    launches do) vs the plain two-branch graph: forward, first-order gradients and an R1-style double
+    backward (create_graph) through both."""
+    from torch_utils.ops import upfirdn2d as up
+    from training import networks_stylegan2 as net
+    torch.manual_seed(29)
+    blk = net.DiscriminatorBlock(64, 64, 128, resolution=32, img_channels=1, first_layer_idx=0, conv_clamp=256,
+                                 use_fp16=(dtype != torch.float32), fp16_dtype=torch.float16).to(DEV)
+    x0 = torch.randn(4, 64, 32, 32, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(4, 128, 16, 16, device=DEV)
+    params = [blk.conv0.weight, blk.conv1.weight, blk.skip.weight]
+
+    def run():
+        x = x0.detach().clone().requires_grad_(True)
+        y = blk(x, None)[0]
+        g = torch.autograd.grad(y, [x] + params, dy.to(y.dtype))
+        x2 = x0.detach().clone().float().requires_grad_(True)
+        y2 = blk(x2.to(dtype).contiguous(memory_format=torch.channels_last), None)[0]
+        (gx,) = torch.autograd.grad(y2.float().square().sum(), [x2], create_graph=True)
+        r1 = torch.autograd.grad(gx.square().sum(), params)
+        return y, g, r1
+
+    assert up.fork_fir_ok(x0, blk.skip.resample_filter)
+    calls = []
+    orig = up.fork_fir
+    monkeypatch.setattr(up, 'fork_fir', lambda *a: calls.append(1) or orig(*a))
+    y_f, g_f, r_f = run()
+    assert calls
+    monkeypatch.setattr(up, 'fork_fir_ok', lambda *a: False)
+    y_p, g_p, r_p = run()
+    # (not bitwise: the split-K convs of this small block accumulate with float atomics, so two runs of
+    # either graph differ in the last bits)
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    assert rel_err(y_f.float(), y_p.float()) < tol
+    for a_, b_ in zip(g_f, g_p):
+        assert rel_err(a_.float(), b_.float()) < tol
+    for a_, b_ in zip(r_f, r_p):
+        assert rel_err(a_.float(), b_.float()) < 1e-3

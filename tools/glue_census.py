@@ -20,6 +20,7 @@ VIEWS = {'view', 'as_strided', 'reshape', 't', 'transpose', 'permute', 'expand',
          'new_empty_strided', '_unsafe_view', 'numpy_T', 'mT', 'expand_as', 'view_as', 'set_', 'clone', 'is_nonzero',
          'item', '_local_scalar_dense', 'resize_', 'contiguous'}
 counts = Counter()
+big = Counter()      # ops over >= 1M-element tensors: (op, origin, shape, dtype) -> count
 
 
 class Census(TorchDispatchMode):
@@ -33,6 +34,9 @@ class Census(TorchDispatchMode):
                 fr = [f for f in traceback.extract_stack() if 'gan-track_amd' in f.filename]
                 origin = ' <- '.join(f'{f.filename.split("gan-track_amd/")[-1]}:{f.lineno}' for f in fr[-2:][::-1])
             counts[(name, origin)] += 1
+            t = next((a for a in args if isinstance(a, torch.Tensor)), None)
+            if t is not None and t.numel() >= (1 << 20):
+                big[(name, origin, tuple(t.shape), str(t.dtype).split('.')[-1])] += 1
         return func(*args, **(kwargs or {}))
 
 
@@ -51,3 +55,6 @@ torch.cuda.synchronize()
 print(f'{sum(counts.values()) / 16:.0f} non-view aten ops per step')
 for (op, origin), n in counts.most_common(70):
     print(f'{n / 16:7.1f}/step {op:18s} {origin[:160]}')
+print('\nops on >= 1M-element tensors (bytes moved dominate the glue time):')
+for (op, origin, shp, dt), n in big.most_common(40):
+    print(f'{n / 16:7.1f}/step {op:14s} {dt:8s} {str(shp):24s} {origin[:120]}')
