@@ -205,6 +205,131 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
     }
 }
 
+// Stride-2 / pad-0 3x3 weight gradient in ONE launch (the discriminator's down-2 layers after their FIR
+// and the transposed convs of the up layers): x coordinate = 2 g + k.  Where the phase split above runs
+// four launches that each re-stage the whole of g and feed 1-4 MFMAs per A fragment, this kernel stages
+// a 16 x 8 g tile and the (2*8+1) x (2*16+1) x region it reads ONCE, with each x row stored
+// column-deinterleaved (its even columns, then its odd ones): the 8 consecutive g pixels of a fragment
+// then read x columns 2 px + kx as 8 consecutive LDS rows for every tap, so all nine taps accumulate per
+// A fragment (9 MFMAs per 16-pixel k-step, as the stride-1 kernel).
+template <typename T, bool SWZ>
+__global__ __launch_bounds__(256) void wgrad3x3_s2_kernel(W3Args a) {
+    constexpr int LD = Lay<SWZ>::LD;
+    constexpr int TW = 16, TH = 8, NP = TW * TH;          // g tile
+    constexpr int XW = 2 * TW + 1, XH = 2 * TH + 1, XEV = TW + 1, HP = XW * XH;   // x region (561 px)
+    constexpr int GCH = NP * 8 / 256;                     // 4 g loads per thread
+    constexpr int XCH = (HP * 8 + 255) / 256;             // 18 x loads per thread
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+
+    __shared__ __attribute__((aligned(16))) T gs[NP * LD];
+    __shared__ __attribute__((aligned(16))) T xs[HP * LD];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wa = wave >> 1, wb = wave & 1;
+    const int a0 = blockIdx.x * BC, b0 = blockIdx.y * BC;
+    const int t_begin = blockIdx.z * a.tiles_per_block;
+    const int t_end = min(a.tiles, t_begin + a.tiles_per_block);
+    const T* __restrict__ gp = (const T*)a.g;
+    const T* __restrict__ xp = (const T*)a.x;
+    const int cc = (tid & 7) * 8;
+    const bool a_ok = a0 + cc < a.A, b_ok = b0 + cc < a.B;
+
+    vec8 rg[GCH], rx[XCH];
+    float gsc[8], xsc[8];
+    const __amdgpu_buffer_rsrc_t rgb = make_rsrc(gp, (int64_t)a.N * a.GH * a.GW * a.A * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(xp, (int64_t)a.N * a.XH * a.XW * a.B * (int64_t)sizeof(T));
+    auto gload = [&](int t) {
+        const int per = a.tiles_x * a.tiles_y;
+        const int n = t / per, r = t - n * per;
+        const int ty0 = (r / a.tiles_x) * TH, tx0 = (r % a.tiles_x) * TW;
+#pragma unroll
+        for (int i = 0; i < GCH; ++i) {
+            const int px = (tid >> 3) + i * 32;
+            const int oy = ty0 + px / TW, ox = tx0 + px % TW;
+            const bool ok = a_ok && oy < a.GH && ox < a.GW;
+            rg[i] = buf_load16<vec8>(rgb, ok ? (((n * a.GH + oy) * a.GW + ox) * a.A + a0 + cc) * (int)sizeof(T) : -1);
+        }
+#pragma unroll
+        for (int i = 0; i < XCH; ++i) {
+            const int hp = (tid >> 3) + i * 32;           // x region pixel, row-major (natural column order)
+            const int iy = 2 * ty0 + hp / XW, ix = 2 * tx0 + hp % XW;
+            const bool ok = b_ok && hp < HP && iy < a.XH && ix < a.XW;
+            rx[i] = buf_load16<vec8>(rxb, ok ? (((n * a.XH + iy) * a.XW + ix) * a.B + b0 + cc) * (int)sizeof(T) : -1);
+        }
+        if (a.gscale) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gsc[j] = a.gscale[n * a.A + (a_ok ? a0 + cc + j : 0)];
+        }
+        if (a.xscale) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xsc[j] = a.xscale[n * a.B + (b_ok ? b0 + cc + j : 0)];
+        }
+    };
+    auto scale8 = [](vec8 v, const float* sc) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (T)((float)v[j] * sc[j]);
+        return v;
+    };
+    auto sstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < GCH; ++i)
+            *(vec8*)(gs + Lay<SWZ>::off((tid >> 3) + i * 32, cc)) = a.gscale ? scale8(rg[i], gsc) : rg[i];
+#pragma unroll
+        for (int i = 0; i < XCH; ++i) {
+            const int hp = (tid >> 3) + i * 32;
+            const int hy = hp / XW, hx = hp - hy * XW;
+            const int row = hy * XW + ((hx & 1) ? XEV + (hx >> 1) : (hx >> 1));   // deinterleaved
+            if (hp < HP) *(vec8*)(xs + Lay<SWZ>::off(row, cc)) = a.xscale ? scale8(rx[i], xsc) : rx[i];
+        }
+    };
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
+
+    if (t_begin < t_end) {
+        gload(t_begin);
+        sstore();
+        __syncthreads();
+        for (int t = t_begin; t < t_end; ++t) {
+            const bool more = t + 1 < t_end;
+            if (more) gload(t + 1);
+#pragma unroll 2
+            for (int k0 = 0; k0 < NP; k0 += 16) {
+                const int pr = k0 + 8 * ((lane >> 4) >> 1);   // 8 pixels of one tile row
+                const int py = pr / TW, px = pr % TW;
+                const v8w<T> fa = frag32<T, SWZ>(gs, pr, wa * 32, lane);
+#pragma unroll
+                for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                    for (int kx = 0; kx < 3; ++kx) {
+                        const int row = (2 * py + ky) * XW + ((kx & 1) ? XEV : 0) + px + (kx >> 1);
+                        const v8w<T> fb = frag32<T, SWZ>(xs, row, wb * 32, lane);
+                        acc[ky * 3 + kx] = mma32<T>(fa, fb, acc[ky * 3 + kx]);
+                    }
+            }
+            __syncthreads();
+            if (more) {
+                sstore();
+                __syncthreads();
+            }
+        }
+    }
+
+    const int b = b0 + wb * 32 + (lane & 31);
+    if (b < a.B) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int ar = a0 + wa * 32 + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+            if (ar >= a.A) continue;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) atomicAdd(a.dw + ((int64_t)ar * 9 + t) * a.B + b, acc[t][j] * a.alpha);
+        }
+    }
+}
+
 template <typename T, int TW, int NT>
 void launch_w3(const W3Args& a, dim3 grid, hipStream_t s) {
     static const bool swz = [] { const char* e = getenv("SG2_WGRAD_SWZ"); return e != nullptr && e[0] == '1'; }();
@@ -247,6 +372,21 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
     W3Args a{};
     a.g = g; a.x = x; a.gscale = gscale; a.xscale = xscale; a.dw = dw; a.alpha = alpha;
     a.N = N; a.GH = OH; a.GW = OW; a.XH = H; a.XW = W; a.A = A; a.B = B; a.KK = KH * KW; a.S = stride;
+    static const bool s2_on = [] { const char* e = getenv("SG2_WGRAD_S2"); return !e || atoi(e) != 0; }();
+    if (s2_on && stride == 2 && KH == 3 && KW == 3 && pad_y == 0 && pad_x == 0) {
+        // all nine taps in one launch (wgrad3x3_s2_kernel), 16 x 8 g tiles
+        a.tiles_x = (int)cdiv(OW, 16);
+        a.tiles_y = (int)cdiv(OH, 8);
+        a.tiles = N * a.tiles_x * a.tiles_y;
+        const int cb = (int)(cdiv(A, BC) * cdiv(B, BC));
+        int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(512, cb), a.tiles / 4));
+        a.tiles_per_block = (int)cdiv(a.tiles, splits);
+        splits = (int)cdiv(a.tiles, a.tiles_per_block);
+        dim3 grid((unsigned)cdiv(A, BC), (unsigned)cdiv(B, BC), (unsigned)splits);
+        if (dtype == SG2_F16) wgrad3x3_s2_kernel<f16_t, false><<<grid, 256, 0, s>>>(a);
+        else wgrad3x3_s2_kernel<bf16_t, false><<<grid, 256, 0, s>>>(a);
+        return launch_status("sg2_conv2d_wgrad (halo, stride 2)");
+    }
     const int TW = OW >= 32 ? 32 : 16;
     a.tiles_x = (int)cdiv(OW, TW);
     a.tiles_y = (int)cdiv(OH, 256 / TW);

@@ -745,14 +745,26 @@ def test_conv_fused_dot_and_scale(dtype, geom):
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize('case', ['conv_s2', 'convT_s2', 'conv_1x1'])
+@pytest.mark.parametrize('case', ['conv_s2', 'convT_s2', 'conv_1x1', 'conv_s2_big'])
 def test_wgrad_halo_phases(dtype, case):
-    """Halo weight gradient split by output phase: stride-2 conv (D down layers), the transposed
-    stride-2 conv of the up layers (with the modulation on the g operand) and 1x1, vs autograd in f64."""
+    """Halo weight gradients: stride-2 conv (D down layers; all nine taps in one launch of
+    wgrad3x3_s2_kernel), the transposed stride-2 conv of the up layers (with the modulation on the g
+    operand) and 1x1 (phase kernel), vs autograd in f64; ragged 16 x 8 tiles, partial 64-channel blocks."""
     from torch_utils.ops import conv2d_gradfix as cg
     torch.manual_seed(31)
     N, Ci, Co = 2, 64, 72
-    if case == 'conv_s2':
+    if case == 'conv_s2_big':
+        N, Ci, Co = 3, 136, 64
+        x = torch.randn(N, Ci, 67, 65, device=DEV)
+        s = torch.rand(N, Ci, device=DEV) + 0.5
+        w = torch.randn(Co, Ci, 3, 3, device=DEV, dtype=torch.float64, requires_grad=True)
+        xs = (x.to(dtype).float() * s[:, :, None, None]).to(dtype).double()
+        y = F.conv2d(xs, w, stride=2)
+        g = torch.randn_like(y)
+        ref, = torch.autograd.grad((y * g.to(dtype).double()).sum(), [w])
+        dw = cg._wgrad_raw(g.to(dtype).contiguous(memory_format=torch.channels_last),
+                           x.to(dtype).contiguous(memory_format=torch.channels_last), 3, 3, 2, (0, 0), x_scale=s)
+    elif case == 'conv_s2':
         x = torch.randn(N, Ci, 33, 41, device=DEV)
         w = torch.randn(Co, Ci, 3, 3, device=DEV, dtype=torch.float64, requires_grad=True)
         y = F.conv2d(x.to(dtype).double(), w, stride=2)
