@@ -270,6 +270,82 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
     }
 }
 
+// The same product with the per-(n, o) dot reduction of a dgrad (toRGB's input gradient with its
+// modulation gradient: dot_out[n, o] = sum_p round(c) * dot_src[n, p, o]).  grid = (blocks per sample, N):
+// a workgroup owns SK_ITERS x (256 / OG) consecutive pixels of ONE sample, so a lane accumulates its 8
+// channels' products in registers, the workgroup combines them in LDS and adds Cout floats to dot_out
+// (instead of the implicit GEMM padding K = Cin to 32 and reducing through per-element atomics).
+constexpr int SK_ITERS = 16;
+template <typename T>
+__global__ __launch_bounds__(256) void conv1x1_smallk_dot_kernel(ConvArgs a) {
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    __shared__ float red[2048];
+    const int OG = a.Cout / 8, HW = a.H * a.W, PPI = 256 / OG;   // host: 256 % OG == 0
+    const int n = blockIdx.y;
+    const T* x = (const T*)a.x;
+    const T* w = (const T*)a.w;
+    const int o0 = (threadIdx.x % OG) * 8;
+    float wv[8][4], bj[8], dacc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wv[j][k] = k < a.Cin ? (float)w[(o0 + j) * a.Cin + k] : 0.f;
+        bj[j] = (a.e.on && a.e.bias) ? (float)(T)a.e.bias[o0 + j] : 0.f;
+        dacc[j] = 0.f;
+    }
+    for (int i = threadIdx.x; i < a.Cout; i += 256) red[i] = 0.f;
+    const bool on = a.e.on;
+    const float slope = (on && a.e.act == 1) ? a.e.alpha : 1.f, eg = on ? a.e.gain : 1.f;
+    const bool clamp_on = on && a.e.clamp >= 0.f;
+    const float cl = a.e.clamp;
+    const int aux_mode = on ? a.e.aux_mode : 0;
+    float isc[4], osc[8];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) isc[c] = (a.in_scale && c < a.Cin) ? a.in_scale[(int64_t)n * a.Cin + c] : 1.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) osc[j] = (on && a.e.out_scale) ? a.e.out_scale[(int64_t)n * a.Cout + o0 + j] : 1.f;
+    const int p_begin = blockIdx.x * SK_ITERS * PPI;
+#pragma unroll 4
+    for (int it = 0; it < SK_ITERS; ++it) {
+        const int p = p_begin + it * PPI + threadIdx.x / OG;
+        if (p >= HW) break;
+        const int64_t pix = (int64_t)n * HW + p;
+        float xv[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float v = c < a.Cin ? (float)x[pix * a.Cin + c] : 0.f;
+            if (a.in_scale && c < a.Cin) v = (float)(T)(v * isc[c]);
+            xv[c] = v;
+        }
+        const float nv = (on && a.e.noise) ? (float)((const T*)a.e.noise)[pix] * a.e.noise_gain : 0.f;
+        const vec8 ds = *(const vec8*)((const T*)a.e.dot_src + pix * a.Cout + o0);
+        vec8 yo, ao, rv;
+        const bool resid = on && a.e.residual;
+        if (resid) rv = *(const vec8*)((const T*)a.e.residual + pix * a.Cout + o0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float c = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) c += xv[k] * wv[j][k];
+            dacc[j] += (float)(T)c * (float)ds[j];
+            float v = c * osc[j];
+            v = v + nv + bj[j];
+            v = (v > 0.f ? v : v * slope) * eg;
+            if (clamp_on) v = fminf(fmaxf(v, -cl), cl);
+            ao[j] = (T)(aux_mode == 1 ? c : v);
+            if (resid) v = (float)(T)v + (float)rv[j];
+            yo[j] = (T)v;
+        }
+        if (aux_mode) *(vec8*)((T*)a.e.aux + pix * a.Cout + o0) = ao;
+        *(vec8*)((T*)a.y + pix * a.Cout + o0) = yo;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&red[o0 + j], dacc[j]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.Cout; i += 256) atomicAdd(a.e.dot_out + (int64_t)n * a.Cout + i, red[i]);
+}
+
 // 1x1 convolution with a tiny output depth (Cout <= 4: G's toRGB, Cin % 8 == 0): a dot product per
 // pixel, HBM-bound on the Cin-wide input.  Eight lanes share a pixel, each summing every eighth
 // 8-channel chunk (16-byte loads, x * in_scale rounded to T as in conv_fwd_kernel), three xor shuffles
@@ -1244,8 +1320,15 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
     }
     // (a 1x1 stride-1 transposed conv is the same product with the caller's transposed pack: dgrad of toRGB)
     if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W &&
-        Cin <= 4 && Cout % 8 == 0 && 256 % (Cout / 8) == 0 && !base.e.dot_out && (uintptr_t)y % 32 == 0 &&
-        (!base.e.aux || (uintptr_t)base.e.aux % 32 == 0) && (!base.e.residual || (uintptr_t)base.e.residual % 32 == 0)) {
+        Cin <= 4 && Cout % 8 == 0 && 256 % (Cout / 8) == 0 && (uintptr_t)y % 32 == 0 &&
+        (!base.e.aux || (uintptr_t)base.e.aux % 32 == 0) && (!base.e.residual || (uintptr_t)base.e.residual % 32 == 0) &&
+        (!base.e.dot_out || (uintptr_t)base.e.dot_src % 16 == 0)) {
+        if (base.e.dot_out) {
+            const int ppb = SK_ITERS * (256 / (Cout / 8));
+            dim3 g((unsigned)cdiv((int64_t)H * W, ppb), (unsigned)N);
+            SG2_DISPATCH(dtype, T, { conv1x1_smallk_dot_kernel<T><<<g, 256, 0, s>>>(base); });
+            return launch_status("sg2_conv2d (1x1, small Cin, dot)");
+        }
         const int64_t total = (int64_t)N * H * W * (Cout / 8);
         const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 64);
         SG2_DISPATCH(dtype, T, { conv1x1_smallk_kernel<T><<<g, 256, 0, s>>>(base); });

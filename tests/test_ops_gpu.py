@@ -717,14 +717,20 @@ def test_fused_torgb_and_f32_layer(dtype):
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float16])
-@pytest.mark.parametrize('geom', [(3, 2, 0, True), (3, 2, 0, False), (3, 1, 1, False), (1, 1, 0, False)])
+@pytest.mark.parametrize('geom', [(3, 2, 0, True), (3, 2, 0, False), (3, 1, 1, False), (1, 1, 0, False),
+                                  (1, 1, 0, True, 1, 64, 67, 61), (1, 1, 0, True, 3, 128, 9, 7),
+                                  (1, 1, 0, False, 2, 512, 16, 16)])
 def test_conv_fused_dot_and_scale(dtype, geom):
     """sg2_conv2d_fused: out_scale epilogue + per-(n, o) dot reduction against dot_src (the modulation
-    gradient of a dgrad), for plain / strided / transposed geometries."""
+    gradient of a dgrad), for plain / strided / transposed geometries; Cin <= 4 runs the 1x1 outer-product
+    kernel with its per-sample dot reduction (toRGB's input gradient), with pixel counts that leave the
+    last workgroup of each sample partly empty."""
     from torch_utils.ops import conv2d_gradfix as cg
-    k, stride, pad, transpose = geom
+    k, stride, pad, transpose = geom[:4]
     torch.manual_seed(29)
     N, Cin, Cout, H, W = 3, 32, 48, 12, 10
+    if len(geom) > 4:
+        Cin, Cout, H, W = geom[4:]
     x = torch.randn(N, Cin, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
     if transpose:
         w = (torch.randn(Cin, Cout, k, k, device=DEV) / (Cin * k * k) ** 0.5).to(dtype)
