@@ -170,18 +170,26 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
         for (int t = t_begin; t < t_end; ++t) {
             const bool more = t + 1 < t_end;
             if (more) gload(t + 1);
+            // rolling prefetch: B fragment tp of the next k-step is read into fb[tp] as soon as this
+            // step's MFMA tp has consumed it, so every MFMA's operands were read a whole step earlier (the
+            // compiler otherwise funnels the B reads through one register quad and waits before each MFMA)
+            auto rowk = [&](int k0) { return k0 + 8 * ((lane >> 4) >> 1); };   // this lane's 8 pixels: one tile row
+            auto hbk = [&](int k0) { const int pr = rowk(k0); return (pr / TW) * HWD + pr % TW; };
+            v8w<T> fa = frag32<T, SWZ>(gs, rowk(0), wa * 32, lane), fb[NT];
+#pragma unroll
+            for (int tp = 0; tp < NT; ++tp) fb[tp] = frag32<T, SWZ>(xs, hbk(0) + toff[tp], wb * 32, lane);
 #pragma unroll 2
             for (int k0 = 0; k0 < 256; k0 += 16) {
-                // this lane's 8 pixels: k0 + 8 * (lane >> 5) + j, all in one tile row
-                const int pr = k0 + 8 * ((lane >> 4) >> 1);
-                const int py = pr / TW, px = pr % TW;
-                const v8w<T> fa = frag32<T, SWZ>(gs, pr, wa * 32, lane);
-                const int hb = py * HWD + px;
+                const bool nx = k0 + 16 < 256;
+                const int kn = nx ? k0 + 16 : k0;
+                const v8w<T> fan = frag32<T, SWZ>(gs, rowk(kn), wa * 32, lane);
+                const int hn = hbk(kn);
 #pragma unroll
                 for (int tp = 0; tp < NT; ++tp) {
-                    const v8w<T> fb = frag32<T, SWZ>(xs, hb + toff[tp], wb * 32, lane);
-                    acc[tp] = mma32<T>(fa, fb, acc[tp]);
+                    acc[tp] = mma32<T>(fa, fb[tp], acc[tp]);
+                    fb[tp] = frag32<T, SWZ>(xs, hn + toff[tp], wb * 32, lane);
                 }
+                fa = fan;
             }
             __syncthreads();
             if (more) {
@@ -296,19 +304,25 @@ __global__ __launch_bounds__(256) void wgrad3x3_s2_kernel(W3Args a) {
         for (int t = t_begin; t < t_end; ++t) {
             const bool more = t + 1 < t_end;
             if (more) gload(t + 1);
+            // rolling prefetch of the next k-step's fragments (see wgrad3x3_kernel)
+            auto rowk = [&](int k0) { return k0 + 8 * ((lane >> 4) >> 1); };   // 8 pixels of one tile row
+            auto xrow = [&](int k0, int ky, int kx) {
+                const int pr = rowk(k0), py = pr / TW, px = pr % TW;
+                return (2 * py + ky) * XW + ((kx & 1) ? XEV : 0) + px + (kx >> 1);
+            };
+            v8w<T> fa = frag32<T, SWZ>(gs, rowk(0), wa * 32, lane), fb[9];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) fb[t] = frag32<T, SWZ>(xs, xrow(0, t / 3, t % 3), wb * 32, lane);
 #pragma unroll 2
             for (int k0 = 0; k0 < NP; k0 += 16) {
-                const int pr = k0 + 8 * ((lane >> 4) >> 1);   // 8 pixels of one tile row
-                const int py = pr / TW, px = pr % TW;
-                const v8w<T> fa = frag32<T, SWZ>(gs, pr, wa * 32, lane);
+                const int kn = k0 + 16 < NP ? k0 + 16 : k0;
+                const v8w<T> fan = frag32<T, SWZ>(gs, rowk(kn), wa * 32, lane);
 #pragma unroll
-                for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                    for (int kx = 0; kx < 3; ++kx) {
-                        const int row = (2 * py + ky) * XW + ((kx & 1) ? XEV : 0) + px + (kx >> 1);
-                        const v8w<T> fb = frag32<T, SWZ>(xs, row, wb * 32, lane);
-                        acc[ky * 3 + kx] = mma32<T>(fa, fb, acc[ky * 3 + kx]);
-                    }
+                for (int t = 0; t < 9; ++t) {
+                    acc[t] = mma32<T>(fa, fb[t], acc[t]);
+                    fb[t] = frag32<T, SWZ>(xs, xrow(kn, t / 3, t % 3), wb * 32, lane);
+                }
+                fa = fan;
             }
             __syncthreads();
             if (more) {
@@ -351,6 +365,14 @@ int dispatch_nt(const W3Args& a, dim3 grid, int nt, hipStream_t s) {
 
 int floordiv_w(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 
+// workgroups per launch the K (pixel) split aims at: one per CU (these kernels hold one workgroup per CU);
+// every workgroup adds its 64 x 9 x 64 partial sums with float atomics, so more workgroups cost atomics
+// (512: +10-25% time, 1024: +40-60%; profiles/r02_wgrad_wgs.log).  SG2_WGRAD_WGS overrides (tuning).
+int wgrad_wgs() {
+    static const int v = [] { const char* e = getenv("SG2_WGRAD_WGS"); return e ? std::max(1, atoi(e)) : 256; }();
+    return v;
+}
+
 }  // namespace
 
 // Is the halo weight gradient applicable?  (3x3 or 1x1 kernel, stride 1 or 2, every tap's shift on
@@ -379,12 +401,18 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
         a.tiles_y = (int)cdiv(OH, 8);
         a.tiles = N * a.tiles_x * a.tiles_y;
         const int cb = (int)(cdiv(A, BC) * cdiv(B, BC));
-        int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(512, cb), a.tiles / 4));
+        int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(wgrad_wgs(), cb), a.tiles / 4));
         a.tiles_per_block = (int)cdiv(a.tiles, splits);
         splits = (int)cdiv(a.tiles, a.tiles_per_block);
         dim3 grid((unsigned)cdiv(A, BC), (unsigned)cdiv(B, BC), (unsigned)splits);
-        if (dtype == SG2_F16) wgrad3x3_s2_kernel<f16_t, false><<<grid, 256, 0, s>>>(a);
-        else wgrad3x3_s2_kernel<bf16_t, false><<<grid, 256, 0, s>>>(a);
+        static const bool swz = [] { const char* e = getenv("SG2_WGRAD_SWZ"); return e != nullptr && e[0] == '1'; }();
+        if (dtype == SG2_F16) {
+            if (swz) wgrad3x3_s2_kernel<f16_t, true><<<grid, 256, 0, s>>>(a);
+            else wgrad3x3_s2_kernel<f16_t, false><<<grid, 256, 0, s>>>(a);
+        } else {
+            if (swz) wgrad3x3_s2_kernel<bf16_t, true><<<grid, 256, 0, s>>>(a);
+            else wgrad3x3_s2_kernel<bf16_t, false><<<grid, 256, 0, s>>>(a);
+        }
         return launch_status("sg2_conv2d_wgrad (halo, stride 2)");
     }
     const int TW = OW >= 32 ? 32 : 16;
@@ -393,7 +421,7 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
     a.tiles = N * a.tiles_x * a.tiles_y;
     const int cb = (int)(cdiv(A, BC) * cdiv(B, BC));
     // ~512 workgroups per launch, at least 4 tiles each
-    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(512, cb), a.tiles / 4));
+    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(wgrad_wgs(), cb), a.tiles / 4));
     a.tiles_per_block = (int)cdiv(a.tiles, splits);
     splits = (int)cdiv(a.tiles, a.tiles_per_block);
     dim3 grid((unsigned)cdiv(A, BC), (unsigned)cdiv(B, BC), (unsigned)splits);

@@ -30,13 +30,15 @@ def timeit(fn, reps=20):
 mode = os.environ.get('SG2_WGRAD_S2', '1')
 # (N, A = g channels, g size, B = x channels): D down layers (g = conv1 output grad, x = FIR'd input) and
 # the up layers' transposed convs (g = layer input, x = FIR-adjoint grad at 2h+1)
-for (n, a, gh, b) in [(32, 128, 128, 64), (32, 256, 64, 128), (32, 512, 32, 256), (32, 512, 16, 512),
-                      (32, 512, 16, 512), (32, 256, 64, 128), (32, 128, 128, 64)]:
-    xh = 2 * gh + 1
+CASES = [(32, 128, 128, 64, 2), (32, 256, 64, 128, 2), (32, 512, 32, 256, 2), (32, 512, 16, 512, 2),
+         (32, 64, 256, 64, 1), (32, 128, 128, 128, 1), (32, 256, 64, 256, 1), (32, 512, 32, 512, 1)]
+for (n, a, gh, b, st) in CASES:
+    xh = 2 * gh + 1 if st == 2 else gh
+    pad = 0 if st == 2 else 1
     g = torch.randn(n, a, gh, gh, device=dev).half().contiguous(memory_format=CL)
     x = torch.randn(n, b, xh, xh, device=dev).half().contiguous(memory_format=CL)
     flops = 2.0 * n * gh * gh * a * b * 9
-    t = timeit(lambda: cg._wgrad_raw(g, x, 3, 3, 2, (0, 0)))
-    dw = cg._wgrad_raw(g, x, 3, 3, 2, (0, 0))
-    print(f'S2={mode} N={n} A={a} g {gh}^2 B={b} x {xh}^2: {t:.3f} ms ({flops / t / 1e9:.0f} TF) '
+    t = timeit(lambda: cg._wgrad_raw(g, x, 3, 3, st, (pad, pad)))
+    dw = cg._wgrad_raw(g, x, 3, 3, st, (pad, pad))
+    print(f'S2={mode} SWZ={os.environ.get("SG2_WGRAD_SWZ", "0")} stride {st} N={n} A={a} g {gh}^2 B={b} x {xh}^2: {t:.3f} ms ({flops / t / 1e9:.0f} TF) '
           f'|dw| {dw.double().norm().item():.6e}', flush=True)
