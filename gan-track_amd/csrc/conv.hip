@@ -1207,7 +1207,10 @@ int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
     const int mt = (int)cdiv(a.A, BM), nt = (int)cdiv(a.B, BN);
     const int KK = a.KH * a.KW;
     const int chunks = (int)cdiv(a.M, BK);
-    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(chunks / 8, cdiv(2048, (int64_t)mt * nt * KK)));
+    // workgroups the pixel split aims at (every workgroup adds a BM x BN partial per tap with float atomics);
+    // SG2_CWGRAD_WGS overrides (tuning runs)
+    static const int target = [] { const char* e = getenv("SG2_CWGRAD_WGS"); return e ? std::max(1, atoi(e)) : 2048; }();
+    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(chunks / 8, cdiv(target, (int64_t)mt * nt * KK)));
     a.kper = (int)cdiv(chunks, splits) * BK;
     a.splits = (int)cdiv(a.M, a.kper);
     dim3 grid(mt, nt, KK * a.splits);
@@ -1352,8 +1355,11 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
         }
         int splits = 1;
         const int64_t total_out = (int64_t)N * OH * OW * Cout;
+        // split-K target 512 workgroups (tools/split_ab.py, profiles/r02_split_ab.log: f32 16^2 / 8^2 / 4^2 fwd
+        // 0.281 / 0.103 / 0.056 ms at 1024 -> 0.263 / 0.083 / 0.044 at 512); SG2_CONV_SPLIT_WGS overrides
+        static const int target = [] { const char* e = getenv("SG2_CONV_SPLIT_WGS"); return e ? std::max(1, atoi(e)) : 512; }();
         if (blocks < 512 && workspace != nullptr && workspace_elems >= total_out)
-            splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(1024, blocks), maxnk / 4));
+            splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(target, blocks), maxnk / 4));
         const bool split = splits > 1;
         if (split) {
             hipError_t e = hipMemsetAsync(workspace, 0, total_out * sizeof(float), s);
