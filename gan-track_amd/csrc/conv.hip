@@ -1268,7 +1268,7 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
         SG2_CHECK((e.dot_src == nullptr) == (e.dot_out == nullptr), "sg2_conv2d: dot_src and dot_out go together");
         SG2_CHECK(!(e.dot_out && e.aux_mode == 2), "sg2_conv2d: the dot reduction needs aux_mode 0 or 1");
         if (e.dot_out) {
-            hipError_t er = hipMemsetAsync(e.dot_out, 0, (size_t)N * Cout * sizeof(float), s);
+            hipError_t er = zero_acc(e.dot_out, (size_t)N * Cout * sizeof(float), s);
             if (er != hipSuccess) { set_error("sg2_conv2d: memset failed"); return (int)er; }
         }
     }
@@ -1411,7 +1411,7 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     SG2_CHECK((int64_t)N * OH * OW * A * 4 < INT32_MAX && (int64_t)N * H * W * B * 4 < INT32_MAX,
               "sg2_conv2d_wgrad: tensor too large (32-bit byte offsets of the buffer loads)");
     hipStream_t s = as_stream(stream);
-    hipError_t e = hipMemsetAsync(dw, 0, (int64_t)A * KH * KW * B * sizeof(float), s);
+    hipError_t e = zero_acc(dw, (int64_t)A * KH * KW * B * sizeof(float), s);
     if (e != hipSuccess) { set_error("sg2_conv2d_wgrad: memset failed"); return (int)e; }
     WgradArgs a{};
     a.g = g; a.x = x; a.dw = dw; a.b_scale = x_scale; a.a_scale = g_scale;

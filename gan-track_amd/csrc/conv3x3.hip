@@ -666,7 +666,7 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     const bool si = a.in_scale != nullptr;
     const bool epi = a.out_scale || a.noise || a.bias || a.act != 0 || a.gain != 1.f || a.clamp >= 0.f;
     if (a.dot_out) {
-        hipError_t e = hipMemsetAsync(a.dot_out, 0, (size_t)a.N * a.Cout * sizeof(float), s);
+        hipError_t e = zero_acc(a.dot_out, (size_t)a.N * a.Cout * sizeof(float), s);
         if (e != hipSuccess) { set_error("sg2_conv3x3: memset failed"); return (int)e; }
     }
     if (stride == 2) {   // 32 x 4 output tiles, two workgroups per CU

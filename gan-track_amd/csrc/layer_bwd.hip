@@ -181,11 +181,11 @@ extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, cons
     SG2_CHECK((int64_t)N * HW * C * 4 < INT32_MAX, "sg2_layer_bwd: tensor too large (32-bit buffer offsets)");
     hipStream_t s = as_stream(stream);
     if (db && dd == db + C) {   // adjacent accumulators (the Python wrapper's layout): one memset
-        hipError_t e = hipMemsetAsync(db, 0, ((int64_t)N + 1) * C * sizeof(float), s);
+        hipError_t e = zero_acc(db, ((int64_t)N + 1) * C * sizeof(float), s);
         if (e) { set_error("memset"); return e; }
     } else {
-        if (db) { hipError_t e = hipMemsetAsync(db, 0, C * sizeof(float), s); if (e) { set_error("memset"); return e; } }
-        if (dd) { hipError_t e = hipMemsetAsync(dd, 0, (int64_t)N * C * sizeof(float), s); if (e) { set_error("memset"); return e; } }
+        if (db) { hipError_t e = zero_acc(db, C * sizeof(float), s); if (e) { set_error("memset"); return e; } }
+        if (dd) { hipError_t e = zero_acc(dd, (int64_t)N * C * sizeof(float), s); if (e) { set_error("memset"); return e; } }
     }
     LBArgs a{};
     a.dy = dy; a.y = y; a.c = c; a.d = d; a.dc = dc; a.db = db; a.dd = dd; a.dnoise = dnoise;

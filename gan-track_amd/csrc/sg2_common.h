@@ -27,6 +27,14 @@ void set_error(const std::string& msg);
         }                                        \
     } while (0)
 
+// Zeroing of an entry point's float accumulator outputs (dot_out, dw, db / dd).  While the host thread has
+// sg2_set_zeroed_accumulators(1) in effect the caller has zeroed them itself (one fill for all of a layer's
+// accumulators instead of a memset per call), and this is a no-op.
+bool accumulators_prezeroed();
+inline hipError_t zero_acc(void* p, size_t bytes, hipStream_t s) {
+    return accumulators_prezeroed() ? hipSuccess : hipMemsetAsync(p, 0, bytes, s);
+}
+
 inline int launch_status(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -4,6 +4,7 @@ The product path has no fallback: if the library is missing, or a tensor is not 
 device, every op raises.  (The reference's ops silently fall back to slow `_ref` paths on CPU,
 SG3/torch_utils/ops/upfirdn2d.py:160-162; here that would hide a broken build, so it is an error.)
 """
+import contextlib
 import ctypes
 import os
 
@@ -42,6 +43,7 @@ SIGNATURES = {
                          ctypes.POINTER(Epilogue), _vp, _i64, _vp],
     'sg2_conv3x3': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _f, _f, _f, _vp, _vp,
                     _vp],
+    'sg2_set_zeroed_accumulators': [_i],
     'sg2_conv3x3_s2': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _f, _f, _f, _vp, _i,
                        _vp, _vp, _vp],
     'sg2_conv3x3_up2': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp],
@@ -84,10 +86,26 @@ def lib():
             fn.restype = ctypes.c_int
         L.sg2_last_error.argtypes = []
         L.sg2_last_error.restype = ctypes.c_char_p
+        L.sg2_set_zeroed_accumulators.restype = None
         if L.sg2_abi_version() != ABI_VERSION:
             raise RuntimeError(f'sg2hip: ABI version mismatch ({L.sg2_abi_version()} != {ABI_VERSION})')
         _lib = L
     return _lib
+
+
+@contextlib.contextmanager
+def zeroed_accumulators(on=True):
+    """Calls inside skip zeroing their float accumulator outputs (sg2_set_zeroed_accumulators): the
+    caller passed buffers it zeroed itself, one fill for all of a layer's accumulators."""
+    if not on:
+        yield
+        return
+    L = lib()
+    L.sg2_set_zeroed_accumulators(1)
+    try:
+        yield
+    finally:
+        L.sg2_set_zeroed_accumulators(0)
 
 
 def check(rc, what):

@@ -92,10 +92,11 @@ def _conv_raw(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose):
 
 def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_scale=None, out_scale=None,
                noise=None, noise_gain=1.0, bias=None, act=0, alpha=0.2, gain=1.0, clamp=-1.0, residual=None,
-               aux_mode=0, dot_src=None):
+               aux_mode=0, dot_src=None, dot_out=None):
     """sg2_conv2d_fused: y = round(clamp(act(conv(x * in_scale, w) * out_scale + noise * g + bias) * gain))
     + residual.  Returns (y, aux) with aux = conv result (aux_mode 1) or activation (aux_mode 2); with
-    dot_src also dot[n, o] = sum_p conv(...)[n, o, p] * dot_src[n, o, p] -> (y, aux, dot)."""
+    dot_src also dot[n, o] = sum_p conv(...)[n, o, p] * dot_src[n, o, p] -> (y, aux, dot).  dot_out: a
+    zeroed f32 [N, Cout] buffer for dot (the call then skips its own memset)."""
     if (out_scale is None and noise is None and bias is None and residual is None and dot_src is None and act == 0 and
             gain == 1.0 and clamp < 0 and not aux_mode and _up2_ok(x, cout, oh, ow, kh, kw, stride, pad, transpose)):
         return _conv_up2(x, wp, cout, in_scale), None
@@ -109,7 +110,7 @@ def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_sca
     if dot_src is not None:
         dot_src = _nhwc(dot_src)
         assert dot_src.shape == y.shape and dot_src.dtype == y.dtype
-        dot = torch.empty([n, cout], dtype=torch.float32, device=x.device)
+        dot = dot_out if dot_out is not None else torch.empty([n, cout], dtype=torch.float32, device=x.device)
     epi = None
     if any(v is not None for v in (out_scale, noise, bias, residual, dot_src)) or act != 0 or gain != 1.0 or \
             clamp >= 0 or aux_mode:
@@ -118,22 +119,26 @@ def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_sca
                             _hip.ptr(dot_src), _hip.ptr(dot))
     total = n * cout * oh * ow
     ws = torch.empty([total], dtype=torch.float32, device=x.device) if total <= _WS_LIMIT else None
-    _hip.check(_hip.lib().sg2_conv2d_fused(
-        _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
-        stride, pad[0], pad[1], int(transpose), _hip.ptr(in_scale), ctypes.byref(epi) if epi is not None else None,
-        _hip.ptr(ws), ws.numel() if ws is not None else 0, _hip.stream_ptr(x.device)), 'sg2_conv2d_fused')
+    with _hip.zeroed_accumulators(dot_out is not None and dot is not None):
+        _hip.check(_hip.lib().sg2_conv2d_fused(
+            _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
+            stride, pad[0], pad[1], int(transpose), _hip.ptr(in_scale), ctypes.byref(epi) if epi is not None else None,
+            _hip.ptr(ws), ws.numel() if ws is not None else 0, _hip.stream_ptr(x.device)), 'sg2_conv2d_fused')
     return (y, aux, dot) if dot_src is not None else (y, aux)
 
 
-def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None, alpha=1.0):
+def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None, alpha=1.0, out=None):
     """dw[a, b, ky, kx] = alpha * sum g[n,a,oy,ox] (* g_scale[n,a]) x[n,b,oy*s+ky-p,ox*s+kx-p] (* x_scale[n,b]);
-    returns f32 [A,B,kh,kw] (NHWC-packed).  alpha: a layer's weight gain (the backward of w * gain)."""
+    returns f32 [A,B,kh,kw] (NHWC-packed).  alpha: a layer's weight gain (the backward of w * gain).
+    out: a zeroed f32 buffer of A*kh*kw*B elements to accumulate into (the call skips its memset)."""
     n, a, oh, ow = g.shape
     _, b, h, w = x.shape
-    dw = torch.empty([a, kh, kw, b], dtype=torch.float32, device=g.device)
-    _hip.check(_hip.lib().sg2_conv2d_wgrad(
-        _hip.ptr(dw), _hip.ptr(g), _hip.ptr(x), _hip.dtype_code(g), n, a, oh, ow, b, h, w, kh, kw, stride,
-        pad[0], pad[1], _hip.ptr(g_scale), _hip.ptr(x_scale), float(alpha), _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad')
+    dw = out.view(a, kh, kw, b) if out is not None else torch.empty([a, kh, kw, b], dtype=torch.float32, device=g.device)
+    with _hip.zeroed_accumulators(out is not None):
+        _hip.check(_hip.lib().sg2_conv2d_wgrad(
+            _hip.ptr(dw), _hip.ptr(g), _hip.ptr(x), _hip.dtype_code(g), n, a, oh, ow, b, h, w, kh, kw, stride,
+            pad[0], pad[1], _hip.ptr(g_scale), _hip.ptr(x_scale), float(alpha), _hip.stream_ptr(g.device)),
+            'sg2_conv2d_wgrad')
     return dw.permute(0, 3, 1, 2)
 
 
@@ -188,7 +193,7 @@ def _halo_s2_ok(x, kh, kw, stride, pad, dot=False):
 
 def conv3x3_fused(x, wp, cout, in_scale=None, out_scale=None, noise=None, noise_gain=0.0, bias=None, act=0,
                   alpha=0.2, gain=1.0, clamp=-1.0, want_raw=False, dot_src=None, stride=1, residual=None,
-                  raw_act=False):
+                  raw_act=False, dot_out=None):
     """sg2_conv3x3 (stride 1, pad 1) / sg2_conv3x3_s2 (stride 2, pad 0) launch.  x NHWC 16-bit, wp packed
     [Cout][3][3][Cin].  Returns (y, raw or None, dot or None) with dot[n,o] = sum_p conv(x)[n,o,p] *
     dot_src[n,o,p]; with stride 2 an optional residual is added after the epilogue and raw_act makes raw
@@ -201,46 +206,54 @@ def conv3x3_fused(x, wp, cout, in_scale=None, out_scale=None, noise=None, noise_
     if dot_src is not None:
         dot_src = _nhwc(dot_src)
         assert dot_src.shape == y.shape and dot_src.dtype == y.dtype
-        dot = torch.empty([n, cout], dtype=torch.float32, device=x.device)
+        dot = dot_out if dot_out is not None else torch.empty([n, cout], dtype=torch.float32, device=x.device)
     lib = _hip.lib()
+    zeroed = dot_out is not None and dot is not None   # the caller zeroed dot_out (no memset in the call)
     common = (_hip.ptr(y), _hip.ptr(raw), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout,
               _hip.ptr(in_scale), _hip.ptr(out_scale), _hip.ptr(noise), float(noise_gain), _hip.ptr(bias), int(act),
               float(alpha), float(gain), float(clamp))
     if stride == 1:
         assert residual is None
-        _hip.check(lib.sg2_conv3x3(*common, _hip.ptr(dot_src), _hip.ptr(dot), _hip.stream_ptr(x.device)),
-                   'sg2_conv3x3')
+        with _hip.zeroed_accumulators(zeroed):
+            _hip.check(lib.sg2_conv3x3(*common, _hip.ptr(dot_src), _hip.ptr(dot), _hip.stream_ptr(x.device)),
+                       'sg2_conv3x3')
     else:
         assert stride == 2
         if residual is not None:
             residual = _nhwc(residual)
             assert residual.shape == y.shape and residual.dtype == y.dtype
-        _hip.check(lib.sg2_conv3x3_s2(*common, _hip.ptr(residual), int(bool(raw_act)), _hip.ptr(dot_src),
-                                      _hip.ptr(dot), _hip.stream_ptr(x.device)), 'sg2_conv3x3_s2')
+        with _hip.zeroed_accumulators(zeroed):
+            _hip.check(lib.sg2_conv3x3_s2(*common, _hip.ptr(residual), int(bool(raw_act)), _hip.ptr(dot_src),
+                                          _hip.ptr(dot), _hip.stream_ptr(x.device)), 'sg2_conv3x3_s2')
     return (y, raw, dot) if dot_src is not None else (y, raw)
 
 
 def layer_bwd(dy, y, c=None, d=None, act=1, alpha=0.2, gain=1.0, clamp=-1.0, want_db=True, want_dd=True,
-              want_dnoise=True):
-    """sg2_layer_bwd: returns (dc, db[C] or None, dd[N,C] or None, dnoise[N,1,H,W] or None)."""
+              want_dnoise=True, acc=None):
+    """sg2_layer_bwd: returns (dc, db[C] or None, dd[N,C] or None, dnoise[N,1,H,W] or None).  acc: a zeroed
+    f32 buffer of (C if want_db) + (N*C if want_dd) elements holding db then dd (no memset in the call)."""
     y = _nhwc(y)
     dy = _nhwc(dy)
     n, ch, h, w = y.shape
     dc = torch.empty_like(y)
     f32 = dict(dtype=torch.float32, device=y.device)
     want_dd = want_dd and d is not None
-    if want_db and want_dd:   # one buffer: the library zeroes both accumulators with one memset
-        acc = torch.empty([ch + n * ch], **f32)
-        db, dd = acc[:ch], acc[ch:].view(n, ch)
+    if acc is not None:
+        db = acc[:ch] if want_db else None
+        dd = acc[(ch if want_db else 0):][:n * ch].view(n, ch) if want_dd else None
+    elif want_db and want_dd:   # one buffer: the library zeroes both accumulators with one memset
+        buf = torch.empty([ch + n * ch], **f32)
+        db, dd = buf[:ch], buf[ch:].view(n, ch)
     else:
         db = torch.empty([ch], **f32) if want_db else None
         dd = torch.empty([n, ch], **f32) if want_dd else None
     dn = torch.empty([n, 1, h, w], **f32) if want_dnoise else None
     c = _nhwc(c) if c is not None else None
-    _hip.check(_hip.lib().sg2_layer_bwd(
-        _hip.ptr(dc), _hip.ptr(db), _hip.ptr(dd), _hip.ptr(dn), _hip.ptr(dy), _hip.ptr(y), _hip.ptr(c),
-        _hip.ptr(d), _hip.dtype_code(y), n, h * w, ch, int(act), float(alpha), float(gain), float(clamp),
-        _hip.stream_ptr(y.device)), 'sg2_layer_bwd')
+    with _hip.zeroed_accumulators(acc is not None):
+        _hip.check(_hip.lib().sg2_layer_bwd(
+            _hip.ptr(dc), _hip.ptr(db), _hip.ptr(dd), _hip.ptr(dn), _hip.ptr(dy), _hip.ptr(y), _hip.ptr(c),
+            _hip.ptr(d), _hip.dtype_code(y), n, h * w, ch, int(act), float(alpha), float(gain), float(clamp),
+            _hip.stream_ptr(y.device)), 'sg2_layer_bwd')
     return dc, db, dd, dn
 
 

@@ -20,6 +20,8 @@ Backward:
     differentiable primitives (bias_act grad op, HIP conv / transposed conv / weight-gradient
     Functions), and c is recomputed as a differentiable conv so d(dL/dd)/dW, /ds, /dx exist.
 """
+import os
+
 import torch
 
 from . import bias_act as _ba
@@ -28,6 +30,7 @@ from . import upfirdn2d as _up
 
 _CL = torch.channels_last
 enabled = True         # switch for A/B tests against the composed (unfused) path
+prezero = os.environ.get('SG2_PREZERO', '1') != '0'   # one zero fill per layer backward (A/B switch)
 fast_backward = True   # first-order backward through the fused kernels (A/B switch)
 _ACT = {0: 'linear', 1: 'lrelu'}
 
@@ -112,33 +115,36 @@ class FusedConv(torch.autograd.Function):
         return g + (dres, None, None, None, None, None, None, None)
 
 
-def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, pad, wgain=1.0):
+def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, pad, wgain=1.0, acc_ds=None,
+                        acc_dw=None):
     """Gradients of c = conv(x * s, W) given dc: dx = convT(dc, W) * s and ds = sum_hw convT(dc, W) * x in
-    one dgrad launch (out_scale / dot_src epilogue), dw = the s-scaled weight gradient."""
+    one dgrad launch (out_scale / dot_src epilogue), dw = the s-scaled weight gradient.  acc_ds / acc_dw:
+    zeroed f32 buffers (N*Cin / Cout*kh*kw*Cin) the reductions accumulate into (no memset per call)."""
     n, cin, h, w = x.shape
     cout, _, kh, kw = weight.shape
     dt = x.dtype
     dx = ds = dw = None
     s32 = _f32(styles)
     want_ds = need_s and styles is not None
+    dso = acc_ds.view(n, cin) if (want_ds and acc_ds is not None) else None
     if need_x or want_ds:
         if _halo(dc, kh, kw, stride, pad):
             wT = _cg._pack_convT(weight, dt, flip=True, scale=wgain)
             if want_ds:
-                dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x)
+                dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x, dot_out=dso)
             else:
                 dx, _ = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32)
         else:
             if want_ds:
                 dx, _, ds = _cg.conv_fused(dc, _cg._pack_convT(weight, dt, scale=wgain), cin, h, w, kh, kw, stride,
-                                           (pad, pad), transpose=True, out_scale=s32, dot_src=x)
+                                           (pad, pad), transpose=True, out_scale=s32, dot_src=x, dot_out=dso)
             else:
                 dx, _ = _cg.conv_fused(dc, _cg._pack_convT(weight, dt, scale=wgain), cin, h, w, kh, kw, stride,
                                        (pad, pad), transpose=True, out_scale=s32)
         ds = ds.to(styles.dtype) if want_ds else None
         dx = dx if need_x else None
     if need_w and not _cg.weight_gradients_disabled:
-        dw = _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32, alpha=wgain).to(weight.dtype)
+        dw = _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32, alpha=wgain, out=acc_dw).to(weight.dtype)
     return dx, ds, dw
 
 
@@ -234,16 +240,31 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
     d32 = _f32(dcoefs)
     want_dd = need[3] and d32 is not None
     want_db, want_dn = need[5] and bias is not None, need[4] and noise is not None
-    if zsrc.shape[1] % 8 == 0:
+    # one zero fill for all of the layer's float accumulators (db, dd, ds, dw) instead of a memset per kernel
+    wide = zsrc.shape[1] % 8 == 0
+    want_ds = need[1] and styles is not None and (need[0] or need[1])
+    want_dw = need[2] and not _cg.weight_gradients_disabled
+    sizes = [cout if (wide and want_db) else 0, n * cout if (wide and want_dd) else 0, n * cin if want_ds else 0,
+             cout * kh * kw * cin if want_dw else 0]
+    if not prezero:
+        sizes = [0, 0, 0, 0]
+    acc = torch.zeros([sum(sizes)], dtype=torch.float32, device=dy.device) if sum(sizes) else None
+    parts, o = [], 0
+    for k in sizes:
+        parts.append(acc[o:o + k] if k else None)
+        o += k
+    if wide:
+        lb = acc[:sizes[0] + sizes[1]] if sizes[0] + sizes[1] else None
         dc, db, dd, dn = _cg.layer_bwd(dy.to(dt), zsrc, c if want_dd else None, d32, act=act, alpha=alpha, gain=gain,
-                                       clamp=clamp, want_db=want_db, want_dd=want_dd, want_dnoise=want_dn)
+                                       clamp=clamp, want_db=want_db, want_dd=want_dd, want_dnoise=want_dn, acc=lb)
     else:   # narrow outputs (toRGB): plain kernels
         dz = _ba.bias_act_grad(dy, zsrc, act=_ACT[act], alpha=alpha, gain=gain, clamp=clamp)
         db = dz.sum([0, 2, 3], dtype=torch.float32) if want_db else None
         dd = (dz * c).sum([2, 3], dtype=torch.float32) if want_dd else None
         dn = dz.sum(1, keepdim=True, dtype=torch.float32) if want_dn else None
         dc = _cg._nhwc(dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None else dz)
-    dx, ds, dw = _scaled_input_grads(dc, x, styles, weight, need[0], need[1], need[2], stride, pad, wgain)
+    dx, ds, dw = _scaled_input_grads(dc, x, styles, weight, need[0], need[1], need[2], stride, pad, wgain,
+                                     acc_ds=parts[2], acc_dw=parts[3])
     db = db.to(bias.dtype) if db is not None else None
     dd = dd.to(dcoefs.dtype) if dd is not None else None
     dn = dn.to(noise.dtype) if dn is not None else None

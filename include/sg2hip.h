@@ -145,6 +145,12 @@ int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, int dtype, i
                 const float* bias, int act, float alpha, float gain, float clamp, const void* dot_src,
                 float* dot_out, void* stream);
 
+/* While on (per host thread), the entry points below skip zeroing their float accumulator outputs --
+ * sg2_conv2d_fused / sg2_conv3x3 / sg2_conv3x3_s2 dot_out, sg2_conv2d_wgrad dw, sg2_layer_bwd db / dd --
+ * because the caller zeroed them (one fill for all of a layer's accumulators instead of one memset per
+ * call).  Default off. */
+void sg2_set_zeroed_accumulators(int on);
+
 /* Stride-2 / pad-0 form of sg2_conv3x3 (conv2d_resample.py:139-142 with down = 2: the discriminator's
  * down-2 3x3 layers after their FIR pre-filter, and the input gradient of the up-2 synthesis layers):
  * x [N, H, W, Cin] -> y [N, (H-3)/2+1, (W-3)/2+1, Cout]; same epilogue and dot as sg2_conv3x3, plus

@@ -13,7 +13,7 @@ HEADER = os.path.join(ROOT, 'include', 'sg2hip.h')
 
 def header_symbols():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r'^\s*(?:int|const char\*)\s+(sg2_\w+)\s*\(', text, flags=re.M)))
+    return sorted(set(re.findall(r'^\s*(?:int|void|const char\*)\s+(sg2_\w+)\s*\(', text, flags=re.M)))
 
 
 def test_header_parses():

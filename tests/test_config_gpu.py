@@ -31,9 +31,12 @@ GROUPS = ['grad/Gmain', 'grad/Greg', 'grad/Dmain', 'grad/Dreg', 'G1', 'D1', 'Gem
 # 16-bit storage, f32 accumulate: per-group flat relative error vs the float64 answer must stay below
 # max(floor, 2 x the reference's own f32 error on that group) -- the reference's f32 CPU result is itself
 # off by up to 9% (C2 Dreg) / 16% (C5 Dreg) there.  Floors: the measured 16-bit errors
-# (profiles/r02_config_parity.jsonl) with ~1.5x margin.
+# (profiles/r02_config_parity.jsonl) with ~1.5x margin.  The regularisation phases are the noisy ones:
+# the product's float atomics make repeated runs differ, and at C2 fp16 six runs gave Greg flat errors of
+# 0.055-0.093 and Dreg 0.066-0.16 (profiles/r02_c2_fp16_repeats.jsonl), so their floors are 1.5x the
+# largest of those.
 FLOOR16 = {
-    'fp16': {'grad/Gmain': 0.03, 'grad/Greg': 0.08, 'grad/Dmain': 0.05, 'grad/Dreg': 0.17, 'param': 1e-3},
+    'fp16': {'grad/Gmain': 0.03, 'grad/Greg': 0.14, 'grad/Dmain': 0.05, 'grad/Dreg': 0.24, 'param': 1e-3},
     'bf16': {'grad/Gmain': 0.06, 'grad/Greg': 0.2, 'grad/Dmain': 0.06, 'grad/Dreg': 0.15, 'param': 2e-3},
 }
 
