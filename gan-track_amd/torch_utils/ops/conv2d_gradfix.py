@@ -142,10 +142,43 @@ def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None, alpha=1.0,
     return dw.permute(0, 3, 1, 2)
 
 
+_pack_cache = None   # {key: packed} while a pack_cache() scope is open
+
+
+@contextlib.contextmanager
+def pack_cache():
+    """Reuse weight packs inside the scope: a training phase packs every conv weight of D twice per form
+    (the fake and the real pass of Dmain, their backward), with the parameters unchanged in between.  Only
+    packs of parameters (or views of them) are cached, keyed by storage, version, view geometry and the
+    pack form; the trainer opens one scope per phase (eagerly or while capturing the phase's graph), so
+    the optimizer step never runs inside one."""
+    global _pack_cache
+    prev = _pack_cache
+    _pack_cache = {} if prev is None else prev
+    try:
+        yield
+    finally:
+        _pack_cache = prev
+
+
 def _pack(w, a_dim, dtype, flip, scale=1.0):
     """out[a][ky][kx][b] = scale * w[.., ky', kx'] with (a, b) = dims (a_dim, 1 - a_dim) of w, cast to dtype,
     the taps reversed when flip -- one sg2_pack_weight launch instead of a strided copy (and, with scale, of
     the reference's `weight * weight_gain` multiply)."""
+    key = None
+    if _pack_cache is not None and (isinstance(w, torch.nn.Parameter) or isinstance(w._base, torch.nn.Parameter)):
+        base = w if isinstance(w, torch.nn.Parameter) else w._base
+        key = (w.data_ptr(), base._version, tuple(w.shape), tuple(w.stride()), a_dim, dtype, bool(flip), float(scale))
+        hit = _pack_cache.get(key)
+        if hit is not None:
+            return hit[0]
+    out = _pack_raw(w, a_dim, dtype, flip, scale)
+    if key is not None:
+        _pack_cache[key] = (out, w)    # (w keeps the parameter view alive for the scope)
+    return out
+
+
+def _pack_raw(w, a_dim, dtype, flip, scale):
     b_dim = 1 - a_dim
     A, B, kh, kw = w.shape[a_dim], w.shape[b_dim], w.shape[2], w.shape[3]
     if kh * kw > 9:    # no such conv in the networks; layout copy on the device

@@ -27,6 +27,7 @@ import torch
 
 import dnnlib
 from torch_utils import misc
+from torch_utils.ops import conv2d_gradfix
 from torch_utils import training_stats
 from training.optim import FlatAdam, EmaLerp, fused_adam_ok
 
@@ -223,11 +224,12 @@ class Trainer:
 
     def _accumulate(self, phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c):
         chunks = list(zip(phase_real_img, phase_real_c, phase_gen_z, phase_gen_c))
-        for ci, (real_img, real_c, gen_z, gen_c) in enumerate(chunks):
-            if ci == len(chunks) - 1:
-                phase.exchange.arm(phase.name, self._passes(phase.name))
-            self.loss.accumulate_gradients(phase=phase.name, real_img=real_img, real_c=real_c, gen_z=gen_z,
-                                           gen_c=gen_c, gain=phase.interval, cur_nimg=self.cur_nimg)
+        with conv2d_gradfix.pack_cache():   # the phase's weights are fixed until its optimizer step
+            for ci, (real_img, real_c, gen_z, gen_c) in enumerate(chunks):
+                if ci == len(chunks) - 1:
+                    phase.exchange.arm(phase.name, self._passes(phase.name))
+                self.loss.accumulate_gradients(phase=phase.name, real_img=real_img, real_c=real_c, gen_z=gen_z,
+                                               gen_c=gen_c, gain=phase.interval, cur_nimg=self.cur_nimg)
 
     def _graph_phase(self, phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c):
         """Replay the phase's graph (capturing it the first time): forward + backward of every micro-batch,
