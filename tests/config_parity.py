@@ -233,10 +233,12 @@ def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
 
 def judge_flat(got_flat, ref_flat, floor, factor=3.0):
     """Per group: the estimated whole-vector error vs f64 (compare_flat) within max(floor, factor x the
-    reference f32's)."""
+    reference f32's).  `floor` is one number or (norm-vector floor, sampled-entry floor)."""
+    fn, fs = floor if isinstance(floor, tuple) else (floor, floor)
     for g, (en, es) in got_flat.items():
-        t = max(floor, factor * max(ref_flat[g]))
-        assert en <= t and es <= t, f'{g}: norm-vector err {en:.3g}, flat err {es:.3g} (bound {t:.3g})'
+        tn = max(fn, factor * max(ref_flat[g]))
+        ts = max(fs, factor * max(ref_flat[g]))
+        assert en <= tn and es <= ts, f'{g}: norm-vector err {en:.3g} (bound {tn:.3g}), flat err {es:.3g} (bound {ts:.3g})'
 
 
 # The regulariser statistics inherit the conditioning of the gradients they are built from: J^T y of the

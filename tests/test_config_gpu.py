@@ -78,7 +78,10 @@ def test_f32_iteration_vs_reference(tag):
     cp.judge_stats_f32(stats, fix)
     cp.judge_pl_mean(got, fix)
     cp.judge_flat({g: v for g, v in flat.items() if g.startswith('grad/')}, ref_flat, floor=1e-4)
-    cp.judge_flat({g: v for g, v in flat.items() if not g.startswith('grad/')}, ref_flat, floor=1e-5)
+    # Parameters after the step: Adam's first step with beta1 = 0 moves an entry by ~lr * sign(g), so an entry
+    # whose gradient is within f32 (atomic-order) noise of zero can land 2 * lr from the float64 answer.  The
+    # norms stay at 1e-5; the sampled entries get 1e-4 (measured 1.3e-5 at C2, 2.8e-5 at C4 on r02_v4).
+    cp.judge_flat({g: v for g, v in flat.items() if not g.startswith('grad/')}, ref_flat, floor=(1e-5, 1e-4))
 
 
 @pytest.mark.timeout(240)
