@@ -155,9 +155,11 @@ def _measured_traffic(key):
     try:
         with open(os.path.join(ROOT, 'profiles', 'roofline_traffic.json')) as f:
             t = json.load(f)
-        return t['hbm_bytes_per_launch'] if t.get('config') == key else None
+        if t.get('config') != key:
+            return None, None
+        return t['hbm_bytes_per_launch'], t.get('hbm_bytes_per_launch_x2_rule')
     except (OSError, ValueError, KeyError):
-        return None
+        return None, None
 
 
 def roofline(device, res, cbase, dtype):
@@ -181,7 +183,8 @@ def roofline(device, res, cbase, dtype):
     else:
         out.update({'bound': 'mfma', 'achieved': round(tflops, 2), 'peak': MFMA_PEAK_FP16, 'unit': 'TFLOP/s',
                     'frac': round(tflops / MFMA_PEAK_FP16, 4)})
-    out.update({'traffic': _measured_traffic(key), 'ms_per_launch': round(ms, 4),
+    traffic, traffic_x2 = _measured_traffic(key)
+    out.update({'traffic': traffic, 'traffic_fetch_x2_rule': traffic_x2, 'ms_per_launch': round(ms, 4),
                 'algorithmic_flops_per_launch': flops, 'algorithmic_hbm_bytes_per_launch': byts,
                 'arithmetic_intensity': round(ai, 1), 'ridge': round(ridge, 1),
                 'mfma_tflops': round(tflops, 1), 'mfma_frac': round(tflops / MFMA_PEAK_FP16, 4)})

@@ -67,4 +67,22 @@ if step micro; then
     (cd "$R" && timeout -k 10 300 python -u tools/conv_micro.py > "$O/micro.log" 2>&1)
     rc=$?; grep -v amdgpu.ids "$O/micro.log"; [ $rc -eq 0 ] || exit $rc
 fi
+if step calib; then
+    # FETCH_SIZE calibration for the C=64 conv's half-line reads (tools/pmc_calib.py)
+    for lib in default d3; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+            echo "== calib $lib $c"
+            if [ $lib = default ]; then unset SG2HIP_LIB; else export SG2HIP_LIB="$R/tools/diag_libs/libsg2hip_$lib.so"; fi
+            timeout -s KILL 120 rocprofv3 --pmc $c -d "$O/calib_${lib}_$c" -o run --output-format csv \
+                -- python3 "$R/tools/pmc_calib.py" > "$O/calib_${lib}_$c.log" 2>&1
+            rc=$?; tail -1 "$O/calib_${lib}_$c.log"; [ $rc -eq 0 ] || exit $rc
+        done
+    done
+    unset SG2HIP_LIB
+fi
+if step wgswz; then
+    echo "== wgrad LDS swizzle A/B"
+    (cd "$R" && for sw in 0 1 0 1; do echo "SWZ=$sw"; SG2_WGRAD_SWZ=$sw timeout -k 10 120 python3 -u tools/wgrad_s2_ab.py || exit 1; done > "$O/wgswz.log" 2>&1)
+    rc=$?; grep -v amdgpu.ids "$O/wgswz.log"; [ $rc -eq 0 ] || exit $rc
+fi
 echo "== done"

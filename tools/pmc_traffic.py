@@ -11,6 +11,7 @@ Usage: python tools/pmc_traffic.py <gpurun_out/tag> [out.json]"""
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
 
@@ -40,17 +41,27 @@ res = {c: per_kernel(c) for c in ('FETCH_SIZE', 'WRITE_SIZE')}
 if any(v is None for v in res.values()):
     print('no data')
     sys.exit(0)
+# The x2 rule is calibrated for whole-line reads.  The persistent C=64 conv reads 64-byte half-lines; its own
+# factor comes from tools/pmc_calib_summary.py (profiles/pmc_calib.json): a lower bound measured on its
+# read-only build, the x2 rule the upper bound.
+CALIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', 'pmc_calib.json')
+calib = json.load(open(CALIB)) if os.path.exists(CALIB) else None
 out = None
 for kname in res['FETCH_SIZE'][0]:
     f = res['FETCH_SIZE'][0][kname]
     w = res['WRITE_SIZE'][0].get(kname, float('nan'))
-    hbm = (2 * f + w) * 1024
+    ff = calib['fetch_factor'] if (calib and calib['kernel'] in kname) else 2.0
+    hbm = (ff * f + w) * 1024
     print(f'{kname[:90]}\n    {res["FETCH_SIZE"][1][kname]} launches: FETCH {f:.1f} KiB, WRITE {w:.1f} KiB -> '
-          f'HBM bytes per launch (2*FETCH + WRITE) = {hbm:.4g} (read {2 * f * 1024:.4g}, write {w * 1024:.4g})')
+          f'HBM bytes per launch ({ff:g}*FETCH + WRITE) = {hbm:.4g} (read {ff * f * 1024:.4g}, write {w * 1024:.4g})'
+          + (f'; at the x2 rule {(2 * f + w) * 1024:.4g}' if ff != 2.0 else ''))
     if ROOFLINE in kname:
-        out = dict(kernel=kname, hbm_bytes_per_launch=round(hbm), fetch_size_kib=f, write_size_kib=w)
+        out = dict(kernel=kname, hbm_bytes_per_launch=round(hbm), hbm_bytes_per_launch_x2_rule=round((2 * f + w) * 1024),
+                   fetch_size_kib=f, write_size_kib=w, fetch_factor=ff)
 if out is not None and len(sys.argv) > 2:
     with open(sys.argv[2], 'w') as fh:
         json.dump(dict(config='sg2_conv3x3 fused 256^2 C=64 N=32 float16', **out,
-                       correction='hbm = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts half of '
-                                  'wide coalesced reads; MI355X_MICROARCH.md HBM section)'), fh, indent=1)
+                       correction='hbm = (fetch_factor * FETCH_SIZE + WRITE_SIZE) * 1024; fetch_factor from the '
+                                  'kernel\'s own read-only calibration (profiles/pmc_calib.json, lower bound) -- '
+                                  'the guide\'s x2 (MI355X_MICROARCH.md HBM section) holds for whole-line reads only'),
+                  fh, indent=1)
