@@ -583,10 +583,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
                             dd[0] = d0.x; dd[1] = d0.y; dd[2] = d0.z; dd[3] = d0.w; dd[4] = d1.x; dd[5] = d1.y; dd[6] = d1.z; dd[7] = d1.w;
                         }
                         vec8 yv, rv;
+                        // (the raw output is only rounded where something consumes it; a packed-f32 form of
+                        // this loop measured the same: profiles/r02_v7_c64p_variants.log)
 #pragma unroll
                         for (int e = 0; e < 8; ++e) {
                             const float cv = acc[i][2 * jj + (e >> 2)][e & 3];
-                            rv[e] = (T)cv;
+                            if (DOT) rv[e] = (T)cv;
                             float v = cv;
                             if (EPI) {
                                 v = fmaf(v, dd[e], nv + bb[e]);
@@ -599,8 +601,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
                         if (!(SG2_DIAG & 2)) {
                             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, (int)(dst * sizeof(T)), 0, 0);
                             // a uniform (scalar) branch: a dropped store still costs its issue slot
-                            if (has_raw) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, (int)(dst * sizeof(T)), 0, 0);
-                        } else if (yv[0] == (T)12345.f && rv[1] == (T)-7.f) {
+                            if (has_raw) {
+                                if (!DOT) {
+#pragma unroll
+                                    for (int e = 0; e < 8; ++e) rv[e] = (T)acc[i][2 * jj + (e >> 2)][e & 3];
+                                }
+                                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, (int)(dst * sizeof(T)), 0, 0);
+                            }
+                        } else if (yv[0] == (T)12345.f && yv[1] == (T)-7.f) {
                             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, (int)(dst * sizeof(T)), 0, 0);
                         }
                     }

@@ -12,6 +12,7 @@ import torch
 from torch_utils import training_stats
 from torch_utils.ops import conv2d_gradfix
 from torch_utils.ops import upfirdn2d
+from training.networks_stylegan2 import MinibatchStdLayer
 
 
 class Loss:
@@ -90,10 +91,63 @@ class StyleGAN2Loss(Loss):
             self._generator_term(gen_z, gen_c, gain, sigma)
         if 'Gpl' in terms:
             self._path_length_term(gen_z, gen_c, gain)
+        if terms == {'Dfake', 'Dreal'} and self._d_batchable():
+            self._discriminator_main_batched(real_img, real_c, gen_z, gen_c, gain, sigma)
+            return
         fake_loss = self._discriminator_fake_term(gen_z, gen_c, gain, sigma) if 'Dfake' in terms else 0
         if 'Dreal' in terms or 'Dr1' in terms:
             self._discriminator_real_term(real_img, real_c, gain, sigma, fake_loss,
                                           main='Dreal' in terms, r1='Dr1' in terms)
+
+    # Dmain's two D passes (generated, real) run as ONE forward + backward over the concatenated batch: D is
+    # per-sample except the minibatch-std layer, which takes its statistics within each half
+    # (MinibatchStdLayer.segments).  Same terms, same RNG draws in the same order (G, augment(fake),
+    # augment(real); D draws nothing), gradients equal up to f32 summation order; half the launches.
+    batch_d_main = True
+
+    def _d_batchable(self):
+        """Batch Dmain only when every minibatch-std layer of D can take per-segment statistics."""
+        mb = [m for m in self.D.modules() if type(m).__name__ == 'MinibatchStdLayer']
+        return self.batch_d_main and all(isinstance(m, MinibatchStdLayer) for m in mb)
+
+    def backward_passes(self, phase):
+        """How many backward passes of `phase` accumulate into each parameter (GradExchange hooks)."""
+        if phase == 'Dboth' or (phase == 'Dmain' and not self._d_batchable()):
+            return 2
+        return 1
+
+    def _d_input(self, img, sigma, allow_aug_debug_print=False):
+        """run_D without D: blur and augment (loss.py:54-60)."""
+        blur_size = np.floor(sigma * 3)
+        if blur_size > 0:
+            with torch.autograd.profiler.record_function('blur'):
+                f = torch.arange(-blur_size, blur_size + 1, device=img.device).div(sigma).square().neg().exp2()
+                img = upfirdn2d.filter2d(img, f / f.sum())
+        if self.augment_pipe is not None:
+            img = self.augment_pipe(img, allow_aug_debug_print)
+        return img
+
+    def _discriminator_main_batched(self, real, real_c, z, c, gain, sigma):
+        with torch.autograd.profiler.record_function('D_main'):
+            img, _ = self.run_G(z, c, update_emas=True)
+            x_fake = self._d_input(img, sigma)
+            x_real = self._d_input(real.detach(), sigma, allow_aug_debug_print=self.allow_aug_debug_print)
+            n = x_fake.shape[0]
+            mbstd = [m for m in self.D.modules() if isinstance(m, MinibatchStdLayer)]
+            for m in mbstd:
+                m.segments = (n, x_real.shape[0])
+            try:
+                logits = self.D(torch.cat([x_fake, x_real]), torch.cat([c, real_c]), update_emas=True)
+            finally:
+                for m in mbstd:
+                    m.segments = None
+            lf, lr = logits[:n], logits[n:]
+            self._report_logits('fake', lf)
+            self._report_logits('real', lr)
+            fake_term = torch.nn.functional.softplus(lf)
+            real_term = torch.nn.functional.softplus(-lr)
+            training_stats.report('Loss/D/loss', fake_term + real_term)
+            (fake_term.mean() + real_term.mean()).mul(gain).backward()
 
     def _report_logits(self, kind, logits):
         training_stats.report(f'Loss/scores/{kind}', logits)

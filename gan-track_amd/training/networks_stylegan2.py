@@ -629,8 +629,16 @@ class MinibatchStdLayer(torch.nn.Module):
     def __init__(self, group_size, num_channels=1):
         super().__init__()
         self.group_size, self.num_channels = group_size, num_channels
+        self.segments = None    # sizes of independent sub-batches (batched D passes, see loss.py), or None
 
     def forward(self, x):
+        seg = getattr(self, 'segments', None)
+        if seg is not None and len(seg) > 1:
+            # the statistics are taken within each sub-batch, as separate D passes would
+            return torch.cat([self._forward(part) for part in x.split(list(seg))])
+        return self._forward(x)
+
+    def _forward(self, x):
         N, C, H, W = x.shape
         G = min(self.group_size, N) if self.group_size is not None else N
         F = self.num_channels

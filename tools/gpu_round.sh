@@ -80,6 +80,11 @@ if step calib; then
     done
     unset SG2HIP_LIB
 fi
+if step var; then
+    echo "== c64p variants: $VARS"
+    (cd "$R" && bash tools/c64p_var.sh run > "$O/var.log" 2>&1)
+    rc=$?; cat "$O/var.log"; [ $rc -eq 0 ] || exit $rc
+fi
 if step wgswz; then
     echo "== wgrad LDS swizzle A/B"
     (cd "$R" && for sw in 0 1 0 1; do echo "SWZ=$sw"; SG2_WGRAD_SWZ=$sw timeout -k 10 120 python3 -u tools/wgrad_s2_ab.py || exit 1; done > "$O/wgswz.log" 2>&1)
