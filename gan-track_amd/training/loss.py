@@ -91,7 +91,7 @@ class StyleGAN2Loss(Loss):
             self._generator_term(gen_z, gen_c, gain, sigma)
         if 'Gpl' in terms:
             self._path_length_term(gen_z, gen_c, gain)
-        if terms == {'Dfake', 'Dreal'} and self._d_batchable():
+        if terms == {'Dfake', 'Dreal'} and self._d_batchable(gen_z.shape[0] + real_img.shape[0]):
             self._discriminator_main_batched(real_img, real_c, gen_z, gen_c, gain, sigma)
             return
         fake_loss = self._discriminator_fake_term(gen_z, gen_c, gain, sigma) if 'Dfake' in terms else 0
@@ -105,14 +105,23 @@ class StyleGAN2Loss(Loss):
     # augment(real); D draws nothing), gradients equal up to f32 summation order; half the launches.
     batch_d_main = True
 
-    def _d_batchable(self):
-        """Batch Dmain only when every minibatch-std layer of D can take per-segment statistics."""
+    def _d_batchable(self, n):
+        """Batch Dmain only when every minibatch-std layer of D can take per-segment statistics and the
+        largest D activation of the combined batch `n` stays within the kernels' 32-bit byte offsets."""
         mb = [m for m in self.D.modules() if type(m).__name__ == 'MinibatchStdLayer']
-        return self.batch_d_main and all(isinstance(m, MinibatchStdLayer) for m in mb)
+        if not (self.batch_d_main and all(isinstance(m, MinibatchStdLayer) for m in mb)):
+            return False
+        per_sample = 0
+        for m in self.D.modules():
+            if all(hasattr(m, k) for k in ('resolution', 'in_channels', 'use_fp16', 'conv0')):
+                ch = max(m.in_channels, m.conv0.in_channels, m.conv0.out_channels)
+                per_sample = max(per_sample, ch * (m.resolution + 3) ** 2 * 4)   # the ABI's size check: 4 B/elt
+        return n * per_sample < (1 << 31) - (1 << 26)
 
-    def backward_passes(self, phase):
-        """How many backward passes of `phase` accumulate into each parameter (GradExchange hooks)."""
-        if phase == 'Dboth' or (phase == 'Dmain' and not self._d_batchable()):
+    def backward_passes(self, phase, n=None):
+        """How many backward passes of `phase` accumulate into each parameter (GradExchange hooks); `n` is
+        the combined Dmain batch (generated + real)."""
+        if phase == 'Dboth' or (phase == 'Dmain' and not (n is not None and self._d_batchable(n))):
             return 2
         return 1
 

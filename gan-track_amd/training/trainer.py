@@ -227,8 +227,8 @@ class Trainer:
         with conv2d_gradfix.pack_cache():   # the phase's weights are fixed until its optimizer step
             for ci, (real_img, real_c, gen_z, gen_c) in enumerate(chunks):
                 if ci == len(chunks) - 1:
-                    passes = self.loss.backward_passes(phase.name) if hasattr(self.loss, 'backward_passes') \
-                        else self._passes(phase.name)
+                    passes = self.loss.backward_passes(phase.name, gen_z.shape[0] + real_img.shape[0]) \
+                        if hasattr(self.loss, 'backward_passes') else self._passes(phase.name)
                     phase.exchange.arm(phase.name, passes)
                 self.loss.accumulate_gradients(phase=phase.name, real_img=real_img, real_c=real_c, gen_z=gen_z,
                                                gen_c=gen_c, gain=phase.interval, cur_nimg=self.cur_nimg)
