@@ -51,30 +51,49 @@ class FlatAdam:
         phase) from `flat`, where parameter i's gradient is flat[offsets[i] : offsets[i] + numel]."""
         if not part:
             return
-        g = self.param_groups[0]
-        lr, (b1, b2), eps = g['lr'], g['betas'], g['eps']
-        dev = flat.device
-        if self.exp_avg is None:
-            self.exp_avg = torch.zeros_like(flat)
-            self.exp_avg_sq = torch.zeros_like(flat)
+        self.prepare(flat, offsets, part)
+        self.launch(flat, part, grad_scale, write_grad)
+
+    def _table(self, flat, offsets, part):
+        """Per participation set: segment table, chunk table and the device buffer of the step scalars."""
         key = tuple(part)
         tab = self._tables.get(key)
         if tab is None:
+            dev = flat.device
             seg = torch.tensor([[self.params[i].data_ptr(), offsets[i], self.params[i].numel()] for i in part],
                                dtype=torch.int64).to(dev)
             blocks, nb = _block_table([self.params[i].numel() for i in part], dev)
-            tab = self._tables[key] = (seg, blocks, nb)
-        seg, blocks, nb = tab
+            coef = torch.zeros([2 * len(part)], dtype=torch.float32, device=dev)
+            tab = self._tables[key] = (seg, blocks, nb, coef)
+        return tab
+
+    def prepare(self, flat, offsets, part):
+        """Advance the step counts of `part` and write torch.optim.Adam's step scalars into the set's device
+        buffer (an asynchronous copy on the current stream, ordered before the launch that reads it -- which
+        may be a replayed HIP graph)."""
+        g = self.param_groups[0]
+        lr, (b1, b2) = g['lr'], g['betas']
+        if self.exp_avg is None:
+            self.exp_avg = torch.zeros_like(flat)
+            self.exp_avg_sq = torch.zeros_like(flat)
+        coef_dev = self._table(flat, offsets, part)[3]
         coef = []
         for i in part:           # torch.optim.Adam's scalars, computed in double as torch does
             self.steps[i] += 1
             s = self.steps[i]
             coef += [lr / (1 - b1 ** s), math.sqrt(1 - b2 ** s)]
-        coef = torch.tensor(coef, dtype=torch.float32).pin_memory().to(dev, non_blocking=True)
+        coef_dev.copy_(torch.tensor(coef, dtype=torch.float32).pin_memory(), non_blocking=True)
+
+    def launch(self, flat, part, grad_scale=1.0, write_grad=True):
+        """The sg2_adam_multi launch of a prepared set (capturable: every operand is a persistent buffer)."""
+        g = self.param_groups[0]
+        (b1, b2), eps = g['betas'], g['eps']
+        seg, blocks, nb, coef = self._tables[tuple(part)]
         L = sg2hip.lib()
         sg2hip.check(L.sg2_adam_multi(sg2hip.ptr(seg), sg2hip.ptr(coef), sg2hip.ptr(blocks), nb, sg2hip.ptr(flat),
                                       sg2hip.ptr(self.exp_avg), sg2hip.ptr(self.exp_avg_sq), b1, b2, eps,
-                                      float(grad_scale), int(write_grad), sg2hip.stream_ptr(dev)), 'sg2_adam_multi')
+                                      float(grad_scale), int(write_grad), sg2hip.stream_ptr(flat.device)),
+                     'sg2_adam_multi')
 
 
 class EmaLerp:

@@ -217,6 +217,9 @@ class Trainer:
         # state (kernel attributes, statistics rows, cached constants, participation sets) exists.
         self.graphs = graphs
         self._graphs = {}
+        self._static_real = None       # graph-mode static copy of the real batch, shared by the phase graphs
+        self._real_staged = None       # the step (self._serial) whose real batch is in it
+        self._serial = 0               # step() calls so far (batch_idx may be reset by the caller)
 
     @staticmethod
     def _passes(name):
@@ -235,15 +238,30 @@ class Trainer:
 
     def _graph_phase(self, phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c):
         """Replay the phase's graph (capturing it the first time): forward + backward of every micro-batch,
-        the bucket fills and (several ranks) the overlapped all_reduces.  Returns the participating
-        parameter indices of the captured exchange."""
+        the bucket fills, (several ranks) the overlapped all_reduces and, with FlatAdam, the optimiser
+        launch.  Returns (participating parameter indices, whether the optimiser step was in the graph)."""
         st = self._graphs.get(phase.name)
         ex = phase.exchange
+        fused_opt = isinstance(phase.opt, FlatAdam)
         if st is None:
             st = dnnlib.EasyDict()
-            st.inputs = [[t.clone() for t in lst] for lst in (phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)]
+            # the real batch is the same for every phase of a step: one static copy shared by the phase graphs
+            if self._static_real is None:
+                self._static_real = [[t.clone() for t in lst] for lst in (phase_real_img, phase_real_c)]
+                self._real_staged = self._serial
+            st.inputs = self._static_real + [[t.clone() for t in lst] for lst in (phase_gen_z, phase_gen_c)]
+            self._stage(st, phase, (phase_real_img, phase_real_c), (phase_gen_z, phase_gen_c))
             phase.opt.zero_grad(set_to_none=True)
-            ex._flat(self.device)
+            flat = ex._flat(self.device)
+            # the optimiser launch joins the graph when the participation set learned by the eager warm-up
+            # step is known: its tables and step-scalar buffer are built here, outside the capture
+            part0 = ex.expect.get(phase.name)
+            st.opt_in_graph = fused_opt and part0 is not None
+            if st.opt_in_graph:
+                phase.opt._table(flat, ex.offsets, part0)
+                if phase.opt.exp_avg is None:
+                    phase.opt.exp_avg = torch.zeros_like(flat)
+                    phase.opt.exp_avg_sq = torch.zeros_like(flat)
             torch.cuda.synchronize(self.device)
             st.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(st.graph):
@@ -252,26 +270,75 @@ class Trainer:
                 st.part = [i for i, p in enumerate(ex.params) if p.grad is not None]
                 st.overlapped = ex.close_capture()
                 phase.module.requires_grad_(False)
+                st.opt_in_graph = st.opt_in_graph and st.part == part0
+                if st.opt_in_graph:
+                    phase.opt.launch(flat, st.part, grad_scale=1.0 / self.num_gpus,
+                                     write_grad=self.on_grads is not None)
             self._graphs[phase.name] = st
+            st.views = False
         else:
-            for dst, src in zip(st.inputs, (phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)):
-                for d, s_ in zip(dst, src):
-                    d.copy_(s_)
+            self._stage(st, phase, (phase_real_img, phase_real_c), (phase_gen_z, phase_gen_c))
+        if st.opt_in_graph:
+            phase.opt.prepare(ex.flat, ex.offsets, st.part)      # the step scalars, ordered before the replay
         st.graph.replay()
         ex._filled = [True] * len(ex.buckets)     # filled and reduced inside the graph
-        return st.part
+        if st.opt_in_graph and st.views:
+            ex._reset()
+        else:
+            # point each .grad at its range of the flat buffer (once: a replay does not touch the attributes)
+            ex.finish(phase.name, st.part)
+            st.views = True
+        return st.part, st.opt_in_graph
+
+    def _stage(self, st, phase, real, gen):
+        """Copy a phase's inputs into its graph's static buffers (the shared real batch only once a step)."""
+        if self._real_staged != self._serial:
+            for dst, src in zip(self._static_real, real):
+                for d, s_ in zip(dst, src):
+                    d.copy_(s_)
+            self._real_staged = self._serial
+        for dst, src in zip(st.inputs[2:], gen):
+            for d, s_ in zip(dst, src):
+                d.copy_(s_)
+
+    def _replay_step(self, active, phase_real_img, phase_real_c):
+        """Graph mode with every active phase captured, its Adam launch inside its graph and its .grad views
+        in place: stage all inputs and step scalars first, then replay the phase graphs back to back.  ROCm's
+        graph launch returns when the graph's last kernels are queued, so host work between two replays is
+        GPU idle time; here there is none (the step scalars of a phase live in a buffer of their own per
+        participation set, and each set is used once per step)."""
+        for phase, gz, gc in active:
+            st = self._graphs[phase.name]
+            self._stage(st, phase, (phase_real_img, phase_real_c), (gz, gc))
+            phase.opt.prepare(phase.exchange.flat, phase.exchange.offsets, st.part)
+        for phase, _, _ in active:
+            st = self._graphs[phase.name]
+            if phase.start_event is not None:
+                phase.start_event.record(torch.cuda.current_stream(self.device))
+            st.graph.replay()
+            if phase.end_event is not None:
+                phase.end_event.record(torch.cuda.current_stream(self.device))
+        for phase, _, _ in active:
+            phase.exchange._reset()
 
     def step(self, phase_real_img, phase_real_c, all_gen_z, all_gen_c):
         """One iteration.  phase_real_img/c: lists of batch_gpu chunks; all_gen_z/c: per phase, lists
         of chunks (the reference's data layout, :317-323)."""
-        for phase, phase_gen_z, phase_gen_c in zip(self.phases, all_gen_z, all_gen_c):
-            if self.batch_idx % phase.interval != 0:
-                continue
+        self._serial += 1
+        active = [(ph, gz, gc) for ph, gz, gc in zip(self.phases, all_gen_z, all_gen_c)
+                  if self.batch_idx % ph.interval == 0]
+        ready = self.graphs and self.on_grads is None and all(
+            ph.name in self._graphs and self._graphs[ph.name].opt_in_graph and self._graphs[ph.name].views
+            for ph, _, _ in active)
+        if ready:
+            self._replay_step(active, phase_real_img, phase_real_c)
+            active = []
+        for phase, phase_gen_z, phase_gen_c in active:
             if phase.start_event is not None:
                 phase.start_event.record(torch.cuda.current_stream(self.device))
-            part = None
+            part, stepped = None, False
             if self.graphs:
-                part = self._graph_phase(phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)
+                part, stepped = self._graph_phase(phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)
             else:
                 phase.opt.zero_grad(set_to_none=True)
                 phase.module.requires_grad_(True)
@@ -279,7 +346,15 @@ class Trainer:
                 phase.module.requires_grad_(False)
             with torch.autograd.profiler.record_function(phase.name + '_opt'):
                 ex = phase.exchange
-                part = ex.finish(phase.name, part)
+                if stepped:
+                    # exchange and Adam ran inside the replayed graph (the /N, nan_to_num and write-back of
+                    # the scaled gradient included), so there is nothing left to launch for this phase
+                    if self.on_grads is not None:
+                        self.on_grads(phase.name, phase.module)
+                    if phase.end_event is not None:
+                        phase.end_event.record(torch.cuda.current_stream(self.device))
+                    continue
+                part = ex.finish(phase.name, part) if not self.graphs else part
                 if isinstance(phase.opt, FlatAdam):
                     phase.opt.step_flat(ex.flat, ex.offsets, part, grad_scale=1.0 / self.num_gpus,
                                         write_grad=self.on_grads is not None)

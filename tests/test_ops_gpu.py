@@ -112,6 +112,28 @@ def test_upfirdn2d_vec_path(dtype):
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
+def test_upfirdn2d_up2_blocks(dtype):
+    """2x up-FIR on channels-last feature maps (upfirdn_nhwc_vec; the adjoint of the D skip's FIR-down-2):
+    even / odd / asymmetric / zero padding, odd output sizes, flipped and asymmetric filters, vs the
+    oracle.  (A 2 x 2-output-block kernel for this case passed this test but measured 1.8x slower than the
+    per-output kernel: profiles/r02_v9_fir_up2_ab.log.)"""
+    from torch_utils.ops import upfirdn2d
+    torch.manual_seed(5)
+    tol = {torch.float32: 1e-5, torch.float16: 2e-3, torch.bfloat16: 1e-2}[dtype]
+    for fk in ([1, 3, 3, 1], [1, 2, 5, 3]):
+        f = upfirdn2d.setup_filter(fk)
+        for (n, c, h, w) in [(2, 64, 17, 17), (1, 32, 16, 9), (3, 128, 8, 8)]:
+            x = torch.randn(n, c, h, w).to(dtype).float()
+            xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+            for pad in ([2, 1, 2, 1], [1, 2, 1, 2], [2, 2, 2, 2], [1, 1, 1, 1], [0, 0, 0, 0], [3, 0, 1, 2]):
+                for flip in (False, True):
+                    y = upfirdn2d.upfirdn2d(xd, f.to(DEV), up=2, padding=pad, flip_filter=flip, gain=4)
+                    r = O.upfirdn2d(x, f, up=2, padding=pad, flip_filter=flip, gain=4)
+                    assert y.shape == r.shape
+                    assert rel_err(y.float(), r) < tol, (fk, n, c, h, w, pad, flip)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
 def test_fir_strip_ragged(dtype):
     """Column-strip FIR kernel (upfirdn_nhwc_f4s): image sizes that are not tile multiples (the last
     tile row/column is shifted back inside the image), partial channel groups (C = 72), plain and
