@@ -361,7 +361,8 @@ int launch3(const Conv3Args& a, hipStream_t s) {
 //     activation dtype -- the reference's `x * styles.to(x.dtype)` (networks_stylegan2.py:69) bit for bit.
 #ifndef SG2_DIAG
 #define SG2_DIAG 0          // timing-only builds (tools/c64p_diag.sh): 1 no MFMA, 2 no output stores, 4 no halo loads,
-                            // 8 both chunks load the first 64 B of each pixel line
+                            // 8 both chunks load the first 64 B of each pixel line, 16 epilogue tables as constants,
+                            // 32 no modulation multiply at the LDS store, 64 no style-scale loads
 #endif
 constexpr int P_TW = 32, P_TH = 16, P_C = 64;
 constexpr int P_HW = P_TW + 2, P_HH = P_TH + 2, P_HP = P_HW * P_HH;      // 34 x 18 halo positions
@@ -444,9 +445,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
             if (!(SG2_DIAG & 4)) rh[i] = buf_load16<vec8>(rxb, ok ? (((n * a.H + iy) * a.W + ix) * P_C + ((SG2_DIAG & 8) ? 0 : c) * CK + hq) * (int)sizeof(T) : -1);
             else rh[i] = vec8{};
         }
-        if (SCALE_IN) {
+        if (SCALE_IN && !(SG2_DIAG & 64)) {
             s0 = buf_load16<float4>(rsc, (n * P_C + c * CK + hq) * 4);
             s1 = buf_load16<float4>(rsc, (n * P_C + c * CK + hq + 4) * 4);
+        } else if (SCALE_IN) {
+            s0 = float4{1.f, 1.f, 1.f, 1.f};
+            s1 = s0;
         }
     };
     auto sstore = [&](int buf) {
@@ -455,7 +459,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
 #pragma unroll
         for (int i = 0; i < NH; ++i) {
             vec8 v = rh[i];
-            if (SCALE_IN) {
+            if (SCALE_IN && !(SG2_DIAG & 32)) {
                 if constexpr (std::is_same<T, f16_t>::value) {
                     v = v * sv8;                         // v_pk_mul_f16: round(x * round(s)), as the reference
                 } else {
@@ -570,13 +574,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int64_t pix = ((int64_t)n * a.H + ty0 + 2 * wave + (i >> 1)) * a.W + tx0 + (i & 1) * 16 + l16;
-                    const float nv = EPI ? nlds[(2 * wave + (i >> 1)) * P_TW + (i & 1) * 16 + l16] : 0.f;
+                    const float nv = (EPI && !(SG2_DIAG & 16)) ? nlds[(2 * wave + (i >> 1)) * P_TW + (i & 1) * 16 + l16] : 0.f;
 #pragma unroll
                     for (int jj = 0; jj < 2; ++jj) {
                         const int ch = jj * 32 + oq8;            // channels ch .. ch + 7: acc[i][2jj][.], acc[i][2jj+1][.]
                         const int64_t dst = pix * P_C + ch;
                         float bb[8], dd[8];
-                        if (EPI) {
+                        if (EPI && (SG2_DIAG & 16)) {
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) { bb[e] = 0.1f * (e + 1); dd[e] = 1.f - 0.01f * e; }
+                        } else if (EPI) {
                             const float4 b0 = *(const float4*)(blds + ch), b1 = *(const float4*)(blds + ch + 4);
                             const float4 d0 = *(const float4*)(dlds + ch), d1 = *(const float4*)(dlds + ch + 4);
                             bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
