@@ -241,10 +241,17 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     num_gpus = world
+    # Rehearsal of the multi-rank path on a 1-GPU box (never the measured configuration):
+    # SG2_BENCH_BACKEND=gloo SG2_BENCH_SHARE_DEVICE=1 puts every rank on cuda:0 and exchanges over gloo.
+    backend = os.environ.get('SG2_BENCH_BACKEND', 'nccl')
+    dev_index = 0 if os.environ.get('SG2_BENCH_SHARE_DEVICE') == '1' else local_rank
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
-    device = torch.device('cuda', local_rank)
+        torch.cuda.set_device(dev_index)
+        if backend == 'nccl':
+            torch.distributed.init_process_group('nccl', device_id=torch.device('cuda', dev_index))
+        else:
+            torch.distributed.init_process_group(backend)
+    device = torch.device('cuda', dev_index)
     torch.backends.cudnn.benchmark = True
 
     tr = build(args, device, rank, num_gpus)

@@ -763,9 +763,10 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
 
 // Split-K finalize: f32 partial sums -> T with the fused epilogue.
 template <typename T>
-__global__ void conv_finalize_kernel(T* y, const float* src, Epi e, int64_t n_el, int Cout, int64_t pix_per_n) {
+__global__ void conv_finalize_kernel(T* y, float* src, Epi e, int64_t n_el, int Cout, int64_t pix_per_n, int clean) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_el; i += (int64_t)gridDim.x * blockDim.x) {
         const float c = src[i];
+        if (clean) src[i] = 0.f;                 // leave the workspace zeroed for the next split-K call
         float v = c;
         if (e.dot_out) {
             const int64_t pix = i / Cout;
@@ -1361,7 +1362,8 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
         if (blocks < 512 && workspace != nullptr && workspace_elems >= total_out)
             splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(target, blocks), maxnk / 4));
         const bool split = splits > 1;
-        if (split) {
+        const bool clean = workspace_clean();
+        if (split && !clean) {
             hipError_t e = hipMemsetAsync(workspace, 0, total_out * sizeof(float), s);
             if (e != hipSuccess) { set_error("sg2_conv2d: memset failed"); return (int)e; }
         }
@@ -1387,7 +1389,8 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
         }
         if (rc == 0 && split) {
             const int g = (int)std::min<int64_t>(cdiv(total_out, 256), 4096);
-            conv_finalize_kernel<T><<<g, 256, 0, s>>>((T*)y, workspace, base.e, total_out, Cout, (int64_t)OH * OW);
+            conv_finalize_kernel<T><<<g, 256, 0, s>>>((T*)y, workspace, base.e, total_out, Cout, (int64_t)OH * OW,
+                                                      (int)clean);
             rc = launch_status("sg2_conv2d finalize");
         }
     });

@@ -31,6 +31,9 @@ void set_error(const std::string& msg);
 // sg2_set_zeroed_accumulators(1) in effect the caller has zeroed them itself (one fill for all of a layer's
 // accumulators instead of a memset per call), and this is a no-op.
 bool accumulators_prezeroed();
+// sg2_set_clean_workspace(1): the split-K workspace passed to the conv entry points is zero on entry, and the
+// call leaves it zero (its finalize clears what it read) -- no memset per split-K call.
+bool workspace_clean();
 inline hipError_t zero_acc(void* p, size_t bytes, hipStream_t s) {
     return accumulators_prezeroed() ? hipSuccess : hipMemsetAsync(p, 0, bytes, s);
 }

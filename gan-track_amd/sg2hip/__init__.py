@@ -44,6 +44,7 @@ SIGNATURES = {
     'sg2_conv3x3': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _f, _f, _f, _vp, _vp,
                     _vp],
     'sg2_set_zeroed_accumulators': [_i],
+    'sg2_set_clean_workspace': [_i],
     'sg2_conv3x3_s2': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _f, _f, _f, _vp, _i,
                        _vp, _vp, _vp],
     'sg2_conv3x3_up2': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp],
@@ -87,10 +88,25 @@ def lib():
         L.sg2_last_error.argtypes = []
         L.sg2_last_error.restype = ctypes.c_char_p
         L.sg2_set_zeroed_accumulators.restype = None
+        L.sg2_set_clean_workspace.restype = None
         if L.sg2_abi_version() != ABI_VERSION:
             raise RuntimeError(f'sg2hip: ABI version mismatch ({L.sg2_abi_version()} != {ABI_VERSION})')
         _lib = L
     return _lib
+
+
+@contextlib.contextmanager
+def clean_workspace(on=True):
+    """Calls inside take their split-K workspace as zeroed and leave it zeroed (sg2_set_clean_workspace)."""
+    if not on:
+        yield
+        return
+    L = lib()
+    L.sg2_set_clean_workspace(1)
+    try:
+        yield
+    finally:
+        L.sg2_set_clean_workspace(0)
 
 
 @contextlib.contextmanager

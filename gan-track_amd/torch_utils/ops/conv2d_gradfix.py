@@ -53,6 +53,20 @@ def _nhwc(t):
 
 
 _WS_LIMIT = 1 << 23  # split-K f32 workspace only for small outputs (low-resolution layers)
+_CLEAN_WS = {}       # device -> persistent zeroed split-K workspace (every call leaves it zeroed)
+
+
+def _workspace(x, total):
+    """(workspace, clean): the device's persistent zeroed workspace when it can be used (created outside any
+    graph capture, so eager calls and replayed graphs share one buffer), else a fresh one per call."""
+    if total > _WS_LIMIT:
+        return None, False
+    ws = _CLEAN_WS.get(x.device)
+    if ws is None:
+        if torch.cuda.is_current_stream_capturing():
+            return torch.empty([total], dtype=torch.float32, device=x.device), False
+        ws = _CLEAN_WS[x.device] = torch.zeros([_WS_LIMIT], dtype=torch.float32, device=x.device)
+    return ws, True
 
 
 def _up2_ok(x, cout, oh, ow, kh, kw, stride, pad, transpose):
@@ -82,11 +96,12 @@ def _conv_raw(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose):
     n, cin, h, w = x.shape
     y = torch.empty([n, cout, oh, ow], dtype=x.dtype, device=x.device, memory_format=_CL)
     total = n * cout * oh * ow
-    ws = torch.empty([total], dtype=torch.float32, device=x.device) if total <= _WS_LIMIT else None
-    _hip.check(_hip.lib().sg2_conv2d(
-        _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
-        stride, pad[0], pad[1], int(transpose), _hip.ptr(ws), ws.numel() if ws is not None else 0,
-        _hip.stream_ptr(x.device)), 'sg2_conv2d')
+    ws, clean = _workspace(x, total)
+    with _hip.clean_workspace(clean):
+        _hip.check(_hip.lib().sg2_conv2d(
+            _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
+            stride, pad[0], pad[1], int(transpose), _hip.ptr(ws), ws.numel() if ws is not None else 0,
+            _hip.stream_ptr(x.device)), 'sg2_conv2d')
     return y
 
 
@@ -118,8 +133,8 @@ def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_sca
                             float(noise_gain), float(alpha), float(gain), float(clamp), int(act), int(aux_mode),
                             _hip.ptr(dot_src), _hip.ptr(dot))
     total = n * cout * oh * ow
-    ws = torch.empty([total], dtype=torch.float32, device=x.device) if total <= _WS_LIMIT else None
-    with _hip.zeroed_accumulators(dot_out is not None and dot is not None):
+    ws, clean = _workspace(x, total)
+    with _hip.zeroed_accumulators(dot_out is not None and dot is not None), _hip.clean_workspace(clean):
         _hip.check(_hip.lib().sg2_conv2d_fused(
             _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
             stride, pad[0], pad[1], int(transpose), _hip.ptr(in_scale), ctypes.byref(epi) if epi is not None else None,

@@ -151,6 +151,11 @@ int sg2_conv3x3(void* y, void* y_raw, const void* x, const void* w, int dtype, i
  * call).  Default off. */
 void sg2_set_zeroed_accumulators(int on);
 
+/* While on (per host thread), the split-K f32 workspace passed to sg2_conv2d / sg2_conv2d_fused is zero on
+ * entry and is left zero on return (the finalize pass clears what it read), so a split-K call issues no
+ * memset.  The caller keeps one persistent zeroed workspace per stream.  Default off. */
+void sg2_set_clean_workspace(int on);
+
 /* Stride-2 / pad-0 form of sg2_conv3x3 (conv2d_resample.py:139-142 with down = 2: the discriminator's
  * down-2 3x3 layers after their FIR pre-filter, and the input gradient of the up-2 synthesis layers):
  * x [N, H, W, Cin] -> y [N, (H-3)/2+1, (W-3)/2+1, Cout]; same epilogue and dot as sg2_conv3x3, plus

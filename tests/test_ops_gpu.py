@@ -1179,3 +1179,23 @@ def test_fork_fir_discriminator_block(dtype, monkeypatch):
         assert rel_err(a_.float(), b_.float()) < tol
     for a_, b_ in zip(r_f, r_p):
         assert rel_err(a_.float(), b_.float()) < 1e-3
+
+
+def test_split_k_clean_workspace():
+    """Split-K convs (f32 low-resolution layers) run on one persistent workspace that each call leaves zeroed
+    (sg2_set_clean_workspace: no memset per call): repeated calls give the same result as a fresh-workspace
+    call, and the workspace is all zeros afterwards."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(11)
+    x = torch.randn(32, 512, 8, 8, device=DEV).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(512, 512, 3, 3, device=DEV) / 48
+    wp = cg._pack_conv(w)
+    first = cg._conv_raw(x, wp, 512, 8, 8, 3, 3, 1, (1, 1), False)
+    assert x.device in cg._CLEAN_WS
+    for _ in range(3):
+        again = cg._conv_raw(x, wp, 512, 8, 8, 3, 3, 1, (1, 1), False)
+        assert torch.equal(again, first) or rel_err(again, first) < 1e-6   # split-K atomics: order may vary
+    torch.cuda.synchronize()
+    assert float(cg._CLEAN_WS[x.device].abs().max()) == 0.0
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), padding=1)
+    assert rel_err(first.double(), ref) < 1e-5
