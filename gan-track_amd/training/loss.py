@@ -108,15 +108,18 @@ class StyleGAN2Loss(Loss):
     def _d_batchable(self, n):
         """Batch Dmain only when every minibatch-std layer of D can take per-segment statistics and the
         largest D activation of the combined batch `n` stays within the kernels' 32-bit byte offsets."""
-        mb = [m for m in self.D.modules() if type(m).__name__ == 'MinibatchStdLayer']
-        if not (self.batch_d_main and all(isinstance(m, MinibatchStdLayer) for m in mb)):
+        if not self.batch_d_main:
             return False
-        per_sample = 0
-        for m in self.D.modules():
-            if all(hasattr(m, k) for k in ('resolution', 'in_channels', 'use_fp16', 'conv0')):
-                ch = max(m.in_channels, m.conv0.in_channels, m.conv0.out_channels)
-                per_sample = max(per_sample, ch * (m.resolution + 3) ** 2 * 4)   # the ABI's size check: 4 B/elt
-        return n * per_sample < (1 << 31) - (1 << 26)
+        cached = getattr(self, '_d_bytes', None)
+        if cached is None or cached[0] is not self.D:
+            mb = [m for m in self.D.modules() if type(m).__name__ == 'MinibatchStdLayer']
+            per_sample = 0 if all(isinstance(m, MinibatchStdLayer) for m in mb) else None
+            for m in self.D.modules():
+                if per_sample is not None and all(hasattr(m, k) for k in ('resolution', 'in_channels', 'use_fp16', 'conv0')):
+                    ch = max(m.in_channels, m.conv0.in_channels, m.conv0.out_channels)
+                    per_sample = max(per_sample, ch * (m.resolution + 3) ** 2 * 4)   # the ABI's size check: 4 B/elt
+            cached = self._d_bytes = (self.D, per_sample)
+        return cached[1] is not None and n * cached[1] < (1 << 31) - (1 << 26)
 
     def backward_passes(self, phase, n=None):
         """How many backward passes of `phase` accumulate into each parameter (GradExchange hooks); `n` is
