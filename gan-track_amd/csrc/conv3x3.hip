@@ -365,10 +365,6 @@ int launch3(const Conv3Args& a, hipStream_t s) {
                             // 32 no modulation multiply at the LDS store, 64 no style-scale loads,
                             // 128 no noise / demod loads, 256 no noise / demod LDS table stores
 #endif
-#ifndef SG2_C64P_SST
-#define SG2_C64P_SST 10     // the tap after which the next chunk is staged into LDS (10: after the epilogue)
-#endif
-constexpr int P_SST = SG2_C64P_SST;
 constexpr int P_TW = 32, P_TH = 16, P_C = 64;
 constexpr int P_HW = P_TW + 2, P_HH = P_TH + 2, P_HP = P_HW * P_HH;      // 34 x 18 halo positions
 constexpr int P_POS = CK * 2;                                             // bytes per position and chunk
@@ -563,18 +559,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
                             if (!(SG2_DIAG & 1)) acc[i][j] = mma<T>(wf[j], pf[i], acc[i][j]);
                             else acc[i][j][0] += (float)wf[j][0] * (float)pf[i][0];
                         }
-                    if (tap == P_SST - 1) {
-                        // stage the next chunk into the other halo buffer while this chunk's last taps run:
-                        // every wave passed the previous chunk's barrier, so nobody reads that buffer any
-                        // more, and its readers come after this chunk's barrier
-                        __builtin_amdgcn_sched_barrier(0);
-                        sstore(c ^ 1);
-                        if (c == 0 && EPI) {
-                            nlds[tid] = (float)e_noise * ngain;
-                            if (tid < P_C) dlds[tid] = a.out_scale ? e_d * dgain : dgain;
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
                 }
             }
             // keep the scheduler from hoisting the staging store's math (which waits for the in-flight halo
@@ -659,12 +643,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
                         }
                 }
             }
-            if (P_SST > 9) {
-                sstore(c ^ 1);
-                if (c == 0 && EPI && !(SG2_DIAG & 256)) {
-                    nlds[tid] = (float)e_noise * ngain;
-                    if (tid < P_C) dlds[tid] = a.out_scale ? e_d * dgain : dgain;
-                }
+            sstore(c ^ 1);
+            if (c == 0 && EPI && !(SG2_DIAG & 256)) {
+                nlds[tid] = (float)e_noise * ngain;
+                if (tid < P_C) dlds[tid] = a.out_scale ? e_d * dgain : dgain;
             }
             __syncthreads();
         }
