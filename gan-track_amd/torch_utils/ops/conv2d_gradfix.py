@@ -413,6 +413,28 @@ class _WGrad(torch.autograd.Function):
         return dg, dx, None, None, None
 
 
+def _depthwise_1d(x, w, groups, stride, py, px):
+    """A depthwise 1-D correlation (one input and one output channel per group, a 1 x K or K x 1 kernel,
+    stride 1, no padding): the ADA image filter (augment_mi.py _filter, groups = N * C, per-sample taps)."""
+    return (groups == x.shape[1] == w.shape[0] and w.shape[1] == 1 and (w.shape[2] == 1 or w.shape[3] == 1)
+            and stride == 1 and py == 0 and px == 0 and w.shape[2] * w.shape[3] <= 64)
+
+
+def _depthwise_1d_conv(x, w):
+    """y[:, g] = sum_t w[g, 0, t] * x[:, g, shifted by t] as K differentiable multiply-adds over the whole
+    tensor (K launches) instead of one conv launch per group (N * C launches)."""
+    kh, kw = w.shape[2], w.shape[3]
+    k = kh * kw
+    oh, ow = x.shape[2] - kh + 1, x.shape[3] - kw + 1
+    taps = w.reshape(1, -1, k, 1, 1).to(x.dtype)
+    y = None
+    for t in range(k):
+        xs = x[:, :, t:t + oh, :] if kh > 1 else x[:, :, :, t:t + ow]
+        term = xs * taps[:, :, t]
+        y = term if y is None else y + term
+    return y
+
+
 def conv2d(input, weight, bias=None, stride=1, padding=0, dilation=1, groups=1):
     """torch.nn.functional.conv2d semantics (correlation)."""
     _hip.require_device(input, weight)
@@ -420,7 +442,9 @@ def conv2d(input, weight, bias=None, stride=1, padding=0, dilation=1, groups=1):
     sy, sx = _pair(stride)
     assert sy == sx, 'anisotropic stride is not supported'
     py, px = _pair(padding)
-    if groups != 1:
+    if groups != 1 and _depthwise_1d(input, weight, groups, sy, py, px):
+        y = _depthwise_1d_conv(input, weight)
+    elif groups != 1:
         xs = input.chunk(groups, dim=1)
         ws = weight.chunk(groups, dim=0)
         y = torch.cat([conv2d(a, b_, None, stride, padding) for a, b_ in zip(xs, ws)], dim=1)

@@ -1199,3 +1199,26 @@ def test_split_k_clean_workspace():
     assert float(cg._CLEAN_WS[x.device].abs().max()) == 0.0
     ref = torch.nn.functional.conv2d(x.double(), w.double(), padding=1)
     assert rel_err(first.double(), ref) < 1e-5
+
+
+def test_depthwise_1d_grouped_conv():
+    """conv2d(groups = C) with one channel per group and a 1 x K / K x 1 kernel (the ADA image filter:
+    groups = N * C, per-sample taps) runs as K multiply-adds: forward, input / weight gradients and the
+    double backward (R1 through the augment pipe) vs torch's fp64 grouped conv."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(7)
+    for kshape in [(1, 12), (12, 1)]:
+        x = torch.randn(1, 10, 30, 27, device=DEV, requires_grad=True)
+        w = torch.randn(10, 1, *kshape, device=DEV, requires_grad=True)
+        assert cg._depthwise_1d(x, w, 10, 1, 0, 0)
+        y = cg.conv2d(x, w, groups=10)
+        xr, wr = x.detach().double().requires_grad_(True), w.detach().double().requires_grad_(True)
+        yr = torch.nn.functional.conv2d(xr, wr, groups=10)
+        assert rel_err(y.double(), yr) < 1e-6
+        dy = torch.randn_like(y)
+        gx, gw = torch.autograd.grad((y * dy).sum(), [x, w], create_graph=True)
+        gxr, gwr = torch.autograd.grad((yr * dy.double()).sum(), [xr, wr], create_graph=True)
+        assert rel_err(gx.double(), gxr) < 1e-6 and rel_err(gw.double(), gwr) < 1e-6
+        ggw, = torch.autograd.grad(gx.square().sum(), [w])
+        ggwr, = torch.autograd.grad(gxr.square().sum(), [wr])
+        assert rel_err(ggw.double(), ggwr) < 1e-5
