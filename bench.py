@@ -15,7 +15,9 @@ on the device each iteration, random one-hot labels; networks randomly initialis
 
 A "step" = one training iteration with the reference's phase schedule (Gmain + Dmain every step,
 Greg every 4th, Dreg every 16th, gradient all-reduce, Adam, EMA, ADA); the phase counter is reset
-at the start of the timed region so K steps contain exactly the reference's mix.
+at the start of the timed region, so K steps contain the schedule's phases as they fall from step 0:
+K = 16 is exactly one cycle (4 Greg, 1 Dreg); K = 20 has 5 Greg and 2 Dreg (10 % Dreg steps against the
+schedule's 6.25 %, so a 20-step value is slightly pessimistic).
 value = images processed by all ranks / max-over-ranks wall time of the K timed steps.
 
 Extra fields: `roofline` for the dominant kernel (the MFMA implicit-GEMM convolution of the 256^2
@@ -175,7 +177,9 @@ def roofline(device, res, cbase, dtype):
     key = f'sg2_conv3x3 fused {res}^2 C={C} N=32 {str(dtype).split(".")[-1]}'
     gbps = byts / (ms * 1e-3) / 1e9
     tflops = flops / (ms * 1e-3) / 1e12
-    kname = 'conv3x3_c64p_kernel (persistent, weights in LDS)' if C == 64 else 'conv3x3_halo_kernel'
+    ring = C == 64 and os.environ.get('SG2_C64_RING', '1') != '0'
+    kname = ('conv3x3_c64r_kernel (LDS-DMA halo ring, weights in registers)' if ring else
+             'conv3x3_c64p_kernel (persistent, weights in LDS)') if C == 64 else 'conv3x3_halo_kernel'
     out = {'kernel': f'{kname} ({key}: modulation + demod/noise/bias/lrelu/clamp epilogue)'}
     if ai < ridge:
         out.update({'bound': 'hbm', 'achieved': round(gbps, 1), 'peak': HBM_PEAK, 'unit': 'GB/s',
@@ -198,13 +202,23 @@ def roofline(device, res, cbase, dtype):
 def cpu_baseline(args):
     """CPU oracle (oracle/sg2_oracle.py, the reference's algorithm restated in PyTorch-CPU fp32) timed on
     the host cores: one Gmain, Greg, Dmain and Dreg phase at the bench resolution with batch 4
-    (bounded sample), combined with the reference's phase frequencies (1, 1/4, 1, 1/16)."""
-    from oracle import sg2_oracle as O
+    (bounded sample), combined with the reference's phase frequencies (1, 1/4, 1, 1/16).  Beside it, the
+    BASELINE configs[0] case (C1: the Claro yaml at 64^2 1-ch, batch 8, cbase 16384, map 8, c_dim 2), the
+    reference's own CPU configuration, timed the same way at its full batch."""
     # the host cores this process may use: its CPU affinity, or the share the GPU box grants it
     # (OMP_NUM_THREADS; os.cpu_count() there reports the whole machine)
     threads = int(os.environ.get('OMP_NUM_THREADS') or len(os.sched_getaffinity(0)))
     torch.set_num_threads(threads)
-    B = 4
+    out = _cpu_iteration(args.res, args.img_channels, args.c_dim, args.cbase, args.map_depth, 4, threads)
+    c1 = _cpu_iteration(64, 1, 2, 16384, 8, 8, threads)
+    c1['sample'] = 'BASELINE configs[0] (C1, claro_stylegan2-ada.yaml 64^2 1-ch bs8): ' + c1['sample']
+    out['c1'] = c1
+    return out
+
+
+def _cpu_iteration(res, img_channels, c_dim, cbase, map_depth, B, threads):
+    from oracle import sg2_oracle as O
+    args = argparse.Namespace(res=res, img_channels=img_channels, c_dim=c_dim, cbase=cbase, map_depth=map_depth)
     torch.manual_seed(0)
     G = O.Generator(z_dim=512, c_dim=args.c_dim, w_dim=512, img_resolution=args.res, img_channels=args.img_channels,
                     channel_base=args.cbase, channel_max=512, num_fp16_res=4, conv_clamp=256,
@@ -302,7 +316,7 @@ def main():
             'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
             'graphs': graphs,
             'scaling': 'weak', 'vs_baseline': None,
-            'dtype': f'{args.fp16_dtype}+fp32 (fp16 at the 4 highest resolutions, fp32 below; f32 accumulate)',
+            'dtype': f'{args.fp16_dtype}+fp32 ({args.fp16_dtype} at the 4 highest resolutions, fp32 below; f32 accumulate)',
             'data': 'synthetic (U(-1,1) reals resident in HBM, device-drawn z, random one-hot c; random-init weights)',
             'config': {'workload': f'StyleGAN2-ADA train iteration, {args.res}x{args.res} {args.img_channels}-ch, '
                                    f'c_dim {args.c_dim}, cbase {args.cbase}, map {args.map_depth}, '
@@ -314,6 +328,12 @@ def main():
             'roofline': roof,
             'cpu_baseline': cpu,
         }
+        # what torch.distributed actually initialised (a scaling run can be checked from the line alone), and
+        # the gradient buckets each phase exchanges
+        line['dist'] = {'backend': torch.distributed.get_backend() if world > 1 else None,
+                        'world_size': torch.distributed.get_world_size() if world > 1 else 1,
+                        'buckets': {ph.name: len(ph.exchange.buckets) for ph in tr.phases},
+                        'bucket_mb': 32, 'overlapped': num_gpus > 1}
         if phase_ms is not None:
             line['last_phase_ms'] = phase_ms
         print(json.dumps(line), flush=True)

@@ -680,6 +680,310 @@ int num_cus() {
     return n;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Ring form of the 64 -> 64 channel layer (round 3; the 256^2 layer of the Claro network, 512^2 at cbase 32768).
+// The persistent kernel above keeps the 74 KB of weights in LDS, which leaves room for only two 39 KB halo
+// chunks: one being read by the MFMAs, one in flight, and every byte of it staged through registers by the
+// computing waves (load -> wait -> modulate -> ds_write), so each CU had ~39 KB of HBM reads in flight and the
+// memory phases added to the MFMA phase instead of hiding under it.  Here:
+//   * the weights live in REGISTERS: wave w owns output channels 32 (w & 1) .. +31 (two A fragments per tap and
+//     chunk: 36 x 16 B = 144 VGPRs), so the whole LDS is a 3-slot ring of 32 x 8 pixel tiles (10 x 40 halo
+//     positions of whole 128-byte pixel lines, 51,200 B a slot) -- two tiles (~100 KB) in flight per CU;
+//   * the halo arrives by LDS-DMA (buffer_load ... lds, 16 B a lane, one 1 KiB wave-instruction = 8 whole pixel
+//     lines), issued two tiles ahead, with no register and no LDS-store pass; out-of-image pixels are buffer
+//     out-of-range loads, which land as zeros.  The DMA destination is lane-linear, so the bank swizzle sits in
+//     the SOURCE address: the 16-byte piece j of position p is stored at j ^ (((p >> 1) & 3) << 1) (conflict-free
+//     ds_read_b128 of 16 consecutive positions at any tap shift; the 40-position row pitch keeps p mod 8 a
+//     function of the lane and kx only, so each read is a per-lane base + an immediate offset);
+//   * the modulation x * s moves onto the weights: once per sample each wave multiplies its register-resident
+//     fragments by s rounded to T (round(W * round(s)) where the reference rounds x * round(s): a product
+//     rounded once either way);
+//   * the tile's noise and demodulation scales arrive by a 1 KiB LDS-DMA into a 4-deep epilogue ring;
+//   * one barrier per tile, counted vmcnt waits (never 0 in the loop), and the two waves of a SIMD staggered:
+//     waves 0-3 run a tile's epilogue after its MFMAs, waves 4-7 defer it to the start of the next tile, so one
+//     wave's epilogue VALU and stores sit beside its partner's MFMAs.
+// Wave w: rows 2 ((w >> 1) & 3), +1 of the tile (4 pixel fragments of 16) x its 32 channels: per tap and chunk 4
+// ds_read_b128 (pixels) feed 8 MFMAs (weights from registers).
+constexpr int R_TW = 32, R_TH = 8, R_PITCH = 40;
+constexpr int R_HPOS = (R_TH + 2) * R_PITCH;          // 400 halo positions (34 used per row)
+constexpr int R_SLOT = R_HPOS * 128;                  // 51,200 B
+constexpr int R_NSLOT = 3;
+constexpr int R_EPI = 1024, R_NEPI = 4;               // noise [256] T at 0, demod [64] f32 at 512
+constexpr int R_HALO_I = R_HPOS / 8;                  // 50 halo DMA wave-instructions per tile
+constexpr int R_DMA = 7;                              // DMA wave-instructions per wave and tile (56 >= 50 + 1)
+constexpr size_t R_LDS = (size_t)R_NSLOT * R_SLOT + R_NEPI * R_EPI + 64 * 4;   // + gain * bias [64]
+static_assert(R_LDS <= 160 * 1024, "ring LDS");
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {    // byte address in LDS of a __shared__ pointer
+    return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {           // s_waitcnt vmcnt(N) (gfx9 encoding), expcnt / lgkmcnt untouched
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <typename T, bool SI, bool EPI, bool RAW>
+__global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band) {
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    constexpr int S = RAW ? 8 : 4;                    // buffer stores per wave and tile
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    char* epil = smem_raw + R_NSLOT * R_SLOT;
+    float* blds = (float*)(epil + R_NEPI * R_EPI);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l16 = lane & 15, q = lane >> 4;
+    const int h = wave & 1, wr = (wave >> 1) & 3;     // channel half, tile row pair
+    const bool late = wave >= 4;                      // staggered half: epilogue deferred by one tile
+    const int tiles_x = a.W / R_TW, tiles_y = a.H / R_TH;
+    const int per_n = tiles_x * tiles_y, per_band = band * tiles_x;
+    const int t_begin = (int)((int64_t)blockIdx.x * tiles_total / gridDim.x);
+    const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles_total / gridDim.x);
+    if (t_begin >= t_end) return;
+    // tile t -> (n, ty, tx): samples, bands of `band` tile rows, column-major inside a band (vertical neighbours,
+    // which share two halo rows, are consecutive in a CU's run)
+    auto tile_of = [&](int t, int& n, int& ty, int& tx) {
+        n = t / per_n;
+        const int r = t - n * per_n, b = r / per_band, rb = r - b * per_band;
+        const int col = rb / band;
+        ty = (b * band + rb - col * band) * R_TH;
+        tx = col * R_TW;
+    };
+    const int64_t npix = (int64_t)a.N * a.H * a.W;
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(a.x, npix * 64 * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rwb = make_rsrc(a.w, (int64_t)64 * 9 * 64 * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rsc = make_rsrc(a.in_scale, SI ? (int64_t)a.N * 64 * 4 : 0);
+    const __amdgpu_buffer_rsrc_t ryb = make_rsrc(a.y, npix * 64 * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t ryr = make_rsrc(a.y_raw, RAW ? npix * 64 * (int64_t)sizeof(T) : 0);
+
+    // ---- weights: this wave's 2 x 9 x 2 A fragments, modulated by the sample's styles ----
+    vec8 wf[2][9][2];
+    auto load_weights = [&](int n) {
+        float4 s4[2][2];
+        if (SI) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) s4[c][hh] = buf_load16<float4>(rsc, (n * 64 + c * 32 + q * 8 + hh * 4) * 4);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int o = p_chan(16 * (2 * h + jj) + l16);
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    vec8 v = buf_load16<vec8>(rwb, ((o * 9 + tap) * 64 + c * 32 + q * 8) * (int)sizeof(T));
+                    if (SI) {
+                        const float4 x0 = s4[c][0], x1 = s4[c][1];
+                        const vec8 sv = vec8{(T)x0.x, (T)x0.y, (T)x0.z, (T)x0.w, (T)x1.x, (T)x1.y, (T)x1.z, (T)x1.w};
+                        if constexpr (std::is_same<T, f16_t>::value) {
+                            v = v * sv;                // v_pk_mul_f16: round(w * round(s))
+                        } else {
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) v[e] = (T)((float)v[e] * (float)sv[e]);
+                        }
+                    }
+                    wf[jj][tap][c] = v;
+                }
+        }
+    };
+    int cur_n;
+    {
+        int ty, tx;
+        tile_of(t_begin, cur_n, ty, tx);
+    }
+    load_weights(cur_n);
+    if (tid < 64) blds[tid] = (EPI && a.bias) ? (float)(T)a.bias[tid] * a.gain : 0.f;
+
+    // ---- LDS-DMA issue: wave w owns instructions i = u * 8 + w, u < R_DMA ----
+    const bool has_noise = EPI && a.noise != nullptr, has_d = EPI && a.out_scale != nullptr;
+    const char* epi_src0 = has_noise ? (const char*)a.noise : (has_d ? (const char*)a.out_scale : (const char*)a.x);
+    const char* epi_src1 = has_d ? (const char*)a.out_scale : epi_src0;
+    // Instruction i < 50 loads halo row hy = i / 5, columns (i % 5) * 8 + lane / 8 (8 whole pixel lines); the
+    // stored piece lane % 8 holds global piece j = (lane % 8) ^ swizzle, a function of the lane only (the column
+    // group adds a multiple of 8).  Row validity is wave-uniform; column validity per lane.
+    const int lx = lane >> 3;
+    const int hlane = lx * 128 + (((lane & 7) ^ (((lx >> 1) & 3) << 1)) * 16);
+    // epilogue table: lanes 0-31 the tile's noise (row lane / 4, 16-byte piece lane % 4), lanes 32-63 the sample's
+    // demodulation scales (16 bytes a lane; lanes 48-63 repeat 32-47 into the unused tail of the table)
+    // (without noise the first half reads the start of whichever buffer stands in for it: always in bounds)
+    const int elane = lane < 32 ? (has_noise ? ((lane >> 2) * a.W + (lane & 3) * 8) * (int)sizeof(T) : 0) : ((lane - 32) & 15) * 16;
+    auto issue = [&](int t, int slot, int eslot) {
+        int n, ty, tx;
+        tile_of(t, n, ty, tx);
+#pragma unroll
+        for (int u = 0; u < R_DMA; ++u) {
+            const int i = u * 8 + wave;               // wave-uniform; u < 6: always a halo instruction (i < 48)
+            if (u < R_DMA - 1 || i < R_HALO_I) {
+                const int hy = i / 5, cg = i - hy * 5;
+                const int iy = ty - 1 + hy, ix0 = tx - 1 + cg * 8;
+                const bool ok = ((unsigned)iy < (unsigned)a.H) & ((unsigned)(ix0 + lx) < (unsigned)a.W) & (cg * 8 + lx < R_TW + 2);
+                const int off = ok ? ((n * a.H + iy) * a.W + ix0) * 128 + hlane : -1;   // -1: out of range, zeros
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rxb, (lds_ptr_t)(smem_raw + slot * R_SLOT + i * 1024), 16, off, 0, 0, 0);
+            } else {                                  // the epilogue table (duplicates write the same bytes)
+                const char* nb = has_noise ? epi_src0 + (int64_t)((n * a.H + ty) * a.W + tx) * (int)sizeof(T) : epi_src0;
+                const char* db = has_d ? epi_src1 + n * 256 : epi_src1;
+                const char* src = (lane < 32 ? nb : db) + elane;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                 (lds_ptr_t)(epil + eslot * R_EPI), 16, 0, 0);
+            }
+        }
+    };
+
+    // MFMA B-fragment addressing: pixel fragment i of the wave at tap (ky, kx), chunk c reads position
+    // (2 wr + (i >> 1) + ky) * 40 + (i & 1) * 16 + l16 + kx, piece c * 4 + q (swizzled as at the DMA)
+    int boff[3][2];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int x = l16 + kx;
+            boff[kx][c] = (2 * wr * R_PITCH + x) * 128 + 16 * ((c * 4 + q) ^ (((x >> 1) & 3) << 1));
+        }
+
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const float lr_alpha = (EPI && a.act == 1) ? a.alpha : 1.f;
+    const float clampv = (EPI && a.clamp >= 0.f) ? a.clamp : __builtin_inff();
+    const float ngain = a.noise_gain * a.gain;
+    const int ch0 = 32 * h + 8 * q;                   // this lane's 8 output channels
+
+    auto epilogue = [&](int t, int eslot) {
+        int n, ty, tx;
+        tile_of(t, n, ty, tx);
+        // The tables are read by inline-asm ds_reads: an LDS-DMA writes this ring, so hipcc would put an
+        // s_waitcnt vmcnt(0) before any ds_read it can see here, draining the two tiles in flight.  The ring
+        // discipline (the DMA of tile t was waited for and a barrier passed) is what orders these reads.
+        const unsigned et = lds_addr(epil + eslot * R_EPI);
+        float bb[8], dd[8], nz[4];
+        if (EPI) {
+            float4 b0, b1, d0, d1;
+            asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
+                         "ds_read_b128 %2, %5 offset:512\n\tds_read_b128 %3, %5 offset:528\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(b0), "=&v"(b1), "=&v"(d0), "=&v"(d1)
+                         : "v"(lds_addr(blds + ch0)), "v"(et + ch0 * 4));
+            bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+            if (has_d) {
+                dd[0] = d0.x; dd[1] = d0.y; dd[2] = d0.z; dd[3] = d0.w; dd[4] = d1.x; dd[5] = d1.y; dd[6] = d1.z; dd[7] = d1.w;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) dd[e] *= a.gain;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) dd[e] = a.gain;
+            }
+            if (has_noise) {
+                unsigned r0, r1, r2, r3;             // pixel (2 wr + (i >> 1)) * 32 + (i & 1) * 16 + l16 of the table
+                const unsigned na = et + (2 * wr * R_TW + l16) * (unsigned)sizeof(T);
+                asm volatile("ds_read_u16 %0, %4\n\tds_read_u16 %1, %4 offset:32\n\tds_read_u16 %2, %4 offset:64\n\t"
+                             "ds_read_u16 %3, %4 offset:96\n\ts_waitcnt lgkmcnt(0)"
+                             : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3) : "v"(na));
+                nz[0] = (float)__builtin_bit_cast(T, (unsigned short)r0) * ngain;
+                nz[1] = (float)__builtin_bit_cast(T, (unsigned short)r1) * ngain;
+                nz[2] = (float)__builtin_bit_cast(T, (unsigned short)r2) * ngain;
+                nz[3] = (float)__builtin_bit_cast(T, (unsigned short)r3) * ngain;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = 2 * wr + (i >> 1), px = (i & 1) * 16 + l16;
+            const int pix = (n * a.H + ty + r) * a.W + tx + px;
+            const float nv = has_noise ? nz[i] : 0.f;
+            vec8 yv, rv;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float cv = acc[i][e >> 2][e & 3];
+                if (RAW) rv[e] = (T)cv;
+                float v = cv;
+                if (EPI) {
+                    v = fmaf(v, dd[e], nv + bb[e]);
+                    v = fmaxf(v, v * lr_alpha);
+                    v = __builtin_amdgcn_fmed3f(v, -clampv, clampv);
+                }
+                yv[e] = (T)v;
+            }
+            const int dst = (pix * 64 + ch0) * (int)sizeof(T);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, dst, 0, 0);
+            if (RAW) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, dst, 0, 0);
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+
+    // ---- prologue: tiles 0 and 1 in flight, wait for tile 0 ----
+    issue(t_begin, 0, 0);
+    issue(min(t_begin + 1, t_end - 1), 1, 1);
+    wait_vm<R_DMA>();
+    __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0): the bias table
+    __builtin_amdgcn_s_barrier();
+
+    int k = 0;
+    for (int t = t_begin; t < t_end; ++t, ++k) {
+        const int slot = k % R_NSLOT;
+        issue(min(t + 2, t_end - 1), (k + 2) % R_NSLOT, (k + 2) % R_NEPI);
+        int n, ty, tx;
+        tile_of(t, n, ty, tx);
+        if (late && k > 0) epilogue(t - 1, (k - 1) % R_NEPI);
+        if (SI && n != cur_n) {                       // a new sample: re-modulate the weights (rare)
+            cur_n = n;
+            load_weights(n);
+        }
+        const char* hb = smem_raw + slot * R_SLOT;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    v8<T> pf[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        pf[i] = *(const v8<T>*)(hb + boff[kx][c] + (((i >> 1) + ky) * R_PITCH + (i & 1) * 16) * 128);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma<T>(wf[jj][ky * 3 + kx][c], pf[i], acc[i][jj]);
+                }
+        if (!late) epilogue(t, k % R_NEPI);
+        // tile t + 1's DMAs (issued one iteration ago) must have landed: everything but the youngest ops of this
+        // wave -- this iteration's DMAs and stores, and the previous iteration's stores issued after them
+        if (!late) {
+            if (k == 0) wait_vm<R_DMA + S>(); else wait_vm<R_DMA + 2 * S>();
+        } else {
+            if (k == 0) wait_vm<R_DMA>(); else if (k == 1) wait_vm<R_DMA + S>(); else wait_vm<R_DMA + 2 * S>();
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): this tile's LDS reads are done
+        __builtin_amdgcn_s_barrier();
+    }
+    if (late) epilogue(t_end - 1, (k - 1) % R_NEPI);
+    wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
+}
+
+template <typename T, bool SI, bool EPI, bool RAW>
+int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
+    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW>;
+    static bool attr_set = false;   // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)R_LDS);
+        attr_set = true;
+    }
+    kern<<<grid, 512, R_LDS, s>>>(a, tiles, band);
+    return launch_status("sg2_conv3x3 (c64 ring)");
+}
+
+template <typename T, bool SI, bool EPI>
+int launch_c64r_raw(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
+    return a.y_raw ? launch_c64r<T, SI, EPI, true>(a, s, tiles, grid, band) : launch_c64r<T, SI, EPI, false>(a, s, tiles, grid, band);
+}
+
 template <typename T>
 int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     const bool si = a.in_scale != nullptr;
@@ -696,6 +1000,21 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         return launch3<T, 32, false, false, 1, 2>(a, s);
     }
     static const bool persist = [] { const char* e = getenv("SG2_HALO_PERSIST"); return !e || atoi(e) != 0; }();
+    static const bool ring = [] { const char* e = getenv("SG2_C64_RING"); return !e || atoi(e) != 0; }();
+    if (ring && !a.dot_out && a.Cin == P_C && a.Cout == P_C && a.H % R_TH == 0 && a.W % R_TW == 0 &&
+        ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 && ((uintptr_t)a.noise % 16) == 0 &&
+        ((uintptr_t)a.out_scale % 16) == 0 && ((uintptr_t)a.in_scale % 16) == 0 &&
+        (!epi || (a.gain > 0.f && (a.act == 0 || (a.alpha >= 0.f && a.alpha <= 1.f))))) {
+        const int tiles = a.N * (a.H / R_TH) * (a.W / R_TW);
+        if (tiles >= 2 * num_cus()) {
+            const int ty = a.H / R_TH;
+            const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
+            const int grid = num_cus();
+            if (si) { if (epi) return launch_c64r_raw<T, true, true>(a, s, tiles, grid, band); return launch_c64r_raw<T, true, false>(a, s, tiles, grid, band); }
+            if (epi) return launch_c64r_raw<T, false, true>(a, s, tiles, grid, band);
+            return launch_c64r_raw<T, false, false>(a, s, tiles, grid, band);
+        }
+    }
     // (the persistent kernel's epilogue folds the gain into the demod / noise / bias terms and evaluates lrelu
     // as max(v, alpha v): it needs gain > 0 and 0 <= alpha <= 1, the StyleGAN2 settings)
     if (persist && a.Cin == P_C && a.Cout == P_C && a.H % P_TH == 0 && a.W % P_TW == 0 &&

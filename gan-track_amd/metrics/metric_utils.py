@@ -211,8 +211,12 @@ def compute_feature_stats_for_dataset(opts, detector_url, detector_kwargs, mode_
     progress = opts.progress.sub(tag='dataset features', num_items=num_items, rel_lo=rel_lo, rel_hi=rel_hi)
     detector = get_feature_detector(detector_url, device=opts.device, num_gpus=opts.num_gpus, rank=opts.rank)
     subset = [(i * opts.num_gpus + opts.rank) % num_items for i in range((num_items - 1) // opts.num_gpus + 1)]
-    for b in range(0, len(subset), batch_size):
-        imgs = torch.from_numpy(np.stack([dataset[i][0] for i in subset[b:b + batch_size]]))
+    # a DataLoader as in the reference (:248): besides batching, creating its iterator draws one value from
+    # torch's global generator, so the generator pass that follows sees the reference's latents
+    if data_loader_kwargs is None:
+        data_loader_kwargs = dict(pin_memory=True, num_workers=3, prefetch_factor=2)
+    for imgs, _labels, _names in torch.utils.data.DataLoader(dataset=dataset, sampler=subset, batch_size=batch_size,
+                                                             **data_loader_kwargs):
         imgs = real_images_to_uint8_quirk(imgs)
         feats = detector(_select_mode(imgs, mode_dict).to(opts.device), **detector_kwargs)
         stats.append_torch(feats, num_gpus=opts.num_gpus, rank=opts.rank)

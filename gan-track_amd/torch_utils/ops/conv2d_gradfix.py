@@ -69,6 +69,21 @@ def _workspace(x, total):
     return ws, True
 
 
+@contextlib.contextmanager
+def _split_k(x, clean):
+    """Split-K calls on the persistent workspace: the call takes it as zeroed and leaves it zeroed (its
+    finalize clears what it read).  A call that fails (a launch error, an aborted capture) may leave it dirty
+    and every later split-K conv would add that garbage: drop the buffer then, so the next call allocates a
+    fresh zeroed one."""
+    try:
+        with _hip.clean_workspace(clean):
+            yield
+    except BaseException:
+        if clean:
+            _CLEAN_WS.pop(x.device, None)
+        raise
+
+
 def _up2_ok(x, cout, oh, ow, kh, kw, stride, pad, transpose):
     """sg2_conv3x3_up2 serves the 16-bit stride-2 transposed 3x3 convs with padding 0 (output 2H+1) from 64^2
     inputs up; below, its 16 x 8 cell tiles are mostly empty (17 x 17 cells at 16^2) and the four-phase
@@ -97,7 +112,7 @@ def _conv_raw(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose):
     y = torch.empty([n, cout, oh, ow], dtype=x.dtype, device=x.device, memory_format=_CL)
     total = n * cout * oh * ow
     ws, clean = _workspace(x, total)
-    with _hip.clean_workspace(clean):
+    with _split_k(x, clean):
         _hip.check(_hip.lib().sg2_conv2d(
             _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
             stride, pad[0], pad[1], int(transpose), _hip.ptr(ws), ws.numel() if ws is not None else 0,
@@ -134,7 +149,7 @@ def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_sca
                             _hip.ptr(dot_src), _hip.ptr(dot))
     total = n * cout * oh * ow
     ws, clean = _workspace(x, total)
-    with _hip.zeroed_accumulators(dot_out is not None and dot is not None), _hip.clean_workspace(clean):
+    with _hip.zeroed_accumulators(dot_out is not None and dot is not None), _split_k(x, clean):
         _hip.check(_hip.lib().sg2_conv2d_fused(
             _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
             stride, pad[0], pad[1], int(transpose), _hip.ptr(in_scale), ctypes.byref(epi) if epi is not None else None,

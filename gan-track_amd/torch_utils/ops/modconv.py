@@ -273,7 +273,9 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
 
 def _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain,
                        clamp, wgain=1.0):
-    """Differentiable form (used under create_graph)."""
+    """Differentiable form (used under create_graph).  With a weight gain the convolutions see weight * wgain
+    (a differentiable op, so the second-order terms reach the raw weight), and the weight gradient is
+    returned for the RAW weight: dL/dW = wgain * dL/d(W * wgain)."""
     if wgain != 1.0:
         weight = weight * wgain        # (rare path: the R1 double backward) the gain as a differentiable op
     n, cin, h, w = x.shape
@@ -312,7 +314,8 @@ def _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c
         if need[1] and styles is not None:
             ds = _cg.dot_hw(dxs, x).to(styles.dtype)
     if need[2] and not _cg.weight_gradients_disabled:
-        dw = _cg._WGrad.apply(dc, _mul(x, s_), (kh, kw), stride, (pad, pad)).to(weight.dtype)
+        dw = _cg._WGrad.apply(dc, _mul(x, s_), (kh, kw), stride, (pad, pad))
+        dw = (dw * wgain if wgain != 1.0 else dw).to(weight.dtype)
     return dx, ds, dw, dd, dnoise, db
 
 

@@ -27,7 +27,8 @@ class _Board:
     def __init__(self):
         self.rows = {}               # name -> row index
         self.tables = {}             # device -> float64 [capacity, 3]
-        self.capacity = 64
+        self.capacity = 256
+        self.captured = False        # a HIP graph holds pointers into the tables: they may not be replaced
         self.total = np.zeros([0, 3], np.float64)   # cumulative moments after the last drain
         self.rank = 0
         self.sync_device = None
@@ -37,8 +38,14 @@ class _Board:
         r = self.rows.get(name)
         if r is None:
             r = self.rows[name] = len(self.rows)
-            if r >= self.capacity:           # grow every table (never during a graph capture: rows are
-                self.capacity *= 2           # registered by the eager warm-up step)
+            if r >= self.capacity:           # grow every table (rows are registered by the eager warm-up step)
+                if self.captured or (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+                    # captured graphs keep accumulating into the old tables: every later report (Loss/signs/real,
+                    # which drives ADA's p, included) would be dropped silently
+                    del self.rows[name]
+                    raise RuntimeError(f'training_stats: statistic {name!r} is new after a HIP graph was captured '
+                                       f'and the board is full ({self.capacity} rows); register it before capture')
+                self.capacity *= 2
                 for dev, t in self.tables.items():
                     g = torch.zeros([self.capacity, 3], dtype=torch.float64, device=dev)
                     g[:t.shape[0]].copy_(t)
@@ -71,6 +78,11 @@ class _Board:
 
 
 _board = _Board()
+
+
+def mark_captured():
+    """A HIP graph that reports statistics has been captured: the device tables are fixed from now on."""
+    _board.captured = True
 
 
 def init_multiprocessing(rank, sync_device):

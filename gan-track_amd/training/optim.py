@@ -46,17 +46,20 @@ class FlatAdam:
             elif p.grad is not None:
                 p.grad.zero_()
 
-    def step_flat(self, flat, offsets, part, grad_scale=1.0, write_grad=True):
+    def step_flat(self, flat, offsets, part, grad_scale=1.0, write_grad=True, tag=None):
         """One Adam step of the parameters `part` (indices into self.params, those with a gradient this
         phase) from `flat`, where parameter i's gradient is flat[offsets[i] : offsets[i] + numel]."""
         if not part:
             return
-        self.prepare(flat, offsets, part)
-        self.launch(flat, part, grad_scale, write_grad)
+        self.prepare(flat, offsets, part, tag)
+        self.launch(flat, part, grad_scale, write_grad, tag)
 
-    def _table(self, flat, offsets, part):
-        """Per participation set: segment table, chunk table and the device buffer of the step scalars."""
-        key = tuple(part)
+    def _table(self, flat, offsets, part, tag=None):
+        """Per (phase tag, participation set): segment table, chunk table and the device buffer of the step
+        scalars.  Keyed by the phase as well: two phases sharing this optimiser (Gmain / Greg) may one day have
+        the same participation set, and a step replays both phase graphs after staging both phases' scalars --
+        one shared buffer would hand the first replay the second phase's bias corrections."""
+        key = (tag, tuple(part))
         tab = self._tables.get(key)
         if tab is None:
             dev = flat.device
@@ -67,7 +70,7 @@ class FlatAdam:
             tab = self._tables[key] = (seg, blocks, nb, coef)
         return tab
 
-    def prepare(self, flat, offsets, part):
+    def prepare(self, flat, offsets, part, tag=None):
         """Advance the step counts of `part` and write torch.optim.Adam's step scalars into the set's device
         buffer (an asynchronous copy on the current stream, ordered before the launch that reads it -- which
         may be a replayed HIP graph)."""
@@ -76,7 +79,7 @@ class FlatAdam:
         if self.exp_avg is None:
             self.exp_avg = torch.zeros_like(flat)
             self.exp_avg_sq = torch.zeros_like(flat)
-        coef_dev = self._table(flat, offsets, part)[3]
+        coef_dev = self._table(flat, offsets, part, tag)[3]
         coef = []
         for i in part:           # torch.optim.Adam's scalars, computed in double as torch does
             self.steps[i] += 1
@@ -84,11 +87,11 @@ class FlatAdam:
             coef += [lr / (1 - b1 ** s), math.sqrt(1 - b2 ** s)]
         coef_dev.copy_(torch.tensor(coef, dtype=torch.float32).pin_memory(), non_blocking=True)
 
-    def launch(self, flat, part, grad_scale=1.0, write_grad=True):
+    def launch(self, flat, part, grad_scale=1.0, write_grad=True, tag=None):
         """The sg2_adam_multi launch of a prepared set (capturable: every operand is a persistent buffer)."""
         g = self.param_groups[0]
         (b1, b2), eps = g['betas'], g['eps']
-        seg, blocks, nb, coef = self._tables[tuple(part)]
+        seg, blocks, nb, coef = self._tables[(tag, tuple(part))]
         L = sg2hip.lib()
         sg2hip.check(L.sg2_adam_multi(sg2hip.ptr(seg), sg2hip.ptr(coef), sg2hip.ptr(blocks), nb, sg2hip.ptr(flat),
                                       sg2hip.ptr(self.exp_avg), sg2hip.ptr(self.exp_avg_sq), b1, b2, eps,

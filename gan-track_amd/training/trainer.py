@@ -258,7 +258,7 @@ class Trainer:
             part0 = ex.expect.get(phase.name)
             st.opt_in_graph = fused_opt and part0 is not None
             if st.opt_in_graph:
-                phase.opt._table(flat, ex.offsets, part0)
+                phase.opt._table(flat, ex.offsets, part0, phase.name)
                 if phase.opt.exp_avg is None:
                     phase.opt.exp_avg = torch.zeros_like(flat)
                     phase.opt.exp_avg_sq = torch.zeros_like(flat)
@@ -273,13 +273,14 @@ class Trainer:
                 st.opt_in_graph = st.opt_in_graph and st.part == part0
                 if st.opt_in_graph:
                     phase.opt.launch(flat, st.part, grad_scale=1.0 / self.num_gpus,
-                                     write_grad=self.on_grads is not None)
+                                     write_grad=self.on_grads is not None, tag=phase.name)
             self._graphs[phase.name] = st
+            training_stats.mark_captured()
             st.views = False
         else:
             self._stage(st, phase, (phase_real_img, phase_real_c), (phase_gen_z, phase_gen_c))
         if st.opt_in_graph:
-            phase.opt.prepare(ex.flat, ex.offsets, st.part)      # the step scalars, ordered before the replay
+            phase.opt.prepare(ex.flat, ex.offsets, st.part, phase.name)   # the step scalars, ordered before the replay
         st.graph.replay()
         ex._filled = [True] * len(ex.buckets)     # filled and reduced inside the graph
         if st.opt_in_graph and st.views:
@@ -305,12 +306,12 @@ class Trainer:
         """Graph mode with every active phase captured, its Adam launch inside its graph and its .grad views
         in place: stage all inputs and step scalars first, then replay the phase graphs back to back.  ROCm's
         graph launch returns when the graph's last kernels are queued, so host work between two replays is
-        GPU idle time; here there is none (the step scalars of a phase live in a buffer of their own per
-        participation set, and each set is used once per step)."""
+        GPU idle time; here there is none (the step scalars of a phase live in a buffer of their own, keyed
+        by phase and participation set, so staging every phase first cannot overwrite another's)."""
         for phase, gz, gc in active:
             st = self._graphs[phase.name]
             self._stage(st, phase, (phase_real_img, phase_real_c), (gz, gc))
-            phase.opt.prepare(phase.exchange.flat, phase.exchange.offsets, st.part)
+            phase.opt.prepare(phase.exchange.flat, phase.exchange.offsets, st.part, phase.name)
         for phase, _, _ in active:
             st = self._graphs[phase.name]
             if phase.start_event is not None:
@@ -357,7 +358,7 @@ class Trainer:
                 part = ex.finish(phase.name, part) if not self.graphs else part
                 if isinstance(phase.opt, FlatAdam):
                     phase.opt.step_flat(ex.flat, ex.offsets, part, grad_scale=1.0 / self.num_gpus,
-                                        write_grad=self.on_grads is not None)
+                                        write_grad=self.on_grads is not None, tag=phase.name)
                 else:
                     flat = ex.flat
                     if self.num_gpus > 1:

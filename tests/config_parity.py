@@ -59,11 +59,28 @@ def make_inputs(cfg, seed=31):
     return dict(z=z, c=c, real=real, gen_z=gen_z, gen_c=gen_c)
 
 
-def run_oracle(cfg, inp, tape, aug_p=0.3):
-    """The CPU oracle's iteration; `tape` records (mode 'record') or replays its draws."""
+def _perturb(t, rel, gen):
+    """t * (1 + rel * u), u = +-1 per entry: an f32-rounding-sized nudge of a state or input."""
+    u = torch.randint(0, 2, t.shape, generator=gen).to(t.dtype) * 2 - 1
+    return t * (1 + rel * u)
+
+
+def run_oracle(cfg, inp, tape, aug_p=0.3, perturb=0.0):
+    """The CPU oracle's iteration; `tape` records (mode 'record') or replays its draws.  perturb > 0: every
+    parameter, real image and latent is multiplied by (1 +- perturb) first (a fixed random sign per entry) --
+    evaluated in float64 with perturb = 2^-24 this measures how far an f32-sized change of the state moves
+    each result, i.e. the conditioning every f32 implementation inherits (config_parity.judge_cond)."""
     from oracle import sg2_oracle as O
     torch.manual_seed(0)
     G, D = _nets(O, cfg, 4)
+    if perturb:
+        gen = torch.Generator().manual_seed(12345)
+        with torch.no_grad():
+            for m in (G, D):
+                for _, p in sorted(m.named_parameters()):
+                    p.copy_(_perturb(p, perturb, gen))
+        inp = {k: (_perturb(torch.from_numpy(np.asarray(v, np.float64)), perturb, gen).numpy()
+                   if k in ('real', 'gen_z', 'z') else v) for k, v in inp.items()}
     G_ema = copy.deepcopy(G).eval()
     aug = O.AugmentPipe(**CLARO_AUG)
     aug.p.fill_(aug_p)
@@ -76,7 +93,7 @@ def run_oracle(cfg, inp, tape, aug_p=0.3):
         out.update(summarize({n: p.grad for n, p in module.named_parameters() if p.grad is not None},
                              f'grad/{name}'))
 
-    T = lambda a: torch.from_numpy(np.array(a, dtype=np.float32)).to(O.REAL)  # noqa: E731
+    T = lambda a: torch.from_numpy(np.array(a, dtype=np.float64)).to(O.REAL)  # noqa: E731 (f32-exact inputs; perturbed ones keep their f64 nudge)
     ctx = tape.record() if not tape.entries else tape.replay()
     with ctx:
         O.train_iteration(loss, O.make_phases(G, D), G, G_ema, T(inp['real']), T(inp['c']), T(inp['gen_z']),
@@ -88,7 +105,7 @@ def run_oracle(cfg, inp, tape, aug_p=0.3):
     return out, [(n, v.numpy()) for n, v in stats]
 
 
-def run_oracle_f64(cfg, inp, tape, aug_p=0.3):
+def run_oracle_f64(cfg, inp, tape, aug_p=0.3, perturb=0.0):
     """The oracle evaluated in float64 on the same draws: the rounding-free answer that f32 results (the
     reference's and the product's alike) are judged against."""
     from oracle import sg2_oracle as O
@@ -96,7 +113,7 @@ def run_oracle_f64(cfg, inp, tape, aug_p=0.3):
     O.REAL = torch.float64
     torch.set_default_dtype(torch.float64)
     try:
-        return run_oracle(cfg, inp, tape, aug_p)
+        return run_oracle(cfg, inp, tape, aug_p, perturb)
     finally:
         O.REAL = prev[0]
         torch.set_default_dtype(prev[1])
@@ -229,6 +246,65 @@ def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
     if check:
         assert not fails, f'{len(fails)} tensors out of bounds; first: {fails[0]}'
     return worst, sorted(ratios)
+
+
+def judge_cond(got, fix, floors=F32_FLOORS, factor=4.0, groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True):
+    """f32 results against the float64 answer, each tensor k held to its OWN conditioning (no phase-wide term):
+
+        err(got_k, f64) <= max(floor, factor * max(err(ref_k, f64), err(f64p_k, f64)))
+
+    f64p is the float64 evaluation with the state and inputs nudged by half an f32 ulp (make_golden.py
+    gen_conditioning): how far a rounding-sized change of the inputs moves tensor k, whatever evaluates it.
+    The reference's own f32 result is a second sample of that spread.  Returns ({group: (worst norm err,
+    worst sample err, worst bound, worst ratio to the bound, its tensor)}, [(ratio, tensor, bound n, bound s)])
+    and raises after computing everything when `check` and any tensor is out of bounds."""
+    truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
+    cond = {k[5:]: v for k, v in fix.items() if k.startswith('f64p/')}
+    assert cond, 'fixture has no f64p/ (conditioning) summaries'
+    kw, kg = _keys(truth, groups), _keys(got, groups)
+    _one_sided_zero(got, truth, kg, kw)
+    keys = sorted(set(kw) & set(kg))
+    worst, rows, fails = {}, [], []
+    for k in keys:
+        gn, gs = _tensor_errs(got, truth, k)
+        rn, rs_ = _tensor_errs(fix, truth, k)
+        cn, cs = _tensor_errs(cond, truth, k) if k + '/norm' in cond else (0.0, 0.0)
+        floor = floors['grad' if k.startswith('grad/') else 'param']
+        bn, bs = max(floor[0], factor * max(rn, cn)), max(floor[1], factor * max(rs_, cs))
+        ratio = max(gn / bn, gs / bs)
+        g = _group(k)
+        w = worst.get(g, (0.0, 0.0, 0.0, 0.0, ''))
+        worst[g] = (max(w[0], gn), max(w[1], gs), max(w[2], bn), max(w[3], ratio), k if ratio > w[3] else w[4])
+        rows.append((ratio, k, bn, bs))
+        if gn > bn:
+            fails.append(f'{k}: norm err vs f64 {gn:.3g} > bound {bn:.3g} (reference f32 {rn:.3g}, conditioning {cn:.3g})')
+        if gs > bs:
+            fails.append(f'{k}: sampled-entry err vs f64 {gs:.3g} > bound {bs:.3g} (reference {rs_:.3g}, conditioning {cs:.3g})')
+    if check:
+        assert not fails, f'{len(fails)} tensors out of bounds; first: {fails[0]}'
+    return worst, sorted(rows, reverse=True)
+
+
+def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True):
+    """Direct product-vs-reference-f32 check on every tensor the reference's f32 result gets right (both its
+    norm and its sampled entries within `well` of the float64 answer): the product must then agree with the
+    reference itself to `tol` on both measures.  Returns (number of tensors checked, worst error, its key)."""
+    truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
+    keys = sorted(set(_keys(truth, groups)) & set(_keys(got, groups)))
+    n, worst, wk, fails = 0, 0.0, '', []
+    for k in keys:
+        rn, rs_ = _tensor_errs(fix, truth, k)
+        if max(rn, rs_) >= well or float(fix[k + '/norm']) == 0.0:
+            continue
+        n += 1
+        en, es = _tensor_errs(got, fix, k)
+        if max(en, es) > worst:
+            worst, wk = max(en, es), k
+        if en > tol or es > tol:
+            fails.append(f'{k}: vs reference f32 norm {en:.3g} samples {es:.3g} > {tol}')
+    if check:
+        assert not fails, f'{len(fails)} of {n} well-conditioned tensors differ from the reference: {fails[0]}'
+    return n, worst, wk
 
 
 def judge_flat(got_flat, ref_flat, floor, factor=3.0):

@@ -466,11 +466,51 @@ def gen_config_iteration(tag, cfg, input_seed=31, tape_seed=13, aug_p=0.3):
     print(tag, 'written', flush=True)
 
 
+# The same widths with the ADA pipe at p = 0: every augmentation's probability is zero, so no discrete choice
+# (integer translation, flips, the reflect-pad margins) can come out differently in f32 and in float64 -- the
+# geometric branch still runs (pad, sym6 up-sampling, identity warp, down-sampling), so R1's double backward
+# still goes through grid_sample.  These fixtures separate rounding from the p = 0.3 fixtures' discrete flips.
+P0_CONFIGS = {f'{k}p0': k for k in ('c2', 'c4', 'c5')}
+
+
+def gen_conditioning(tag, cache_dir=None):
+    """Add 'f64p/...' to train_<tag>.npz: the float64 oracle on the fixture's state, inputs and draws with
+    every parameter, real image and latent nudged by a factor (1 +- 2^-24) -- half an f32 ulp, a fixed random
+    sign per entry (config_parity.run_oracle).  How far that moves each result from the float64 answer is the
+    conditioning any f32 evaluation inherits: measured at C2 / ADA p = 0 it moves the R1 (Dreg) flat gradient
+    by 1.6 % and its bias gradients by 5-17 %, the size of the reference's own f32 error there
+    (profiles/r03_conditioning.txt).  The GPU tests bound each tensor by it (config_parity.judge_cond).
+    Oracle only; slow (C2 ~17 min on 8 cores).  cache_dir: reuse a saved f64p_<tag>.npz."""
+    import config_parity as cp
+    from golden_init import unpack
+    path = os.path.join(OUT, f'train_{tag}.npz')
+    with np.load(path, allow_pickle=False) as f:
+        z = unpack(f)
+    z = {k: v for k, v in z.items() if not k.startswith('f64p/')}
+    with np.load(path, allow_pickle=False) as f:
+        cfg, inp, tape, _ = cp.load_fixture(f)
+    cached = os.path.join(cache_dir, f'f64p_{tag}.npz') if cache_dir else None
+    if cached and os.path.exists(cached):
+        with np.load(cached, allow_pickle=False) as f:
+            out = unpack(f)
+    else:
+        out, _ = cp.run_oracle_f64(cfg, inp, tape, cfg.get('aug_p', 0.3), perturb=2.0 ** -24)
+    z.update({f'f64p/{k}': v for k, v in out.items()})
+    np.savez_compressed(path, **pack(z))
+    print(tag, 'conditioning written', flush=True)
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['ops', 'nets'] + list(CONFIGS)
     for tag in CONFIGS:
         if tag in which:
             gen_config_iteration(tag, CONFIGS[tag])
+    for tag, base in P0_CONFIGS.items():
+        if tag in which:
+            gen_config_iteration(tag, CONFIGS[base], aug_p=0.0)
+    for w in which:
+        if w.startswith('cond:'):          # cond:<tag>[:<cache dir>]
+            parts = w.split(':')
+            gen_conditioning(parts[1], parts[2] if len(parts) > 2 else None)
     if 'ops' not in which:
         sys.exit(0)
     gen_upfirdn2d()

@@ -96,6 +96,60 @@ def test_16bit_iteration_vs_reference(tag, dt):
     _check_flat(res, ref, FLOOR16[dt])
 
 
+# ADA at p = 0 (tests/golden/make_golden.py P0_CONFIGS): no discrete augmentation choice can differ between
+# f32 and float64, and each fixture carries the float64 conditioning summaries (f64p/: the state nudged by
+# half an f32 ulp).  Every tensor is held to max(1e-4, 4 x max(reference f32 error, conditioning)) -- its own
+# conditioning, no phase-wide term -- and every tensor the reference's f32 gets within 1e-4 of float64 must
+# also match the reference's f32 result itself to 3e-4.
+P0_TAGS = ['c2p0', 'c4p0', 'c5p0']
+P0_FLOOR16 = {
+    'fp16': {'grad/Gmain': 1e-2, 'grad/Greg': 2e-2, 'grad/Dmain': 1e-2, 'grad/Dreg': 2e-2, 'param': 1e-3},
+    'bf16': {'grad/Gmain': 4e-2, 'grad/Greg': 6e-2, 'grad/Dmain': 4e-2, 'grad/Dreg': 6e-2, 'param': 2e-3},
+}
+
+
+def _cond_flat(fix):
+    truth = _truth(fix)
+    cond = {k[5:]: v for k, v in fix.items() if k.startswith('f64p/')}
+    ref = cp.compare_flat(fix, truth, GROUPS)
+    con = cp.compare_flat(cond, truth, GROUPS)
+    return {g: (max(ref[g][0], con[g][0]), max(ref[g][1], con[g][1])) for g in GROUPS}, ref, con
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize('tag', P0_TAGS)
+def test_f32_iteration_conditioned(tag):
+    cfg, inp, tape, fix = cp.load_fixture(load(f'train_{tag}.npz'))
+    got, stats = cp.run_product(cfg, inp, tape, DEV, aug_p=cfg['aug_p'])
+    cp.save_summary(f'{tag}_f32', got)
+    worst, rows = cp.judge_cond(got, fix, check=False)
+    nref, wref, kref = cp.judge_vs_reference(got, fix, check=False)
+    spread, ref_flat, cond_flat = _cond_flat(fix)
+    flat = cp.compare_flat(got, _truth(fix), GROUPS)
+    cp.record(f'{tag}_f32_cond', dict(worst=worst, top=rows[:8], max_bound={g: w[2] for g, w in worst.items()},
+                                      vs_reference=(nref, wref, kref), flat=flat, reference_flat=ref_flat,
+                                      conditioning_flat=cond_flat))
+    cp.judge_cond(got, fix)
+    cp.judge_vs_reference(got, fix)
+    cp.judge_stats_f32(stats, fix)
+    cp.judge_pl_mean(got, fix)
+    cp.judge_flat({g: v for g, v in flat.items() if g.startswith('grad/')}, spread, floor=1e-4)
+    cp.judge_flat({g: v for g, v in flat.items() if not g.startswith('grad/')}, spread, floor=(1e-5, 1e-4))
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize('tag,dt', [('c2p0', 'fp16'), ('c4p0', 'fp16'), ('c5p0', 'bf16'), ('c2p0', 'bf16')])
+def test_16bit_iteration_conditioned(tag, dt):
+    cfg, inp, tape, fix = cp.load_fixture(load(f'train_{tag}.npz'))
+    got, _ = cp.run_product(cfg, inp, tape, DEV, fp16_dtype=torch.float16 if dt == 'fp16' else torch.bfloat16,
+                            aug_p=cfg['aug_p'])
+    cp.save_summary(f'{tag}_{dt}', got)
+    res = cp.compare_flat(got, _truth(fix), GROUPS)
+    spread, ref_flat, cond_flat = _cond_flat(fix)
+    cp.record(f'{tag}_{dt}_cond', dict(flat=res, reference_f32_flat=ref_flat, conditioning_flat=cond_flat))
+    _check_flat(res, spread, P0_FLOOR16[dt])
+
+
 class _RecordingTape(cp.Tape):
     """A tape whose replay() records instead: the product draws the sequence itself."""
     def replay(self):

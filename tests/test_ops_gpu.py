@@ -1199,6 +1199,25 @@ def test_split_k_clean_workspace():
     assert float(cg._CLEAN_WS[x.device].abs().max()) == 0.0
     ref = torch.nn.functional.conv2d(x.double(), w.double(), padding=1)
     assert rel_err(first.double(), ref) < 1e-5
+    # captured into a graph and replayed back to back with eager calls: the same shared workspace
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        cap = cg._conv_raw(x, wp, 512, 8, 8, 3, 3, 1, (1, 1), False)
+    for _ in range(2):
+        g.replay()
+        eager = cg._conv_raw(x, wp, 512, 8, 8, 3, 3, 1, (1, 1), False)
+    torch.cuda.synchronize()
+    assert rel_err(cap, first) < 1e-6 and rel_err(eager, first) < 1e-6
+    assert float(cg._CLEAN_WS[x.device].abs().max()) == 0.0
+    # a failing call drops the workspace (it may be dirty); the next call gets a fresh zeroed one
+    ws0 = cg._CLEAN_WS[x.device]
+    with pytest.raises(RuntimeError):
+        with cg._split_k(x, True):
+            raise RuntimeError('launch failed')
+    assert x.device not in cg._CLEAN_WS
+    again = cg._conv_raw(x, wp, 512, 8, 8, 3, 3, 1, (1, 1), False)
+    assert cg._CLEAN_WS[x.device] is not ws0 and rel_err(again, first) < 1e-6
 
 
 def test_depthwise_1d_grouped_conv():
@@ -1222,3 +1241,87 @@ def test_depthwise_1d_grouped_conv():
         ggw, = torch.autograd.grad(gx.square().sum(), [w])
         ggwr, = torch.autograd.grad(gxr.square().sum(), [wr])
         assert rel_err(ggw.double(), ggwr) < 1e-5
+
+
+@pytest.mark.parametrize('mode', ['composed', 'create_graph'])
+def test_fused_conv_wgain_weight_grad(mode):
+    """FusedConv with a weight gain (a Conv2dLayer's 1/sqrt(fan_in), networks_stylegan2.py:173) on the composed
+    backward -- modconv.fast_backward off, or a create_graph backward -- vs float64 torch: the weight gradient is
+    for the RAW weight, dL/dW = wgain * dL/d(W * wgain), as are dx and db (the composed path once
+    returned dL/d(W * wgain))."""
+    from torch_utils.ops import modconv
+    torch.manual_seed(51)
+    N, Cin, H, Cout = 2, 16, 12, 24
+    wgain = 1 / np.sqrt(Cin * 9)
+    x0 = torch.randn(N, Cin, H, H, device=DEV).contiguous(memory_format=torch.channels_last)
+    w0 = torch.randn(Cout, Cin, 3, 3, device=DEV)
+    b0 = torch.randn(Cout, device=DEV) * 0.1
+    dy = torch.randn(N, Cout, H, H, device=DEV)
+    x, w, b = (t.clone().requires_grad_(True) for t in (x0, w0, b0))
+    prev = modconv.fast_backward
+    modconv.fast_backward = mode != 'composed'
+    try:
+        y = modconv.fused_conv(x, w, bias=b, padding=1, act='lrelu', gain=np.sqrt(2), clamp=256.0, wgain=wgain)
+        grads = torch.autograd.grad((y * dy).sum(), [x, w, b], create_graph=(mode == 'create_graph'))
+    finally:
+        modconv.fast_backward = prev
+    xr, wr, br = (t.detach().double().requires_grad_(True) for t in (x0, w0, b0))
+    yr = F.leaky_relu(F.conv2d(xr, wr * wgain, br, padding=1), 0.2) * np.sqrt(2)
+    ref = torch.autograd.grad((yr * dy.double()).sum(), [xr, wr, br])
+    assert rel_err(y.double(), yr) < 1e-5
+    for name, g, r in zip(('dx', 'dw', 'db'), grads, ref):
+        assert rel_err(g.double(), r) < 1e-4, name
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(4, 256, 256), (11, 48, 256), (13, 40, 256), (3, 64, 704)])
+@pytest.mark.parametrize('form', ['mod_epi_raw', 'mod_epi', 'mod_only', 'plain_epi', 'plain', 'epi_no_noise'])
+def test_conv3x3_c64_ring(dtype, shape, form):
+    """The 64 -> 64 channel ring kernel (LDS-DMA halo ring, weights in registers modulated per sample, staggered
+    epilogue; conv3x3.hip conv3x3_c64r_kernel) in every form the layers use -- the synthesis forward (modulation,
+    demod, noise, bias, lrelu, clamp, raw output), the path-length pass's scaled transposed conv (modulation only),
+    the D conv (bias + lrelu + clamp), a plain conv -- against float64.  Shapes cover bands of 4 / 2 / 1 tile rows,
+    runs that cross samples (the per-sample weight re-modulation) and image borders on every side."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    N, H, W = shape
+    C = 64
+    assert N * (H // 8) * (W // 32) >= 512          # the ring kernel's minimum of two tiles per CU
+    torch.manual_seed(17)
+    x = torch.randn(N, C, H, W)
+    w = torch.randn(C, C, 3, 3) / np.sqrt(C * 9)
+    s = torch.rand(N, C) + 0.5
+    d = torch.rand(N, C) + 0.5
+    noise = torch.randn(N, 1, H, W)
+    b = torch.randn(C) * 0.1
+    mod = form.startswith('mod')
+    epi = 'epi' in form
+    demod_noise = form.startswith('mod_epi')
+    kw = {}
+    if epi:
+        kw.update(bias=b.to(DEV), act=1, alpha=0.2, gain=np.sqrt(2), clamp=1.5)
+    if demod_noise:
+        kw.update(out_scale=d.to(DEV), noise=noise.to(DEV, dtype).reshape(N, H, W).contiguous(), noise_gain=0.3)
+    if form == 'epi_no_noise':
+        kw.update(out_scale=d.to(DEV))
+    xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    wp = cg._pack_conv(w.to(DEV, dtype))
+    y, raw = cg.conv3x3_fused(xd, wp, C, in_scale=s.to(DEV) if mod else None, want_raw=form.endswith('raw'), **kw)
+    xs = (x.to(dtype).float() * s[:, :, None, None]).to(dtype).double() if mod else x.to(dtype).double()
+    c = F.conv2d(xs, w.to(dtype).double(), padding=1)
+    ref = c
+    if epi:
+        z = c * (d[:, :, None, None] if (demod_noise or form == 'epi_no_noise') else 1)
+        if demod_noise:
+            z = z + noise.to(dtype).double() * 0.3
+        z = z + b[None, :, None, None]
+        ref = (F.leaky_relu(z, 0.2) * np.sqrt(2)).clamp(-1.5, 1.5)
+    tol = 5e-3 if dtype == torch.float16 else 2e-2
+    assert rel_err(y.float(), ref) < tol
+    if form.endswith('raw'):
+        assert rel_err(raw.float(), c) < tol
+    # every border pixel and every sample individually (a missed halo zero or a stale weight set shows here)
+    for n in range(N):
+        assert rel_err(y[n].float(), ref[n]) < 2 * tol, n
+    edge = torch.zeros(H, W, dtype=torch.bool)
+    edge[0], edge[-1], edge[:, 0], edge[:, -1] = True, True, True, True
+    assert rel_err(y.float()[..., edge], ref[..., edge]) < 2 * tol

@@ -94,7 +94,9 @@ class _FakeWork:
 def test_graph_exchange_overlap_simulated_ranks(monkeypatch):
     """Two ranks simulated on one GPU: all_reduce(t) -> t *= 2 (the sum of two identical ranks) on the
     stream it is issued on.  Eager hook path, graph path (fills and reductions captured from the hooks)
-    and the non-overlapped single exchange must give identical parameters."""
+    and the non-overlapped single exchange must give identical parameters.  Six iterations with both reg
+    intervals 2: iteration 4 replays all four phase graphs back to back (_replay_step), with Gmain / Greg and
+    Dmain / Dreg each sharing one FlatAdam whose step scalars are staged for both phases before either replays."""
     from training.trainer import Trainer
     from golden_util import load
     from parity_train import build_product, CLARO_AUG
@@ -117,7 +119,7 @@ def test_graph_exchange_overlap_simulated_ranks(monkeypatch):
         gen = torch.Generator(device=DEV)
         gen.manual_seed(5)
         torch.manual_seed(123)
-        for it in range(4):
+        for it in range(6):
             if it == 1:
                 tr.graphs = mode == 'graph'
             real = torch.rand([cfg['batch'], 1, 32, 32], device=DEV, generator=gen) * 2 - 1

@@ -24,24 +24,13 @@ import torch
 
 # ------------------------------------------------------------------------------------------- dataset
 def _make_zip(path, modalities=('CT',), res=16, patients=3, slices=4, labels=True, evil=False):
-    rs = np.random.RandomState(0)
-    names, lab = [], []
-    with zipfile.ZipFile(path, 'w') as z:
-        for split in ('train', 'val'):
-            for p in range(patients):
-                for s in range(slices):
-                    d = {m: (rs.rand(res, res) * 255).astype(np.float64) for m in modalities}
-                    rel = f'p{p:03d}/p{p:03d}_{s:05d}.pickle'
-                    z.writestr(f'{split}/{rel}', pickle.dumps(d))
-                    if split == 'train':
-                        names.append(rel)
-                        lab.append([rel, p % 2])
-            if labels:
-                z.writestr(f'{split}/dataset.json', json.dumps({'labels': lab if split == 'train' else []}))
-        if evil:
-            class Evil:
-                def __reduce__(self):
-                    return (os.system, ('echo pwned',))
+    from synth_zip import make_zip
+    names = make_zip(path, modalities=modalities, res=res, patients=patients, slices=slices, labels=labels)
+    if evil:
+        class Evil:
+            def __reduce__(self):
+                return (os.system, ('echo pwned',))
+        with zipfile.ZipFile(path, 'a') as z:
             z.writestr('train/zzz/zzz_00000.pickle', pickle.dumps({'CT': Evil()}))
     return names
 
@@ -286,3 +275,163 @@ def copy_module(m):
 
 
 
+
+
+def test_stats_board_refuses_growth_after_capture():
+    """training_stats keeps one device table per device; captured phase graphs hold pointers into it.  A new
+    statistic name that needs a bigger table after a capture must raise instead of silently re-allocating
+    (the captured reports -- Loss/signs/real, which drives ADA's p -- would go to the old table)."""
+    from torch_utils import training_stats as ts
+    b = ts._Board()
+    b.table(torch.device('cpu'))
+    for i in range(b.capacity):
+        b.row(f'stat{i}')
+    b.row('stat0')                       # existing names never grow the table
+    b.captured = True
+    with pytest.raises(RuntimeError, match='after a HIP graph was captured'):
+        b.row('one_too_many')
+    assert 'one_too_many' not in b.rows and len(b.rows) == b.capacity
+    b.captured = False
+    b.row('one_too_many')                # before any capture the board grows, keeping its rows
+    assert b.tables[torch.device('cpu')].shape[0] == b.capacity == 512
+
+
+# ------------------------------------------------------------------------- parity with the reference's own runs
+# tests/golden/shell_ref.npz was written by the REFERENCE (tests/golden/make_shell_golden.py) on the same
+# synthetic zips (tests/golden/synth_zip.py): bit-exact for the index / byte work, float64 rounding for FID.
+def _shell_ref():
+    import ast
+    z = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'shell_ref.npz'), allow_pickle=False)
+    return z, ast.literal_eval(str(z['zips'])), ast.literal_eval(str(z['datasets']))
+
+
+def _ref_zips(tmp_path, zips):
+    from synth_zip import make_zip
+    paths = {}
+    for name, kw in zips.items():
+        paths[name] = str(tmp_path / f'{name}.zip')
+        make_zip(paths[name], **kw)
+    return paths
+
+
+def _dataset_kwargs(zpath, kw):
+    import dnnlib
+    d = dict(class_name='training.dataset_mi_multimodal.CustomImageFolderDataset', path=zpath, dtype='float32',
+             split='train', use_labels=False, xflip=False, max_size=None)
+    d.update(kw)
+    return dnnlib.EasyDict(d)
+
+
+def test_data_path_matches_reference(tmp_path):
+    """Every item (file name, label, CRC of the decoded float32 image after the x-flip), max_size / xflip
+    indexing, the split's substring file selection, InfiniteSampler's index streams and the first batches the
+    training loop consumes (DeviceImageCache vs the reference's DataLoader + / 127.5 - 1), bit for bit against
+    the reference's own run (SG3/training/dataset_mi_multimodal.py:30-285, torch_utils/misc.py:111-142)."""
+    import zlib
+    import dnnlib
+    from torch_utils import misc
+    from training.dataset_mi_multimodal import DeviceImageCache
+    z, zips, datasets = _shell_ref()
+    paths = _ref_zips(tmp_path, zips)
+    crc = lambda a: zlib.crc32(np.ascontiguousarray(a).tobytes())   # noqa: E731
+    for name, (zname, kw) in datasets.items():
+        ds = dnnlib.util.construct_class_by_name(**_dataset_kwargs(paths[zname], kw))
+        assert len(ds) == int(z[f'ds/{name}/len']), name
+        assert np.array_equal(ds._raw_idx, z[f'ds/{name}/raw_idx']) and np.array_equal(ds._xflip, z[f'ds/{name}/xflip'])
+        items = [ds[i] for i in range(len(ds))]
+        assert [it[2] for it in items] == z[f'ds/{name}/fnames'].tolist(), name
+        assert np.array_equal(np.stack([it[1] for it in items]).astype(np.float32), z[f'ds/{name}/labels']), name
+        assert [crc(it[0]) for it in items] == z[f'ds/{name}/crc'].tolist(), name
+        for key in [k for k in z.files if k.startswith(f'ds/{name}/sampler/')]:
+            rank, nrep, seed = map(int, key.rsplit('/', 1)[1].split('_'))
+            it = iter(misc.InfiniteSampler(ds, rank=rank, num_replicas=nrep, seed=seed))
+            assert [next(it) for _ in range(100)] == z[key].tolist(), key
+        for key in [k for k in z.files if k.startswith(f'ds/{name}/batches/')]:
+            rank, nrep, seed = map(int, key.rsplit('/', 1)[1].split('_'))
+            cache = DeviceImageCache(ds, 'cpu', batch_size=5, rank=rank, num_replicas=nrep, seed=seed)
+            got = [[crc(img.numpy()), crc(c.numpy())] for img, c in (next(cache) for _ in range(3))]
+            assert got == z[key].tolist(), key
+    assert int(z['ds/quirk/len']) == 14      # 12 train slices + the 2 'val/retrain*' ones the substring rule admits
+
+
+@pytest.mark.parametrize('case', ['ct_peak', 'pelvis'])
+def test_fid_pipeline_matches_reference(tmp_path, case):
+    """compute_fid and both feature-statistics passes (real: the x 255 / uint8 quirk or the pass-through, per
+    modality; generated: latents, labels from the dataset, uint8 conversion) against the reference's own run with
+    the same stub detector and generator (tests/golden/stub_metric.py) and seeds: moments to float64 rounding,
+    FID to 1e-9 relative (SG3/metrics/metric_utils.py:201-306, frechet_inception_distance.py:19-40).  The real
+    Inception network is not available offline, so FID-50k itself stays unmeasured here."""
+    import ast
+    from metrics import metric_utils, frechet_inception_distance as fidm
+    from stub_metric import StubDetector, StubGenerator
+    z, zips, _ = _shell_ref()
+    paths = _ref_zips(tmp_path, zips)
+    args = ast.literal_eval(str(z[f'fid/{case}/args']))
+    if case == 'ct_peak':
+        dkw = _dataset_kwargs(paths['ct_peak'], dict(modalities=['CT'], use_labels=True))
+        G = StubGenerator(c_dim=2, img_channels=1)
+    else:
+        dkw = _dataset_kwargs(paths['pelvis'], dict(modalities=['MR_MR_T2', 'MR_nonrigid_CT']))
+        G = StubGenerator(c_dim=0, img_channels=2)
+    metric_utils.register_detector(fidm.DETECTOR_URL, StubDetector(res=16))
+    mode = args['mode']
+
+    def opts():
+        return metric_utils.MetricOptions(G=G, dataset_kwargs=dkw, num_gpus=1, rank=0, device=torch.device('cpu'),
+                                          cache=False, mode_dict=mode)
+    np.random.seed(5)
+    torch.manual_seed(6)
+    fid = fidm.compute_fid(opts(), args['max_real'], args['num_gen'])
+    np.random.seed(5)
+    torch.manual_seed(6)
+    kw = dict(detector_url=fidm.DETECTOR_URL, detector_kwargs=dict(return_features=True), mode_dict=mode,
+              capture_mean_cov=True)
+    mr, sr = metric_utils.compute_feature_stats_for_dataset(opts=opts(), rel_lo=0, rel_hi=0, max_items=args['max_real'],
+                                                            **kw).get_mean_cov()
+    mg, sg = metric_utils.compute_feature_stats_for_generator(opts=opts(), rel_lo=0, rel_hi=1, max_items=args['num_gen'],
+                                                              **kw).get_mean_cov()
+    for k, v in dict(mu_real=mr, sigma_real=sr, mu_gen=mg, sigma_gen=sg).items():
+        ref = z[f'fid/{case}/{k}']
+        assert np.allclose(v, ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max()), k
+    ref_fid = float(z[f'fid/{case}/fid'])
+    assert abs(fid - ref_fid) <= 1e-9 * abs(ref_fid), (fid, ref_fid)
+
+
+REF_SG3 = '/root/reference/src/models/stylegan3'
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_SG3), reason='needs the reference tree (build container only)')
+def test_snapshot_from_reference(tmp_path):
+    """A network-snapshot pickle written by the REFERENCE's own persistence / pickling (tests/golden/ref_snapshot.py,
+    run in a subprocess on the reference tree) loads with this build's legacy.load_network_pkl -- without executing
+    the source it embeds -- into this build's classes, every parameter and buffer bit-equal, the constructor
+    arguments and the augment pipe's p preserved (SG3/torch_utils/persistence.py:35-130, legacy.py:22-58).  The
+    pickle embeds the reference's source, so it is produced here and never committed."""
+    import subprocess
+    import sys
+    import legacy
+    from training import networks_stylegan2 as net, augment_mi
+    pkl, npz = tmp_path / 'network-snapshot-000000.pkl', tmp_path / 'ref_state.npz'
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE='1',
+               PYTHONPATH=os.pathsep.join([REF_SG3, os.path.join(os.path.dirname(__file__), 'golden')]))
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), 'golden', 'ref_snapshot.py'), str(pkl),
+                        str(npz)], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    ref = np.load(npz, allow_pickle=False)
+    with open(pkl, 'rb') as f:
+        data = legacy.load_network_pkl(f)
+    assert isinstance(data['G'], net.Generator) and isinstance(data['D'], net.Discriminator)
+    assert isinstance(data['G_ema'], net.Generator) and isinstance(data['augment_pipe'], augment_mi.AugmentPipe)
+    assert data['training_set_kwargs']['modalities'] == ['CT']
+    import ast
+    n_checked = 0
+    for key in ('G', 'D', 'G_ema', 'augment_pipe'):
+        got = dict(list(data[key].named_parameters()) + list(data[key].named_buffers()))
+        want = {k.split('/', 1)[1]: ref[k] for k in ref.files if k.startswith(key + '/') and not k.endswith('init_kwargs')}
+        assert set(got) == set(want), (key, set(got) ^ set(want))
+        for n, v in want.items():
+            assert got[n].dtype == torch.from_numpy(v).dtype and np.array_equal(got[n].detach().numpy(), v), (key, n)
+            n_checked += 1
+        assert not data[key].training
+        assert dict(data[key].init_kwargs) == ast.literal_eval(str(ref[f'{key}/init_kwargs'])), key
+    assert float(data['augment_pipe'].p) == 0.375 and n_checked > 100
