@@ -715,6 +715,9 @@ constexpr size_t R_LDS = (size_t)R_NSLOT * R_SLOT + R_NEPI * R_EPI + 64 * 4;   /
 static_assert(R_LDS <= 160 * 1024, "ring LDS");
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+#ifndef SG2_RDIAG
+#define SG2_RDIAG 0         // timing-only builds of the ring kernel (tools/ring_diag.sh): 16 no loads, 32 no stores, 64 no MFMA
+#endif
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {    // byte address in LDS of a __shared__ pointer
     return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
@@ -738,27 +741,35 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l16 = lane & 15, q = lane >> 4;
     const int h = wave & 1, wr = (wave >> 1) & 3;     // channel half, tile row pair
-    const bool late = wave >= 4;                      // staggered half: epilogue deferred by one tile
-    const int tiles_x = a.W / R_TW, tiles_y = a.H / R_TH;
-    const int per_n = tiles_x * tiles_y, per_band = band * tiles_x;
     const int t_begin = (int)((int64_t)blockIdx.x * tiles_total / gridDim.x);
     const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles_total / gridDim.x);
     if (t_begin >= t_end) return;
     // tile t -> (n, ty, tx): samples, bands of `band` tile rows, column-major inside a band (vertical neighbours,
-    // which share two halo rows, are consecutive in a CU's run)
-    auto tile_of = [&](int t, int& n, int& ty, int& tx) {
-        n = t / per_n;
-        const int r = t - n * per_n, b = r / per_band, rb = r - b * per_band;
-        const int col = rb / band;
-        ty = (b * band + rb - col * band) * R_TH;
-        tx = col * R_TW;
+    // which share two halo rows, are consecutive in a CU's run).  Lane j of tinfo0 / tinfo1 holds tile
+    // t_begin + j / + 64 + j packed, so a tile's coordinates are one v_readlane in the loop, not three runtime
+    // divisions (the host sends at most 128 tiles per workgroup here)
+    auto pack_tile = [&](int t) -> int {
+        const int tiles_x = a.W / R_TW, per_n = tiles_x * (a.H / R_TH), per_band = band * tiles_x;
+        const int n = t / per_n, r = t - n * per_n, b = r / per_band, rb = r - b * per_band, col = rb / band;
+        return (n << 20) | ((b * band + rb - col * band) << 10) | col;
     };
-    const int64_t npix = (int64_t)a.N * a.H * a.W;
-    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(a.x, npix * 64 * (int64_t)sizeof(T));
-    const __amdgpu_buffer_rsrc_t rwb = make_rsrc(a.w, (int64_t)64 * 9 * 64 * (int64_t)sizeof(T));
-    const __amdgpu_buffer_rsrc_t rsc = make_rsrc(a.in_scale, SI ? (int64_t)a.N * 64 * 4 : 0);
-    const __amdgpu_buffer_rsrc_t ryb = make_rsrc(a.y, npix * 64 * (int64_t)sizeof(T));
-    const __amdgpu_buffer_rsrc_t ryr = make_rsrc(a.y_raw, RAW ? npix * 64 * (int64_t)sizeof(T) : 0);
+    const int tinfo0 = t_begin + lane < t_end ? pack_tile(t_begin + lane) : 0;
+    const int tinfo1 = t_begin + 64 + lane < t_end ? pack_tile(t_begin + 64 + lane) : 0;
+    auto tile_of = [&](int t, int& n, int& ty, int& tx) {
+        const int j = t - t_begin;
+        const int v = j < 64 ? __builtin_amdgcn_readlane(tinfo0, j) : __builtin_amdgcn_readlane(tinfo1, j - 64);
+        n = v >> 20;
+        ty = ((v >> 10) & 1023) * R_TH;
+        tx = (v & 1023) * R_TW;
+    };
+    // (the host checked N H W 64 sizeof(T) < 2^31; readfirstlane keeps the descriptors provably uniform -- a
+    // descriptor hipcc cannot prove uniform is rebuilt per lane in a readfirstlane loop around every load)
+    const int xbytes = __builtin_amdgcn_readfirstlane(a.N * a.H * a.W * 64 * (int)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(a.x, xbytes);
+    const __amdgpu_buffer_rsrc_t rwb = make_rsrc(a.w, 64 * 9 * 64 * (int)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rsc = make_rsrc(a.in_scale, SI ? __builtin_amdgcn_readfirstlane(a.N * 64 * 4) : 0);
+    const __amdgpu_buffer_rsrc_t ryb = make_rsrc(a.y, xbytes);
+    const __amdgpu_buffer_rsrc_t ryr = make_rsrc(a.y_raw, RAW ? xbytes : 0);
 
     // ---- weights: this wave's 2 x 9 x 2 A fragments, modulated by the sample's styles ----
     vec8 wf[2][9][2];
@@ -814,6 +825,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
     // (without noise the first half reads the start of whichever buffer stands in for it: always in bounds)
     const int elane = lane < 32 ? (has_noise ? ((lane >> 2) * a.W + (lane & 3) * 8) * (int)sizeof(T) : 0) : ((lane - 32) & 15) * 16;
     auto issue = [&](int t, int slot, int eslot) {
+        if (SG2_RDIAG & 16) return;                   // timing-only build: no loads
         int n, ty, tx;
         tile_of(t, n, ty, tx);
 #pragma unroll
@@ -822,8 +834,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
             if (u < R_DMA - 1 || i < R_HALO_I) {
                 const int hy = i / 5, cg = i - hy * 5;
                 const int iy = ty - 1 + hy, ix0 = tx - 1 + cg * 8;
-                const bool ok = ((unsigned)iy < (unsigned)a.H) & ((unsigned)(ix0 + lx) < (unsigned)a.W) & (cg * 8 + lx < R_TW + 2);
-                const int off = ok ? ((n * a.H + iy) * a.W + ix0) * 128 + hlane : -1;   // -1: out of range, zeros
+                // uniform row base; a row outside the image gets a negative base (every lane out of range: zeros).
+                // Per lane only the image's left / right border column must read zeros; the pad lanes (column
+                // 34 .. 39 of the halo row, never read) may load whatever follows.
+                const int base = (unsigned)iy < (unsigned)a.H ? ((n * a.H + iy) * a.W + ix0) * 128 : -(1 << 30);
+                const bool kill = ((tx == 0) & (cg == 0) & (lx == 0)) | ((tx + R_TW == a.W) & (cg == 4) & (lx == 1));
+                const int off = kill ? -1 : base + hlane;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rxb, (lds_ptr_t)(smem_raw + slot * R_SLOT + i * 1024), 16, off, 0, 0, 0);
             } else {                                  // the epilogue table (duplicates write the same bytes)
                 const char* nb = has_noise ? epi_src0 + (int64_t)((n * a.H + ty) * a.W + tx) * (int)sizeof(T) : epi_src0;
@@ -847,11 +863,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
         }
 
     f32x4 acc[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-
     const float lr_alpha = (EPI && a.act == 1) ? a.alpha : 1.f;
     const float clampv = (EPI && a.clamp >= 0.f) ? a.clamp : __builtin_inff();
     const float ngain = a.noise_gain * a.gain;
@@ -910,11 +921,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
                 }
                 yv[e] = (T)v;
             }
-            const int dst = (pix * 64 + ch0) * (int)sizeof(T);
+            const int dst = (pix * 64 + ch0) * (int)sizeof(T) | -(int)((SG2_RDIAG & 32) != 0);   // timing-only build: dropped
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, dst, 0, 0);
             if (RAW) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, dst, 0, 0);
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
 
@@ -931,7 +940,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
         issue(min(t + 2, t_end - 1), (k + 2) % R_NSLOT, (k + 2) % R_NEPI);
         int n, ty, tx;
         tile_of(t, n, ty, tx);
-        if (late && k > 0) epilogue(t - 1, (k - 1) % R_NEPI);
         if (SI && n != cur_n) {                       // a new sample: re-modulate the weights (rare)
             cur_n = n;
             load_weights(n);
@@ -947,23 +955,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
                         pf[i] = *(const v8<T>*)(hb + boff[kx][c] + (((i >> 1) + ky) * R_PITCH + (i & 1) * 16) * 128);
+                    const bool first = c == 0 && ky == 0 && kx == 0;   // the tile's first tap starts each chain at 0
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
 #pragma unroll
-                        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma<T>(wf[jj][ky * 3 + kx][c], pf[i], acc[i][jj]);
+                        for (int jj = 0; jj < 2; ++jj) {
+                            if (SG2_RDIAG & 64) acc[i][jj][0] = (first ? 0.f : acc[i][jj][0]) + (float)pf[i][jj] * (float)wf[jj][ky * 3 + kx][c][i];   // timing-only build
+                            else acc[i][jj] = mma<T>(wf[jj][ky * 3 + kx][c], pf[i], first ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jj]);
+                        }
                 }
-        if (!late) epilogue(t, k % R_NEPI);
+        epilogue(t, k % R_NEPI);
         // tile t + 1's DMAs (issued one iteration ago) must have landed: everything but the youngest ops of this
         // wave -- this iteration's DMAs and stores, and the previous iteration's stores issued after them
-        if (!late) {
-            if (k == 0) wait_vm<R_DMA + S>(); else wait_vm<R_DMA + 2 * S>();
-        } else {
-            if (k == 0) wait_vm<R_DMA>(); else if (k == 1) wait_vm<R_DMA + S>(); else wait_vm<R_DMA + 2 * S>();
-        }
+        if (k == 0) wait_vm<R_DMA + S>(); else wait_vm<R_DMA + 2 * S>();
         __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): this tile's LDS reads are done
         __builtin_amdgcn_s_barrier();
     }
-    if (late) epilogue(t_end - 1, (k - 1) % R_NEPI);
     wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
 }
 
@@ -1006,7 +1013,7 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         ((uintptr_t)a.out_scale % 16) == 0 && ((uintptr_t)a.in_scale % 16) == 0 &&
         (!epi || (a.gain > 0.f && (a.act == 0 || (a.alpha >= 0.f && a.alpha <= 1.f))))) {
         const int tiles = a.N * (a.H / R_TH) * (a.W / R_TW);
-        if (tiles >= 2 * num_cus()) {
+        if (tiles >= 2 * num_cus() && tiles <= 128 * num_cus() && a.N < 4096 && a.H / R_TH < 1024 && a.W / R_TW < 1024) {
             const int ty = a.H / R_TH;
             const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
             const int grid = num_cus();

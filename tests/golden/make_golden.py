@@ -203,7 +203,9 @@ def gen_augment():
     d = {}
     names = []
     for cfg_name, cfg, shape in [('claro', CLARO_AUG, (2, 1, 32, 32)), ('full3', FULL_AUG, (2, 3, 24, 24)),
-                                 ('full1', FULL_AUG, (2, 1, 28, 28))]:
+                                 ('full1', FULL_AUG, (2, 1, 28, 28)),
+                                 # + the additive-noise branch (augment_mi.py:427-433), which FULL_AUG leaves out
+                                 ('noise3', dict(FULL_AUG, noise=1), (2, 3, 24, 24))]:
         pipe = augment_mi.AugmentPipe(run_dir=None, batch_size=shape[0], **cfg)
         d[f'{cfg_name}_cfg'] = np.array(repr(cfg))
         for pct in [0.1, 0.5, 0.9]:
@@ -211,7 +213,14 @@ def gen_augment():
             names.append(name)
             r = rs(int(pct * 100) + len(cfg))
             x = T(r.uniform(-1, 1, shape), rg=True)
-            y = pipe(x, False, debug_percentile=pct)
+            if cfg.get('noise', 0):
+                # the noise branch draws its pixel noise even at a debug percentile (augment_mi.py:431): record it
+                tape = Tape(seed=11)
+                with tape.record():
+                    y = pipe(x, False, debug_percentile=pct)
+                d.update(tape.to_npz_dict(prefix=f'{name}_tape'))
+            else:
+                y = pipe(x, False, debug_percentile=pct)
             dy = r.standard_normal(tuple(y.shape)).astype(np.float32)
             gx, = torch.autograd.grad((y * T(dy)).sum(), [x])
             d[f'{name}_x'] = npy(x)
@@ -511,6 +520,8 @@ if __name__ == '__main__':
         if w.startswith('cond:'):          # cond:<tag>[:<cache dir>]
             parts = w.split(':')
             gen_conditioning(parts[1], parts[2] if len(parts) > 2 else None)
+    if 'aug' in which:
+        gen_augment()
     if 'ops' not in which:
         sys.exit(0)
     gen_upfirdn2d()

@@ -110,6 +110,11 @@ def test_augment(name):
         tape = Tape.from_npz(z, prefix=f'{name}_tape')
         with tape.replay():
             y = pipe(x, False)
+    elif any(k.startswith(f'{name}_tape') for k in z.files):    # the noise branch: pixel noise drawn at any percentile
+        tape = Tape.from_npz(z, prefix=f'{name}_tape')
+        with tape.replay():
+            y = pipe(x, False, debug_percentile=float(name.split('_p')[1]))
+        assert tape.pos == len(tape.entries)
     else:
         y = pipe(x, False, debug_percentile=float(name.split('_p')[1]))
     assert rel_err(y, z[f'{name}_y']) < 1e-5
