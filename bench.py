@@ -21,7 +21,8 @@ schedule's 6.25 %, so a 20-step value is slightly pessimistic).
 value = images processed by all ranks / max-over-ranks wall time of the K timed steps.
 
 Extra fields: `roofline` for the dominant kernel (the MFMA implicit-GEMM convolution of the 256^2
-layers, timed with HIP events on the launching stream after the timed region) and `cpu_baseline`
+layers -- the top-resolution synthesis layer at the run's own batch, so C4 / C5 report their 512^2 C=64 /
+1024^2 C=32 layers -- timed with HIP events on the launching stream after the timed region) and `cpu_baseline`
 (the CPU oracle restatement of the same iteration on the host cores, bounded sample, rank 0, N=1).
 """
 import argparse
@@ -164,17 +165,17 @@ def _measured_traffic(key):
         return None, None
 
 
-def roofline(device, res, cbase, dtype):
+def roofline(device, res, cbase, dtype, N=32):
     """Roofline of the dominant kernel, the LDS-halo MFMA 3x3 conv (sg2_conv3x3; at C = 64 its persistent
     form conv3x3_c64p_kernel), on the 256^2 synthesis layer the north star names.  Its
     arithmetic intensity (~286 FLOP/B at C = 64, 16-bit) is below the MI355X ridge (2500 TFLOP/s / 8 TB/s
     = 312 FLOP/B), so the bound is HBM: achieved = algorithmic bytes / measured launch time.  The MFMA
     view of the same launch and of the MFMA-bound 32^2 / C = 512 layer are reported beside it."""
     C = min(cbase // res, 512)
-    ms, flops, byts = _layer_launch(device, res, C, dtype)
+    ms, flops, byts = _layer_launch(device, res, C, dtype, N)
     ai = flops / byts
     ridge = MFMA_PEAK_FP16 * 1e12 / (HBM_PEAK * 1e9)
-    key = f'sg2_conv3x3 fused {res}^2 C={C} N=32 {str(dtype).split(".")[-1]}'
+    key = f'sg2_conv3x3 fused {res}^2 C={C} N={N} {str(dtype).split(".")[-1]}'
     gbps = byts / (ms * 1e-3) / 1e9
     tflops = flops / (ms * 1e-3) / 1e12
     ring = C == 64 and os.environ.get('SG2_C64_RING', '1') != '0'
@@ -305,7 +306,8 @@ def main():
                     if ph.start_event is not None}
     roof = None
     if not args.no_roofline:
-        roof = roofline(device, args.res, args.cbase, torch.float16 if args.fp16_dtype == 'fp16' else torch.bfloat16)
+        roof = roofline(device, args.res, args.cbase, torch.float16 if args.fp16_dtype == 'fp16' else torch.bfloat16,
+                        args.batch_gpu)
     cpu = None
     if rank == 0 and num_gpus == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)

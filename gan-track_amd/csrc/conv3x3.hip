@@ -699,24 +699,38 @@ int num_cus() {
 //     fragments by s rounded to T (round(W * round(s)) where the reference rounds x * round(s): a product
 //     rounded once either way);
 //   * the tile's noise and demodulation scales arrive by a 1 KiB LDS-DMA into a 4-deep epilogue ring;
-//   * one barrier per tile, counted vmcnt waits (never 0 in the loop), and the two waves of a SIMD staggered:
-//     waves 0-3 run a tile's epilogue after its MFMAs, waves 4-7 defer it to the start of the next tile, so one
-//     wave's epilogue VALU and stores sit beside its partner's MFMAs.
-// Wave w: rows 2 ((w >> 1) & 3), +1 of the tile (4 pixel fragments of 16) x its 32 channels: per tap and chunk 4
+//   * one barrier per tile and counted vmcnt waits (never 0 in the loop);
+//   * (default form, TH = 4) two workgroups of 4 waves per CU, each on its own 32 x 4 tiles with a 2-slot ring,
+//     so that a SIMD's two waves belong to workgroups that drift apart: one's MFMAs run beside the other's
+//     epilogue VALU, stores and barrier wait (measured: the memory streams alone -- the halo DMA 0.053 ms, the
+//     stores at 7 TB/s, tools/membench.py -- are well under the kernel time; its one-workgroup 8-wave form
+//     spent the difference with both waves of a SIMD in the same phase).
+// Wave w: rows 2 (w >> 1), +1 of the tile (4 pixel fragments of 16) x its 32 channels: per tap and chunk 4
 // ds_read_b128 (pixels) feed 8 MFMAs (weights from registers).
-constexpr int R_TW = 32, R_TH = 8, R_PITCH = 40;
-constexpr int R_HPOS = (R_TH + 2) * R_PITCH;          // 400 halo positions (34 used per row)
-constexpr int R_SLOT = R_HPOS * 128;                  // 51,200 B
-constexpr int R_NSLOT = 3;
-constexpr int R_EPI = 1024, R_NEPI = 4;               // noise [256] T at 0, demod [64] f32 at 512
-constexpr int R_HALO_I = R_HPOS / 8;                  // 50 halo DMA wave-instructions per tile
-constexpr int R_DMA = 7;                              // DMA wave-instructions per wave and tile (56 >= 50 + 1)
-constexpr size_t R_LDS = (size_t)R_NSLOT * R_SLOT + R_NEPI * R_EPI + 64 * 4;   // + gain * bias [64]
-static_assert(R_LDS <= 160 * 1024, "ring LDS");
+constexpr int R_TW = 32, R_PITCH = 40;
+constexpr int R_EPI = 1024, R_NEPI = 4;               // noise [TH x 32] T at 0, demod [64] f32 at 512
+// Two forms (template TH): TH = 8 -- 32 x 8 tiles, 8 waves, one workgroup per CU, a 3-slot ring (two tiles in
+// flight); TH = 4 -- 32 x 4 tiles, 4 waves, TWO workgroups per CU, each with a 2-slot ring.  The waves of a
+// workgroup meet at one barrier per tile, so in the one-workgroup form a SIMD's two waves reach their MFMA,
+// epilogue and barrier phases together; two workgroups drift apart and one's MFMAs run beside the other's
+// epilogue, stores and barrier wait.
+template <int TH> struct Ring {
+    static constexpr int NW = TH;                                     // waves: 2 channel halves x TH / 2 row pairs
+    static constexpr int NSLOT = TH == 8 ? 3 : 2;
+    static constexpr int HPOS = (TH + 2) * R_PITCH;                   // halo positions (34 used per row)
+    static constexpr int SLOT = HPOS * 128;                           // 51,200 / 30,720 B
+    static constexpr int HALO_I = HPOS / 8;                           // halo DMA wave-instructions per tile
+    static constexpr int DMA = (HALO_I + 1 + NW - 1) / NW;            // per wave and tile (+ the epilogue table)
+    static constexpr size_t LDS = (size_t)NSLOT * SLOT + R_NEPI * R_EPI + 64 * 4;   // + gain * bias [64]
+    static constexpr int WGS_PER_CU = TH == 8 ? 1 : 2;
+    static_assert(LDS * WGS_PER_CU <= 160 * 1024, "ring LDS");
+    static_assert((DMA - 1) * NW <= HALO_I && DMA * NW > HALO_I, "the last DMA round holds the epilogue table");
+};
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 #ifndef SG2_RDIAG
 #define SG2_RDIAG 0         // timing-only builds of the ring kernel (tools/ring_diag.sh): 16 no loads, 32 no stores, 64 no MFMA
+                            // (128: the pad lanes load the pixels that follow, the round-3 first form)
 #endif
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {    // byte address in LDS of a __shared__ pointer
@@ -729,9 +743,11 @@ __device__ __forceinline__ void wait_vm() {           // s_waitcnt vmcnt(N) (gfx
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <typename T, bool SI, bool EPI, bool RAW>
-__global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band) {
+template <typename T, bool SI, bool EPI, bool RAW, int R_TH>
+__global__ __launch_bounds__(Ring<R_TH>::NW * 64, Ring<R_TH>::WGS_PER_CU) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
+    typedef Ring<R_TH> RG;
+    constexpr int R_NSLOT = RG::NSLOT, R_SLOT = RG::SLOT, R_HALO_I = RG::HALO_I, R_DMA = RG::DMA, NW = RG::NW;
     constexpr int S = RAW ? 8 : 4;                    // buffer stores per wave and tile
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     char* epil = smem_raw + R_NSLOT * R_SLOT;
@@ -740,7 +756,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l16 = lane & 15, q = lane >> 4;
-    const int h = wave & 1, wr = (wave >> 1) & 3;     // channel half, tile row pair
+    const int h = wave & 1, wr = wave >> 1;           // channel half, tile row pair
     const int t_begin = (int)((int64_t)blockIdx.x * tiles_total / gridDim.x);
     const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles_total / gridDim.x);
     if (t_begin >= t_end) return;
@@ -811,7 +827,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
     load_weights(cur_n);
     if (tid < 64) blds[tid] = (EPI && a.bias) ? (float)(T)a.bias[tid] * a.gain : 0.f;
 
-    // ---- LDS-DMA issue: wave w owns instructions i = u * 8 + w, u < R_DMA ----
+    // ---- LDS-DMA issue: wave w owns instructions i = u * NW + w, u < R_DMA ----
     const bool has_noise = EPI && a.noise != nullptr, has_d = EPI && a.out_scale != nullptr;
     const char* epi_src0 = has_noise ? (const char*)a.noise : (has_d ? (const char*)a.out_scale : (const char*)a.x);
     const char* epi_src1 = has_d ? (const char*)a.out_scale : epi_src0;
@@ -820,25 +836,29 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
     // group adds a multiple of 8).  Row validity is wave-uniform; column validity per lane.
     const int lx = lane >> 3;
     const int hlane = lx * 128 + (((lane & 7) ^ (((lx >> 1) & 3) << 1)) * 16);
-    // epilogue table: lanes 0-31 the tile's noise (row lane / 4, 16-byte piece lane % 4), lanes 32-63 the sample's
-    // demodulation scales (16 bytes a lane; lanes 48-63 repeat 32-47 into the unused tail of the table)
+    // epilogue table: lanes 0-31 the tile's noise (row (lane / 4) mod TH, 16-byte piece lane % 4; with TH = 4 lanes
+    // 16-31 repeat rows 0-3 into the unused rows 4-7 of the table), lanes 32-63 the sample's demodulation scales
+    // (16 bytes a lane; lanes 48-63 repeat 32-47 into the unused tail of the table)
     // (without noise the first half reads the start of whichever buffer stands in for it: always in bounds)
-    const int elane = lane < 32 ? (has_noise ? ((lane >> 2) * a.W + (lane & 3) * 8) * (int)sizeof(T) : 0) : ((lane - 32) & 15) * 16;
+    const int elane = lane < 32 ? (has_noise ? (((lane >> 2) % R_TH) * a.W + (lane & 3) * 8) * (int)sizeof(T) : 0)
+                                : ((lane - 32) & 15) * 16;
     auto issue = [&](int t, int slot, int eslot) {
         if (SG2_RDIAG & 16) return;                   // timing-only build: no loads
         int n, ty, tx;
         tile_of(t, n, ty, tx);
 #pragma unroll
         for (int u = 0; u < R_DMA; ++u) {
-            const int i = u * 8 + wave;               // wave-uniform; u < 6: always a halo instruction (i < 48)
+            const int i = u * NW + wave;              // wave-uniform; u < R_DMA - 1: always a halo instruction
             if (u < R_DMA - 1 || i < R_HALO_I) {
                 const int hy = i / 5, cg = i - hy * 5;
                 const int iy = ty - 1 + hy, ix0 = tx - 1 + cg * 8;
                 // uniform row base; a row outside the image gets a negative base (every lane out of range: zeros).
-                // Per lane only the image's left / right border column must read zeros; the pad lanes (column
-                // 34 .. 39 of the halo row, never read) may load whatever follows.
+                // Per lane the image's left / right border column reads zeros, and the pad lanes (column 34 .. 39
+                // of the halo row, never read) read nothing: an out-of-range lane moves no bytes (15 % of the
+                // halo's requests)
                 const int base = (unsigned)iy < (unsigned)a.H ? ((n * a.H + iy) * a.W + ix0) * 128 : -(1 << 30);
-                const bool kill = ((tx == 0) & (cg == 0) & (lx == 0)) | ((tx + R_TW == a.W) & (cg == 4) & (lx == 1));
+                const bool kill = ((tx == 0) & (cg == 0) & (lx == 0)) | ((tx + R_TW == a.W) & (cg == 4) & (lx == 1)) |
+                                  (!(SG2_RDIAG & 128) & (cg == 4) & (lx >= 2));
                 const int off = kill ? -1 : base + hlane;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rxb, (lds_ptr_t)(smem_raw + slot * R_SLOT + i * 1024), 16, off, 0, 0, 0);
             } else {                                  // the epilogue table (duplicates write the same bytes)
@@ -927,17 +947,21 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
         }
     };
 
-    // ---- prologue: tiles 0 and 1 in flight, wait for tile 0 ----
+    // ---- prologue: tiles 0 .. NSLOT - 2 in flight, wait for tile 0 ----
     issue(t_begin, 0, 0);
-    issue(min(t_begin + 1, t_end - 1), 1, 1);
-    wait_vm<R_DMA>();
+    if (R_NSLOT == 3) {
+        issue(min(t_begin + 1, t_end - 1), 1, 1);
+        wait_vm<R_DMA>();
+    } else {
+        wait_vm<0>();
+    }
     __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0): the bias table
     __builtin_amdgcn_s_barrier();
 
     int k = 0;
     for (int t = t_begin; t < t_end; ++t, ++k) {
         const int slot = k % R_NSLOT;
-        issue(min(t + 2, t_end - 1), (k + 2) % R_NSLOT, (k + 2) % R_NEPI);
+        issue(min(t + R_NSLOT - 1, t_end - 1), (k + R_NSLOT - 1) % R_NSLOT, (k + R_NSLOT - 1) % R_NEPI);
         int n, ty, tx;
         tile_of(t, n, ty, tx);
         if (SI && n != cur_n) {                       // a new sample: re-modulate the weights (rare)
@@ -965,30 +989,43 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64r_kernel(Conv3Args a, int t
                         }
                 }
         epilogue(t, k % R_NEPI);
-        // tile t + 1's DMAs (issued one iteration ago) must have landed: everything but the youngest ops of this
-        // wave -- this iteration's DMAs and stores, and the previous iteration's stores issued after them
-        if (k == 0) wait_vm<R_DMA + S>(); else wait_vm<R_DMA + 2 * S>();
+        // tile t + 1's DMAs must have landed: everything but the youngest ops of this wave.  3 slots: t + 1 was
+        // issued one iteration ago, younger are this iteration's DMAs and stores and the previous iteration's
+        // stores; 2 slots: t + 1 was issued at the top of this iteration, younger are this iteration's stores
+        if (R_NSLOT == 2) wait_vm<S>();
+        else if (k == 0) wait_vm<R_DMA + S>();
+        else wait_vm<R_DMA + 2 * S>();
         __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): this tile's LDS reads are done
         __builtin_amdgcn_s_barrier();
     }
     wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
 }
 
-template <typename T, bool SI, bool EPI, bool RAW>
+template <typename T, bool SI, bool EPI, bool RAW, int TH>
 int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
-    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW>;
+    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW, TH>;
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)R_LDS);
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)Ring<TH>::LDS);
         attr_set = true;
     }
-    kern<<<grid, 512, R_LDS, s>>>(a, tiles, band);
+    kern<<<grid, Ring<TH>::NW * 64, Ring<TH>::LDS, s>>>(a, tiles, band);
     return launch_status("sg2_conv3x3 (c64 ring)");
 }
 
-template <typename T, bool SI, bool EPI>
+template <typename T, bool SI, bool EPI, int TH>
 int launch_c64r_raw(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
-    return a.y_raw ? launch_c64r<T, SI, EPI, true>(a, s, tiles, grid, band) : launch_c64r<T, SI, EPI, false>(a, s, tiles, grid, band);
+    return a.y_raw ? launch_c64r<T, SI, EPI, true, TH>(a, s, tiles, grid, band)
+                   : launch_c64r<T, SI, EPI, false, TH>(a, s, tiles, grid, band);
+}
+
+template <typename T, bool SI, bool EPI>
+int launch_c64r_th(const Conv3Args& a, hipStream_t s, int th) {
+    const int tiles = a.N * (a.H / th) * (a.W / R_TW);
+    const int ty = a.H / th;
+    const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
+    if (th == 4) return launch_c64r_raw<T, SI, EPI, 4>(a, s, tiles, 2 * num_cus(), band);
+    return launch_c64r_raw<T, SI, EPI, 8>(a, s, tiles, num_cus(), band);
 }
 
 template <typename T>
@@ -1007,19 +1044,20 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         return launch3<T, 32, false, false, 1, 2>(a, s);
     }
     static const bool persist = [] { const char* e = getenv("SG2_HALO_PERSIST"); return !e || atoi(e) != 0; }();
-    static const bool ring = [] { const char* e = getenv("SG2_C64_RING"); return !e || atoi(e) != 0; }();
-    if (ring && !a.dot_out && a.Cin == P_C && a.Cout == P_C && a.H % R_TH == 0 && a.W % R_TW == 0 &&
+    // SG2_C64_RING: 0 off, 8 the one-workgroup 32 x 8 form, 4 (default) the two-workgroup 32 x 4 form
+    const char* ring_env = getenv("SG2_C64_RING");   // read per launch: tests switch forms in one process
+    const int ring = ring_env ? atoi(ring_env) : 4;
+    const int rth = ring == 8 ? 8 : 4;
+    if (ring && !a.dot_out && a.Cin == P_C && a.Cout == P_C && a.H % rth == 0 && a.W % R_TW == 0 &&
         ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 && ((uintptr_t)a.noise % 16) == 0 &&
         ((uintptr_t)a.out_scale % 16) == 0 && ((uintptr_t)a.in_scale % 16) == 0 &&
         (!epi || (a.gain > 0.f && (a.act == 0 || (a.alpha >= 0.f && a.alpha <= 1.f))))) {
-        const int tiles = a.N * (a.H / R_TH) * (a.W / R_TW);
-        if (tiles >= 2 * num_cus() && tiles <= 128 * num_cus() && a.N < 4096 && a.H / R_TH < 1024 && a.W / R_TW < 1024) {
-            const int ty = a.H / R_TH;
-            const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
-            const int grid = num_cus();
-            if (si) { if (epi) return launch_c64r_raw<T, true, true>(a, s, tiles, grid, band); return launch_c64r_raw<T, true, false>(a, s, tiles, grid, band); }
-            if (epi) return launch_c64r_raw<T, false, true>(a, s, tiles, grid, band);
-            return launch_c64r_raw<T, false, false>(a, s, tiles, grid, band);
+        const int tiles = a.N * (a.H / rth) * (a.W / R_TW);
+        const int grid = (rth == 4 ? 2 : 1) * num_cus();
+        if (tiles >= 2 * grid && tiles <= 128 * grid && a.N < 4096 && a.H / rth < 1024 && a.W / R_TW < 1024) {
+            if (si) { if (epi) return launch_c64r_th<T, true, true>(a, s, rth); return launch_c64r_th<T, true, false>(a, s, rth); }
+            if (epi) return launch_c64r_th<T, false, true>(a, s, rth);
+            return launch_c64r_th<T, false, false>(a, s, rth);
         }
     }
     // (the persistent kernel's epilogue folds the gain into the demod / noise / bias terms and evaluates lrelu

@@ -32,6 +32,7 @@ _CL = torch.channels_last
 enabled = True         # switch for A/B tests against the composed (unfused) path
 prezero = os.environ.get('SG2_PREZERO', '1') != '0'   # one zero fill per layer backward (A/B switch)
 fast_backward = True   # first-order backward through the fused kernels (A/B switch)
+fused_vjp = os.environ.get('SG2_FUSED_VJP', '1') != '0'   # create_graph input-gradient pass as one node (A/B)
 _ACT = {0: 'linear', 1: 'lrelu'}
 
 
@@ -109,6 +110,11 @@ class FusedConv(torch.autograd.Function):
         if not torch.is_grad_enabled() and fast_backward:
             g = _fast_backward(need, dy, _cg._nhwc(x), styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act,
                                alpha, gain, clamp, wgain)
+        elif fused_vjp and _cg.weight_gradients_disabled and not has_res and (dcoefs is None or c is not None):
+            # the path-length / R1 pass: input gradients only, as one node with fused kernels both ways
+            dx, ds, dd = _LayerVJP.apply(dy, x, styles, weight, dcoefs, zsrc, c, need[0], need[1], need[3],
+                                         stride, pad, act, alpha, gain, clamp, wgain)
+            g = (dx, ds, None, dd, None, None)
         else:
             g = _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha,
                                    gain, clamp, wgain)
@@ -229,6 +235,128 @@ class _SavedRaw(torch.autograd.Function):
         dx, ds, dw = _scaled_input_grads(_cg._nhwc(dc.to(x.dtype)), _cg._nhwc(x), styles,
                                          weight, need[0], need[1], need[2], stride, pad)
         return dx, ds, dw, None, None, None
+
+
+def _conv_any(x, weight, cout, oh, ow, stride, pad, transpose, wgain, **epi):
+    """One fused conv launch of the layer geometry: the LDS-halo kernel for 16-bit 3x3/s1/p1, the implicit GEMM
+    otherwise.  transpose: the input gradient's convT (weight [Cout, Cin, kh, kw] read as its adjoint).  epi:
+    in_scale / out_scale / dot_src / want_raw.  Returns (y, raw or None, dot or None)."""
+    kh, kw = weight.shape[2], weight.shape[3]
+    dt = x.dtype
+    want_raw = epi.pop('want_raw', False)
+    dot_src = epi.get('dot_src')
+    if _halo(x, kh, kw, stride, pad):
+        wp = _cg._pack_convT(weight, dt, flip=True, scale=wgain) if transpose else _cg._pack_conv(weight, dt, scale=wgain)
+        res = _cg.conv3x3_fused(x, wp, cout, want_raw=want_raw, **epi)
+    else:
+        wp = _cg._pack_convT(weight, dt, scale=wgain) if transpose else _cg._pack_conv(weight, dt, scale=wgain)
+        res = _cg.conv_fused(x, wp, cout, oh, ow, kh, kw, stride, (pad, pad), transpose=transpose,
+                             aux_mode=1 if want_raw else 0, **epi)
+    return res[0], res[1], (res[2] if dot_src is not None else None)
+
+
+class _LayerVJP(torch.autograd.Function):
+    """The layer's input-gradient VJP as one differentiable node: the path-length pass (loss.py pl_no_weight_grad,
+    reference loss.py:85-100 under conv2d_gradfix.no_weight_gradients) and R1's create_graph pass differentiate it
+    once more.  For z = act(c * d + noise + b) * gain, c = conv(x * s, W):
+        forward    dc = act'(dy; y) * d, dd = sum_hw act'(dy; y) * c      (sg2_layer_bwd, one pass)
+                   dxs = convT(dc, W); dx = dxs * s; ds = sum_hw dxs * x     (one dgrad launch, raw dxs kept)
+        backward   G = g_dx * s + g_ds * x
+                   A = conv(G, W):  g_dy = act'(A * d + g_dd * c; y),  g_d = sum_hw A * dc / d
+                   H = g_dd * act'(dy; y) = dc * (g_dd / d):
+                       g_x = g_ds * dxs + convT(H, W) * s,   g_s = sum_hw g_dx * dxs + sum_hw convT(H, W) * x
+                   g_W = wgrad(dc, G) + wgrad(dc * g_dd / d, x * s)   (x wgain for the raw weight)
+    (act' of lrelu / linear is piecewise constant in y: no second-order term in y, as the reference's bias_act grad.)
+    Each conv is one fused launch with its scales on the operand staging and its reductions in the epilogue, where
+    the composed form runs the conv recompute, two dot kernels and the elementwise products as separate nodes."""
+
+    @staticmethod
+    def forward(ctx, dy, x, styles, weight, dcoefs, zsrc, c, need_x, need_s, need_d, stride, pad, act, alpha, gain,
+                clamp, wgain):
+        xk = _cg._nhwc(x)
+        n, cin, h, w = xk.shape
+        cout = weight.shape[0]
+        dt = xk.dtype
+        d32, s32 = _f32(dcoefs), _f32(styles)
+        want_dd = need_d and d32 is not None
+        want_ds = need_s and s32 is not None
+        if zsrc.shape[1] % 8 == 0:
+            dc, _, dd, _ = _cg.layer_bwd(dy.to(dt), zsrc, c if want_dd else None, d32, act=act, alpha=alpha, gain=gain,
+                                         clamp=clamp, want_db=False, want_dd=want_dd, want_dnoise=False)
+        else:   # narrow outputs (toRGB)
+            dz = _ba.bias_act_grad(dy.to(dt), zsrc, act=_ACT[act], alpha=alpha, gain=gain, clamp=clamp)
+            dd = (dz * c).sum([2, 3], dtype=torch.float32) if want_dd else None
+            dc = _cg._nhwc(dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if d32 is not None else dz)
+        dx, dxs, ds = _conv_any(dc, weight, cin, h, w, stride, pad, True, wgain, out_scale=s32,
+                                dot_src=xk if want_ds else None, want_raw=s32 is not None)
+        if dxs is None:
+            dxs = dx
+        ctx.save_for_backward(xk, styles, weight, dcoefs, zsrc, c, dc, dxs)
+        ctx.cfg = (stride, pad, act, alpha, gain, clamp, wgain)
+        return (dx if need_x else None, ds.to(styles.dtype) if want_ds else None,
+                dd.to(dcoefs.dtype) if want_dd else None)
+
+    @staticmethod
+    def backward(ctx, g_dx, g_ds, g_dd):
+        if torch.is_grad_enabled():
+            raise RuntimeError('_LayerVJP: third-order gradients are not supported (set modconv.fused_vjp = False)')
+        x, styles, weight, dcoefs, zsrc, c, dc, dxs = ctx.saved_tensors
+        stride, pad, act, alpha, gain, clamp, wgain = ctx.cfg
+        need = ctx.needs_input_grad
+        n, cin, h, w = x.shape
+        cout, _, kh, kw = weight.shape
+        oh, ow = dc.shape[2], dc.shape[3]
+        dt = x.dtype
+        d32, s32 = _f32(dcoefs), _f32(styles)
+        s_ = styles.to(dt).reshape(n, -1, 1, 1) if styles is not None else None
+        g_dy = g_x = g_s = g_w = g_d = None
+        # G = dL/d(dxs)
+        G = None
+        if g_dx is not None:
+            G = _cg._nhwc(_mul(g_dx.to(dt), s_))
+        if g_ds is not None and s_ is not None:
+            t = x * g_ds.to(dt).reshape(n, -1, 1, 1)
+            G = t if G is None else G + t
+        hscale = (g_dd.float() / d32).contiguous() if (g_dd is not None and d32 is not None) else None
+        if G is not None and (need[0] or need[4]):
+            A_d, _, dot = _conv_any(G, weight, cout, oh, ow, stride, pad, False, wgain, out_scale=d32,
+                                    dot_src=dc if (need[4] and d32 is not None) else None)
+            if need[4] and d32 is not None:
+                g_d = (dot / d32).to(dcoefs.dtype)
+            if need[0]:
+                gz = A_d if hscale is None else torch.addcmul(A_d, c, g_dd.to(dt).reshape(n, -1, 1, 1))
+                g_dy = _act_grad(gz, zsrc, act, alpha, gain, clamp)
+        elif need[0] and hscale is not None:
+            g_dy = _act_grad(c * g_dd.to(dt).reshape(n, -1, 1, 1), zsrc, act, alpha, gain, clamp)
+        if need[1] or need[2]:
+            if g_ds is not None and need[1]:
+                g_x = dxs * g_ds.to(dt).reshape(n, -1, 1, 1)
+            if g_dx is not None and need[2] and s_ is not None:
+                g_s = _cg.dot_hw(_cg._nhwc(g_dx.to(dt)), dxs)
+            if hscale is not None:
+                gxc, _, gsc = _conv_any(dc, weight, cin, h, w, stride, pad, True, wgain, in_scale=hscale,
+                                        out_scale=s32, dot_src=x if (need[2] and s32 is not None) else None)
+                if need[1]:
+                    g_x = gxc if g_x is None else g_x + gxc
+                if gsc is not None:
+                    g_s = gsc if g_s is None else g_s + gsc
+        if need[3] and (G is not None or hscale is not None):
+            acc = torch.zeros([cout * kh * kw * cin], dtype=torch.float32, device=x.device)
+            if G is not None:
+                _cg._wgrad_raw(dc, G, kh, kw, stride, (pad, pad), alpha=wgain, out=acc)
+            if hscale is not None:
+                _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32, g_scale=hscale, alpha=wgain, out=acc)
+            g_w = acc.view(cout, kh, kw, cin).permute(0, 3, 1, 2).to(weight.dtype)
+        g_s = g_s.to(styles.dtype) if g_s is not None else None
+        return (g_dy, g_x, g_s, g_w, g_d) + (None,) * 12
+
+
+def _act_grad(g, y, act, alpha, gain, clamp):
+    """act'(g; y): the bias_act gradient with respect to its input, given the output y (no bias term)."""
+    if y.shape[1] % 8 == 0:
+        return _cg.layer_bwd(g, y, None, None, act=act, alpha=alpha, gain=gain, clamp=clamp, want_db=False,
+                             want_dd=False, want_dnoise=False)[0]
+    return _ba.bias_act_grad(g, y, act=_ACT[act], alpha=alpha, gain=gain, clamp=clamp)
 
 
 def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain, clamp,
@@ -394,6 +522,11 @@ class UpModConv(torch.autograd.Function):
         oh, ow = y.shape[2], y.shape[3]
         aup, adown, apad, aflip = _up.adjoint_params(f, (th, tw), (oh, ow), 1, 1, fpad, False)
         dx = ds = dw = dd = dn = db = None
+        if torch.is_grad_enabled() and fused_vjp and _cg.weight_gradients_disabled and c is not None:
+            # the path-length pass: input gradients only, one node with fused kernels both ways
+            dx, ds, dd = _UpLayerVJP.apply(dy, x, styles, weight, dcoefs, y, c, f, need[0], need[1], need[3],
+                                           alpha, gain, clamp, tpad, (th, tw), fpad)
+            return (dx, ds, None, dd, None, None, None, None, None, None)
         if not torch.is_grad_enabled() and fast_backward:
             d32, s32 = _f32(dcoefs), _f32(styles)
             want_dd = need[3] and d32 is not None
@@ -442,6 +575,102 @@ class UpModConv(torch.autograd.Function):
         cast = lambda g, ref: g.to(ref.dtype) if (g is not None and ref is not None) else g
         return (dx, cast(ds, styles), cast(dw, weight), cast(dd, dcoefs), cast(dn, noise), cast(db, bias),
                 None, None, None, None)
+
+
+class _UpLayerVJP(torch.autograd.Function):
+    """_LayerVJP for the up-2 layer (c = FIR(convT_s2(x * s, W)) * 4, z = act(c * d + noise + b) * gain), the
+    path-length pass's other layer form.  With F the 4x4 FIR and L_W the stride-2 transposed conv:
+        forward    dc = act'(dy; y) * d, dd = sum_hw act'(dy; y) * c                 (sg2_layer_bwd)
+                   u = F^T dc (adjoint FIR), dxs = L_W^T u; dx = dxs * s, ds = sum_hw dxs * x   (one dgrad launch)
+        backward   G = g_dx * s + g_ds * x
+                   A d = F(L_W G) * d  (the layer's own forward on G: up-2 conv + FIR with the d scale)
+                   g_dy = act'(A d + g_dd * c; y),  g_d = sum_hw (A d) * dc / d^2
+                   H = g_dd * act'(dy; y) = dc * g_dd / d, and F^T H = u * g_dd / d (F is per channel), so
+                   g_x = g_ds * dxs + L_W^T(u * g_dd / d) * s, g_s = sum g_dx * dxs + sum L_W^T(u * g_dd / d) * x
+                   g_W = wgrad(G, u) + wgrad(x * s, u * g_dd / d)
+    (reference: modulated_conv2d's up path, networks_stylegan2.py:66-76, through conv2d_resample.py:112-129)."""
+
+    @staticmethod
+    def forward(ctx, dy, x, styles, weight, dcoefs, y, c, f, need_x, need_s, need_d, alpha, gain, clamp, tpad,
+                t_hw, fpad):
+        n, cin, h, w = x.shape
+        kh, kw = weight.shape[2], weight.shape[3]
+        dt = x.dtype
+        d32, s32 = _f32(dcoefs), _f32(styles)
+        oh, ow = y.shape[2], y.shape[3]
+        aup, adown, apad, aflip = _up.adjoint_params(f, t_hw, (oh, ow), 1, 1, fpad, False)
+        dc, _, dd, _ = _cg.layer_bwd(dy.to(dt), y, c if need_d else None, d32, act=1, alpha=alpha, gain=gain,
+                                     clamp=clamp, want_db=False, want_dd=need_d, want_dnoise=False)
+        u = _up.upfirdn2d(dc, f, up=aup, down=adown, padding=apad, flip_filter=aflip, gain=4)
+        wT = _cg._pack_conv(weight.transpose(0, 1), dt)
+        if _cg._halo_s2_ok(u, kh, kw, 2, tpad, dot=need_s):
+            dx, dxs, ds = _cg.conv3x3_fused(u, wT, cin, out_scale=s32, dot_src=x if need_s else None, stride=2,
+                                            want_raw=True) + ((None,) if not need_s else ())
+        else:
+            res = _cg.conv_fused(u, wT, cin, h, w, kh, kw, 2, tpad, out_scale=s32, dot_src=x if need_s else None,
+                                 aux_mode=1)
+            dx, dxs, ds = res if need_s else res + (None,)
+        ctx.save_for_backward(x, styles, weight, dcoefs, y, c, f, dc, u, dxs)
+        ctx.cfg = (alpha, gain, clamp, tpad, t_hw, fpad)
+        return (dx if need_x else None, ds.to(styles.dtype) if need_s else None,
+                dd.to(dcoefs.dtype) if need_d else None)
+
+    @staticmethod
+    def backward(ctx, g_dx, g_ds, g_dd):
+        if torch.is_grad_enabled():
+            raise RuntimeError('_UpLayerVJP: third-order gradients are not supported (set modconv.fused_vjp = False)')
+        x, styles, weight, dcoefs, y, c, f, dc, u, dxs = ctx.saved_tensors
+        alpha, gain, clamp, tpad, (th, tw), fpad = ctx.cfg
+        need = ctx.needs_input_grad
+        n, cin, h, w = x.shape
+        cout, _, kh, kw = weight.shape
+        dt = x.dtype
+        d32, s32 = _f32(dcoefs), _f32(styles)
+        g_dy = g_x = g_s = g_w = g_d = None
+        G = None
+        if g_dx is not None:
+            G = _cg._nhwc(g_dx.to(dt) * styles.to(dt).reshape(n, -1, 1, 1))
+        if g_ds is not None:
+            t = x * g_ds.to(dt).reshape(n, -1, 1, 1)
+            G = t if G is None else G + t
+        hscale = (g_dd.float() / d32).contiguous() if g_dd is not None else None
+        if G is not None and (need[0] or need[4]):
+            tG, _ = _cg.conv_fused(G, _cg._pack_conv(weight, dt), cout, th, tw, kh, kw, 2, tpad, transpose=True)
+            A_d, _ = _up.fir_fused(tG, f, fpad, gain=4.0, out_scale=d32)
+            if need[4]:
+                g_d = (_cg.dot_hw(A_d, dc) / (d32 * d32)).to(dcoefs.dtype)
+            if need[0]:
+                gz = A_d if hscale is None else torch.addcmul(A_d, c, g_dd.to(dt).reshape(n, -1, 1, 1))
+                g_dy = _act_grad(gz, y, 1, alpha, gain, clamp)
+        elif need[0] and hscale is not None:
+            g_dy = _act_grad(c * g_dd.to(dt).reshape(n, -1, 1, 1), y, 1, alpha, gain, clamp)
+        wT = None
+        if need[1] or need[2]:
+            if g_ds is not None and need[1]:
+                g_x = dxs * g_ds.to(dt).reshape(n, -1, 1, 1)
+            if g_dx is not None and need[2]:
+                g_s = _cg.dot_hw(_cg._nhwc(g_dx.to(dt)), dxs)
+            if hscale is not None:
+                wT = _cg._pack_conv(weight.transpose(0, 1), dt)
+                dot_src = x if need[2] else None
+                if _cg._halo_s2_ok(u, kh, kw, 2, tpad, dot=need[2]):
+                    res = _cg.conv3x3_fused(u, wT, cin, in_scale=hscale, out_scale=s32, dot_src=dot_src, stride=2)
+                else:
+                    res = _cg.conv_fused(u, wT, cin, h, w, kh, kw, 2, tpad, in_scale=hscale, out_scale=s32,
+                                         dot_src=dot_src)
+                if need[1]:
+                    g_x = res[0] if g_x is None else g_x + res[0]
+                if need[2]:
+                    g_s = res[2] if g_s is None else g_s + res[2]
+        if need[3] and (G is not None or hscale is not None):
+            acc = torch.zeros([cin * kh * kw * cout], dtype=torch.float32, device=x.device)
+            if G is not None:
+                _cg._wgrad_raw(G, u, kh, kw, 2, tpad, out=acc)
+            if hscale is not None:
+                _cg._wgrad_raw(x, u, kh, kw, 2, tpad, g_scale=s32, x_scale=hscale, out=acc)
+            g_w = acc.view(cin, kh, kw, cout).permute(3, 0, 1, 2).to(weight.dtype)
+        g_s = g_s.to(styles.dtype) if g_s is not None else None
+        return (g_dy, g_x, g_s, g_w, g_d) + (None,) * 12
 
 
 def up_modconv_layer(x, styles, weight, dcoefs, noise, bias, f, alpha, gain, clamp):

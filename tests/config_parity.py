@@ -248,16 +248,20 @@ def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
     return worst, sorted(ratios)
 
 
-def judge_cond(got, fix, floors=F32_FLOORS, factor=4.0, groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True):
+def judge_cond(got, fix, floors=F32_FLOORS, factor=4.0, groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True,
+               rerun=None):
     """f32 results against the float64 answer, each tensor k held to its OWN conditioning (no phase-wide term):
 
-        err(got_k, f64) <= max(floor, factor * max(err(ref_k, f64), err(f64p_k, f64)))
+        err(got_k, f64) <= max(floor, factor * max(err(ref_k, f64), err(f64p_k, f64), err(got_k, rerun_k)))
 
     f64p is the float64 evaluation with the state and inputs nudged by half an f32 ulp (make_golden.py
     gen_conditioning): how far a rounding-sized change of the inputs moves tensor k, whatever evaluates it.
-    The reference's own f32 result is a second sample of that spread.  Returns ({group: (worst norm err,
-    worst sample err, worst bound, worst ratio to the bound, its tensor)}, [(ratio, tensor, bound n, bound s)])
-    and raises after computing everything when `check` and any tensor is out of bounds."""
+    The reference's own f32 result is a second sample of that spread.  rerun: the product's second run of the
+    same iteration (or a list of them) -- its float-atomic reductions sum in a different order each run, a rounding-sized change
+    INSIDE the evaluation, which the downstream conditioning amplifies as it does the input nudge (the reference
+    run on a GPU has the same: cuDNN's weight gradients accumulate with atomics too).  Returns ({group: (worst
+    norm err, worst sample err, worst bound, worst ratio to the bound, its tensor)}, [(ratio, tensor, bound n,
+    bound s)]) and raises after computing everything when `check` and any tensor is out of bounds."""
     truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
     cond = {k[5:]: v for k, v in fix.items() if k.startswith('f64p/')}
     assert cond, 'fixture has no f64p/ (conditioning) summaries'
@@ -269,6 +273,9 @@ def judge_cond(got, fix, floors=F32_FLOORS, factor=4.0, groups=('grad/', 'G1/', 
         gn, gs = _tensor_errs(got, truth, k)
         rn, rs_ = _tensor_errs(fix, truth, k)
         cn, cs = _tensor_errs(cond, truth, k) if k + '/norm' in cond else (0.0, 0.0)
+        for rr in (rerun if isinstance(rerun, (list, tuple)) else [rerun] if rerun is not None else []):
+            pn, ps = _tensor_errs(rr, got, k)
+            cn, cs = max(cn, pn), max(cs, ps)
         floor = floors['grad' if k.startswith('grad/') else 'param']
         bn, bs = max(floor[0], factor * max(rn, cn)), max(floor[1], factor * max(rs_, cs))
         ratio = max(gn / bn, gs / bs)
@@ -277,7 +284,8 @@ def judge_cond(got, fix, floors=F32_FLOORS, factor=4.0, groups=('grad/', 'G1/', 
         worst[g] = (max(w[0], gn), max(w[1], gs), max(w[2], bn), max(w[3], ratio), k if ratio > w[3] else w[4])
         rows.append((ratio, k, bn, bs))
         if gn > bn:
-            fails.append(f'{k}: norm err vs f64 {gn:.3g} > bound {bn:.3g} (reference f32 {rn:.3g}, conditioning {cn:.3g})')
+            fails.append(f'{k}: norm err vs f64 {gn:.3g} > bound {bn:.3g} (reference f32 {rn:.3g}, conditioning / '
+                         f'rerun {cn:.3g})')
         if gs > bs:
             fails.append(f'{k}: sampled-entry err vs f64 {gs:.3g} > bound {bs:.3g} (reference {rs_:.3g}, conditioning {cs:.3g})')
     if check:
@@ -285,10 +293,12 @@ def judge_cond(got, fix, floors=F32_FLOORS, factor=4.0, groups=('grad/', 'G1/', 
     return worst, sorted(rows, reverse=True)
 
 
-def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True):
+def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True,
+                       rerun=None):
     """Direct product-vs-reference-f32 check on every tensor the reference's f32 result gets right (both its
     norm and its sampled entries within `well` of the float64 answer): the product must then agree with the
-    reference itself to `tol` on both measures.  Returns (number of tensors checked, worst error, its key)."""
+    reference itself to `tol` (or 4x the product's own run-to-run difference on that tensor, when `rerun` is
+    given) on both measures.  Returns (number of tensors checked, worst error, its key)."""
     truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
     keys = sorted(set(_keys(truth, groups)) & set(_keys(got, groups)))
     n, worst, wk, fails = 0, 0.0, '', []
@@ -300,7 +310,9 @@ def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/', 'G1/', 'D
         en, es = _tensor_errs(got, fix, k)
         if max(en, es) > worst:
             worst, wk = max(en, es), k
-        if en > tol or es > tol:
+        reruns = rerun if isinstance(rerun, (list, tuple)) else [rerun] if rerun is not None else []
+        t = max([tol] + [4.0 * max(_tensor_errs(rr, got, k)) for rr in reruns])
+        if en > t or es > t:
             fails.append(f'{k}: vs reference f32 norm {en:.3g} samples {es:.3g} > {tol}')
     if check:
         assert not fails, f'{len(fails)} of {n} well-conditioned tensors differ from the reference: {fails[0]}'

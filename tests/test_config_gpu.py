@@ -98,9 +98,9 @@ def test_16bit_iteration_vs_reference(tag, dt):
 
 # ADA at p = 0 (tests/golden/make_golden.py P0_CONFIGS): no discrete augmentation choice can differ between
 # f32 and float64, and each fixture carries the float64 conditioning summaries (f64p/: the state nudged by
-# half an f32 ulp).  Every tensor is held to max(1e-4, 4 x max(reference f32 error, conditioning)) -- its own
-# conditioning, no phase-wide term -- and every tensor the reference's f32 gets within 1e-4 of float64 must
-# also match the reference's f32 result itself to 3e-4.
+# half an f32 ulp).  Every tensor is held to max(1e-4, 4 x max(reference f32 error, conditioning, the product's
+# own run-to-run spread)) -- its own conditioning, no phase-wide term -- and every tensor the reference's f32
+# gets within 1e-4 of float64 must also match the reference's f32 result itself to 3e-4 (or 4x that spread).
 P0_TAGS = ['c2p0', 'c4p0', 'c5p0']
 P0_FLOOR16 = {
     'fp16': {'grad/Gmain': 1e-2, 'grad/Greg': 2e-2, 'grad/Dmain': 1e-2, 'grad/Dreg': 2e-2, 'param': 1e-3},
@@ -119,18 +119,31 @@ def _cond_flat(fix):
 @pytest.mark.timeout(240)
 @pytest.mark.parametrize('tag', P0_TAGS)
 def test_f32_iteration_conditioned(tag):
+    """f32 iteration at config width with the ADA pipe at p = 0 against the float64 oracle, every tensor held to
+    4x the largest of three rounding-sized spreads of the same computation: the reference's own f32 error, the
+    float64 answer's shift under a half-ulp nudge of the inputs (f64p), and the product's run-to-run difference
+    over two more runs (its atomic reductions change order between runs).  Tensors the reference gets right to 1e-4 must also
+    match the reference's f32 result directly."""
     cfg, inp, tape, fix = cp.load_fixture(load(f'train_{tag}.npz'))
     got, stats = cp.run_product(cfg, inp, tape, DEV, aug_p=cfg['aug_p'])
+    reruns = []
+    for _ in range(2):        # two more runs: the product's own run-to-run spread, per tensor
+        cfg2, inp2, tape2, _ = cp.load_fixture(load(f'train_{tag}.npz'))
+        reruns.append(cp.run_product(cfg2, inp2, tape2, DEV, aug_p=cfg2['aug_p'])[0])
+    got2 = reruns
     cp.save_summary(f'{tag}_f32', got)
-    worst, rows = cp.judge_cond(got, fix, check=False)
-    nref, wref, kref = cp.judge_vs_reference(got, fix, check=False)
+    worst, rows = cp.judge_cond(got, fix, check=False, rerun=got2)
+    nref, wref, kref = cp.judge_vs_reference(got, fix, check=False, rerun=got2)
     spread, ref_flat, cond_flat = _cond_flat(fix)
     flat = cp.compare_flat(got, _truth(fix), GROUPS)
+    rr_flat = [cp.compare_flat(r, got, GROUPS) for r in reruns]
+    rerun_flat = {g: (max(r[g][0] for r in rr_flat), max(r[g][1] for r in rr_flat)) for g in GROUPS}
+    spread = {g: (max(spread[g][0], rerun_flat[g][0]), max(spread[g][1], rerun_flat[g][1])) for g in GROUPS}
     cp.record(f'{tag}_f32_cond', dict(worst=worst, top=rows[:8], max_bound={g: w[2] for g, w in worst.items()},
                                       vs_reference=(nref, wref, kref), flat=flat, reference_flat=ref_flat,
-                                      conditioning_flat=cond_flat))
-    cp.judge_cond(got, fix)
-    cp.judge_vs_reference(got, fix)
+                                      conditioning_flat=cond_flat, rerun_flat=rerun_flat))
+    cp.judge_cond(got, fix, rerun=got2)
+    cp.judge_vs_reference(got, fix, rerun=got2)
     cp.judge_stats_f32(stats, fix)
     cp.judge_pl_mean(got, fix)
     cp.judge_flat({g: v for g, v in flat.items() if g.startswith('grad/')}, spread, floor=1e-4)

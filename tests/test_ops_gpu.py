@@ -464,7 +464,8 @@ def test_fused_synthesis_layer_pl_pass(dtype, res):
     conv2d_gradfix.no_weight_gradients() (where the dgrad goes through _ScaledConvT, the demodulation scale
     on the operand staging), then the penalty's backward with weight gradients enabled (_ScaledConvT's
     backward: conv(G, W) * d with the dd dot epilogue, and the d-scaled wgrad).  Fused path vs the composed
-    one (x*s, conv, fma, bias_act kernels); 16-bit at 16^2 runs the halo kernels, f32 and 4^2 the generic."""
+    one (x*s, conv, fma, bias_act kernels) and against the fused layer's composed VJP (modconv.fused_vjp off);
+    16-bit at 16^2 runs the halo kernels, f32 and 4^2 the generic."""
     from training import networks_stylegan2 as net
     from torch_utils.ops import conv2d_gradfix, modconv
     torch.manual_seed(13)
@@ -478,8 +479,8 @@ def test_fused_synthesis_layer_pl_pass(dtype, res):
     pl = torch.randn(4, 48, res, res, device=DEV)
     params = [layer.weight, layer.bias, layer.noise_strength, layer.affine.weight, layer.affine.bias]
     out = []
-    for fused in [True, False]:
-        modconv.enabled = fused
+    for fused, vjp in [(True, True), (False, False), (True, False)]:
+        modconv.enabled, modconv.fused_vjp = fused, vjp
         x = x0.clone().requires_grad_(True)
         wv = w0.clone().requires_grad_(True)
         orig = torch.randn
@@ -492,15 +493,16 @@ def test_fused_synthesis_layer_pl_pass(dtype, res):
             g_w, = torch.autograd.grad((y.float() * pl).sum(), [wv], create_graph=True)
         g2 = torch.autograd.grad(g_w.square().sum(), params + [x, wv], allow_unused=True)
         out.append((g_w.float(), [g if g is None else g.float() for g in g2]))
-    modconv.enabled = True
+    modconv.enabled, modconv.fused_vjp = True, True
     tol = {torch.float16: 2e-2, torch.bfloat16: 5e-2, torch.float32: 1e-4}[dtype]
-    (gw1, g21), (gw2, g22) = out
-    assert rel_err(gw1, gw2) < tol
-    for a_, b_ in zip(g21, g22):
-        if b_ is None:
-            continue
-        assert a_ is not None
-        assert rel_err(a_, b_) < 4 * tol
+    # the fused VJP node (_LayerVJP) against the unfused layer, and against the fused layer's composed VJP
+    for (gw1, g21), (gw2, g22) in [(out[0], out[1]), (out[0], out[2])]:
+        assert rel_err(gw1, gw2) < tol
+        for a_, b_ in zip(g21, g22):
+            if b_ is None:
+                continue
+            assert a_ is not None
+            assert rel_err(a_, b_) < 4 * tol
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
@@ -586,12 +588,16 @@ def test_conv3x3_dot_and_scaled_wgrad(dtype, shape):
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
-def test_fused_d_conv_layer_matches_composed(dtype):
+@pytest.mark.parametrize('r1_pass', [False, True])
+def test_fused_d_conv_layer_matches_composed(dtype, r1_pass):
     """Discriminator 3x3 Conv2dLayer (bias + lrelu + clamp) through one sg2_conv3x3 launch and the fused
     backward vs the composed path (conv kernel + bias_act kernel): output, input/param grads and the
-    R1-style second-order grads."""
+    R1-style second-order grads.  r1_pass: the create_graph gradient under no_weight_gradients, as loss.py's
+    R1 term runs it (reference loss.py:125), which takes the fused VJP node (modconv._LayerVJP)."""
+    import contextlib
     from training import networks_stylegan2 as net
-    from torch_utils.ops import modconv
+    from torch_utils.ops import conv2d_gradfix, modconv
+    ctx = conv2d_gradfix.no_weight_gradients if r1_pass else contextlib.nullcontext
     torch.manual_seed(13)
     layer = net.Conv2dLayer(32, 48, kernel_size=3, activation='lrelu', conv_clamp=256).to(DEV)
     with torch.no_grad():
@@ -604,7 +610,8 @@ def test_fused_d_conv_layer_matches_composed(dtype):
         modconv.enabled = fused
         x = x0.clone().requires_grad_(True)
         y = layer(x, gain=np.sqrt(0.5))
-        gx, = torch.autograd.grad((y.float() * dy).sum(), [x], create_graph=True)
+        with ctx():
+            gx, = torch.autograd.grad((y.float() * dy).sum(), [x], create_graph=True)
         g2 = torch.autograd.grad(gx.float().square().sum(), params)
         y = layer(x)
         g1 = torch.autograd.grad((y.float() * dy).sum(), [x] + params)
@@ -1281,16 +1288,22 @@ def test_fused_conv_wgain_weight_grad(mode):
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize('shape', [(4, 256, 256), (11, 48, 256), (13, 40, 256), (3, 64, 704)])
 @pytest.mark.parametrize('form', ['mod_epi_raw', 'mod_epi', 'mod_only', 'plain_epi', 'plain', 'epi_no_noise'])
-def test_conv3x3_c64_ring(dtype, shape, form):
-    """The 64 -> 64 channel ring kernel (LDS-DMA halo ring, weights in registers modulated per sample, staggered
-    epilogue; conv3x3.hip conv3x3_c64r_kernel) in every form the layers use -- the synthesis forward (modulation,
-    demod, noise, bias, lrelu, clamp, raw output), the path-length pass's scaled transposed conv (modulation only),
-    the D conv (bias + lrelu + clamp), a plain conv -- against float64.  Shapes cover bands of 4 / 2 / 1 tile rows,
-    runs that cross samples (the per-sample weight re-modulation) and image borders on every side."""
+@pytest.mark.parametrize('ring', ['4', '8'])
+def test_conv3x3_c64_ring(dtype, shape, form, ring, monkeypatch):
+    """The 64 -> 64 channel ring kernel (LDS-DMA halo ring, weights in registers modulated per sample;
+    conv3x3.hip conv3x3_c64r_kernel) in both forms (ring 4: two workgroups per CU on 32 x 4 tiles, 2-slot rings;
+    ring 8: one workgroup on 32 x 8 tiles, 3-slot ring) and every form the layers use -- the synthesis forward
+    (modulation, demod, noise, bias, lrelu, clamp, raw output), the path-length pass's scaled transposed conv
+    (modulation only), the D conv (bias + lrelu + clamp), a plain conv -- against float64.  Shapes cover bands of
+    4 / 2 / 1 tile rows, runs that cross samples (the per-sample weight re-modulation) and image borders on every
+    side."""
     from torch_utils.ops import conv2d_gradfix as cg
+    monkeypatch.setenv('SG2_C64_RING', ring)
     N, H, W = shape
     C = 64
-    assert N * (H // 8) * (W // 32) >= 512          # the ring kernel's minimum of two tiles per CU
+    th = int(ring)
+    wgs = (2 if th == 4 else 1) * torch.cuda.get_device_properties(DEV).multi_processor_count
+    assert N * (H // th) * (W // 32) >= 2 * wgs      # the ring kernel's minimum of two tiles per workgroup
     torch.manual_seed(17)
     x = torch.randn(N, C, H, W)
     w = torch.randn(C, C, 3, 3) / np.sqrt(C * 9)

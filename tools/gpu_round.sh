@@ -62,6 +62,18 @@ if step diag; then
         -d "$O/diag" -o run --output-format csv -- python3 "$R/tools/conv_micro.py" --reps 3 > "$O/diag.log" 2>&1
     rc=$?; tail -5 "$O/diag.log"; [ $rc -eq 0 ] || exit $rc
 fi
+if step mem; then
+    echo "== memory-path microbenchmarks"
+    (cd "$R" && timeout -k 10 120 python -u tools/membench.py > "$O/mem.log" 2>&1)
+    rc=$?; grep -v amdgpu.ids "$O/mem.log"; [ $rc -eq 0 ] || exit $rc
+fi
+if step trace; then
+    echo "== kernel trace of the iteration's parts and loss phases"
+    timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/tr" -o run --output-format csv \
+        -- python3 "$R/tools/trace_parts.py" > "$O/trace.log" 2>&1
+    rc=$?; tail -1 "$O/trace.log"; [ $rc -eq 0 ] || exit $rc
+    python3 "$R/tools/trace_report.py" "$O/tr" 30 > "$O/trace_report.txt" 2>&1; grep "===" "$O/trace_report.txt"
+fi
 if step micro; then
     echo "== conv micro"
     (cd "$R" && timeout -k 10 300 python -u tools/conv_micro.py > "$O/micro.log" 2>&1)

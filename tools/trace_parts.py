@@ -1,7 +1,7 @@
 """Run each part of one training iteration once, separated by idle gaps, for a rocprofv3 kernel trace:
     rocprofv3 --kernel-trace -d gpurun_out/tr -o run --output-format csv -- python tools/trace_parts.py
     python tools/trace_report.py gpurun_out/tr
-Parts: synthesis fwd, D fwd, G fwd+bwd, D fwd+bwd (aug), Greg-like PL pass, Dreg-like R1 pass."""
+Parts: synthesis fwd, D fwd, G fwd+bwd, D fwd+bwd (aug), then the loss phases Gmain, Greg, Dmain, Dreg (eager)."""
 import os
 import sys
 import time
@@ -61,7 +61,24 @@ def dfb():
     D.requires_grad_(False)
 
 
+real = torch.rand([32, 1, 256, 256], device=dev) * 2 - 1
+
+
+def phase(name):
+    # one phase's loss gradients exactly as the trainer runs them (eager; no optimizer step)
+    def run():
+        mod = G if name.startswith('G') else D
+        mod.requires_grad_(True)
+        tr.loss.accumulate_gradients(phase=name, real_img=real, real_c=c, gen_z=z, gen_c=c, gain=1, cur_nimg=0)
+        mod.requires_grad_(False)
+        for p in mod.parameters():
+            p.grad = None
+    return run
+
+
 part('synthesis_fwd', syn)
 part('D_fwd', dfwd)
 part('G_fwd_bwd', gfb)
 part('augD_fwd_bwd', dfb)
+for ph in (sys.argv[1:] or ['Gmain', 'Greg', 'Dmain', 'Dreg']):
+    part(ph, phase(ph))

@@ -20,7 +20,7 @@ for r in rows:
     last = int(r['End_Timestamp'])
 parts.append(cur)
 # each part is run 3x (2 warm + 1 traced) with sleeps around the traced run: keep sections after gaps
-names = ['synthesis_fwd', 'D_fwd', 'G_fwd_bwd', 'augD_fwd_bwd']
+names = ['synthesis_fwd', 'D_fwd', 'G_fwd_bwd', 'augD_fwd_bwd', 'Gmain', 'Greg', 'Dmain', 'Dreg']
 sections = [p for p in parts if p]
 print(f'{len(sections)} sections')
 
@@ -31,9 +31,10 @@ def short(n):
 
 
 for i, sec in enumerate(sections):
+    label = names[i] if len(sections) == len(names) else str(i)
     tot = sum(int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in sec)
     span = int(sec[-1]['End_Timestamp']) - int(sec[0]['Start_Timestamp'])
-    print(f'\n=== section {i}: {len(sec)} kernels, busy {tot / 1e6:.2f} ms, span {span / 1e6:.2f} ms')
+    print(f'\n=== section {i} {label}: {len(sec)} kernels, busy {tot / 1e6:.2f} ms, span {span / 1e6:.2f} ms')
     agg = defaultdict(lambda: [0, 0])
     for r in sec:
         k = short(r['Kernel_Name'])
