@@ -714,8 +714,8 @@ constexpr int R_EPI = 1024, R_NEPI = 4;               // noise [TH x 32] T at 0,
 // workgroup meet at one barrier per tile, so in the one-workgroup form a SIMD's two waves reach their MFMA,
 // epilogue and barrier phases together; two workgroups drift apart and one's MFMAs run beside the other's
 // epilogue, stores and barrier wait.
-template <int TH> struct Ring {
-    static constexpr int NW = TH;                                     // waves: 2 channel halves x TH / 2 row pairs
+template <int TH, int WR> struct Ring {
+    static constexpr int NW = 2 * TH / WR;                            // waves: 2 channel halves x TH / WR row groups
     static constexpr int NSLOT = TH == 8 ? 3 : 2;
     static constexpr int HPOS = (TH + 2) * R_PITCH;                   // halo positions (34 used per row)
     static constexpr int SLOT = HPOS * 128;                           // 51,200 / 30,720 B
@@ -730,7 +730,8 @@ template <int TH> struct Ring {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 #ifndef SG2_RDIAG
 #define SG2_RDIAG 0         // timing-only builds of the ring kernel (tools/ring_diag.sh): 16 no loads, 32 no stores, 64 no MFMA
-                            // (128: the pad lanes load the pixels that follow, the round-3 first form)
+                            // (128: the pad lanes load the pixels that follow, the round-3 first form;
+                            //  256: whole-line store addressing with the data misplaced)
 #endif
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {    // byte address in LDS of a __shared__ pointer
@@ -743,12 +744,13 @@ __device__ __forceinline__ void wait_vm() {           // s_waitcnt vmcnt(N) (gfx
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <typename T, bool SI, bool EPI, bool RAW, int R_TH>
-__global__ __launch_bounds__(Ring<R_TH>::NW * 64, Ring<R_TH>::WGS_PER_CU) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band) {
+template <typename T, bool SI, bool EPI, bool RAW, int R_TH, int WR, bool PIPE, bool STG>
+__global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER_CU)) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
-    typedef Ring<R_TH> RG;
+    typedef Ring<R_TH, WR> RG;
+    constexpr int NF = 2 * WR;                        // pixel fragments (16 px) per wave
     constexpr int R_NSLOT = RG::NSLOT, R_SLOT = RG::SLOT, R_HALO_I = RG::HALO_I, R_DMA = RG::DMA, NW = RG::NW;
-    constexpr int S = RAW ? 8 : 4;                    // buffer stores per wave and tile
+    constexpr int S = (RAW ? 2 : 1) * 2 * WR;         // buffer stores per wave and tile
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     char* epil = smem_raw + R_NSLOT * R_SLOT;
     float* blds = (float*)(epil + R_NEPI * R_EPI);
@@ -756,7 +758,7 @@ __global__ __launch_bounds__(Ring<R_TH>::NW * 64, Ring<R_TH>::WGS_PER_CU) void c
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l16 = lane & 15, q = lane >> 4;
-    const int h = wave & 1, wr = wave >> 1;           // channel half, tile row pair
+    const int h = wave & 1, wr = wave >> 1;           // channel half, tile row group (rows WR wr .. + WR - 1)
     const int t_begin = (int)((int64_t)blockIdx.x * tiles_total / gridDim.x);
     const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles_total / gridDim.x);
     if (t_begin >= t_end) return;
@@ -879,72 +881,153 @@ __global__ __launch_bounds__(Ring<R_TH>::NW * 64, Ring<R_TH>::WGS_PER_CU) void c
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int x = l16 + kx;
-            boff[kx][c] = (2 * wr * R_PITCH + x) * 128 + 16 * ((c * 4 + q) ^ (((x >> 1) & 3) << 1));
+            boff[kx][c] = (WR * wr * R_PITCH + x) * 128 + 16 * ((c * 4 + q) ^ (((x >> 1) & 3) << 1));
         }
 
-    f32x4 acc[4][2];
     const float lr_alpha = (EPI && a.act == 1) ? a.alpha : 1.f;
     const float clampv = (EPI && a.clamp >= 0.f) ? a.clamp : __builtin_inff();
     const float ngain = a.noise_gain * a.gain;
     const int ch0 = 32 * h + 8 * q;                   // this lane's 8 output channels
 
-    auto epilogue = [&](int t, int eslot) {
-        int n, ty, tx;
-        tile_of(t, n, ty, tx);
-        // The tables are read by inline-asm ds_reads: an LDS-DMA writes this ring, so hipcc would put an
-        // s_waitcnt vmcnt(0) before any ds_read it can see here, draining the two tiles in flight.  The ring
-        // discipline (the DMA of tile t was waited for and a barrier passed) is what orders these reads.
+    // The epilogue tables are read by inline-asm ds_reads: an LDS-DMA writes this ring, so hipcc would put an
+    // s_waitcnt vmcnt(0) before any ds_read it can see here, draining the tiles in flight.  The ring discipline
+    // (the DMA of the tile was waited for and a barrier passed) is what orders these reads.  Branch-free: a
+    // missing noise / demod table is read anyway (its DMA read a stand-in buffer) and selected away.
+    auto epi_table = [&](int eslot, float (&bb)[8], float (&dd)[8], float (&nz)[NF]) {
+        if (!EPI) return;
         const unsigned et = lds_addr(epil + eslot * R_EPI);
-        float bb[8], dd[8], nz[4];
-        if (EPI) {
-            float4 b0, b1, d0, d1;
-            asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
-                         "ds_read_b128 %2, %5 offset:512\n\tds_read_b128 %3, %5 offset:528\n\ts_waitcnt lgkmcnt(0)"
-                         : "=&v"(b0), "=&v"(b1), "=&v"(d0), "=&v"(d1)
-                         : "v"(lds_addr(blds + ch0)), "v"(et + ch0 * 4));
-            bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
-            if (has_d) {
-                dd[0] = d0.x; dd[1] = d0.y; dd[2] = d0.z; dd[3] = d0.w; dd[4] = d1.x; dd[5] = d1.y; dd[6] = d1.z; dd[7] = d1.w;
+        float4 b0, b1, d0, d1;
+        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
+                     "ds_read_b128 %2, %5 offset:512\n\tds_read_b128 %3, %5 offset:528\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(b0), "=&v"(b1), "=&v"(d0), "=&v"(d1)
+                     : "v"(lds_addr(blds + ch0)), "v"(et + ch0 * 4));
+        const float bq[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        const float dq[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
 #pragma unroll
-                for (int e = 0; e < 8; ++e) dd[e] *= a.gain;
-            } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) dd[e] = a.gain;
-            }
-            if (has_noise) {
-                unsigned r0, r1, r2, r3;             // pixel (2 wr + (i >> 1)) * 32 + (i & 1) * 16 + l16 of the table
-                const unsigned na = et + (2 * wr * R_TW + l16) * (unsigned)sizeof(T);
-                asm volatile("ds_read_u16 %0, %4\n\tds_read_u16 %1, %4 offset:32\n\tds_read_u16 %2, %4 offset:64\n\t"
-                             "ds_read_u16 %3, %4 offset:96\n\ts_waitcnt lgkmcnt(0)"
-                             : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3) : "v"(na));
-                nz[0] = (float)__builtin_bit_cast(T, (unsigned short)r0) * ngain;
-                nz[1] = (float)__builtin_bit_cast(T, (unsigned short)r1) * ngain;
-                nz[2] = (float)__builtin_bit_cast(T, (unsigned short)r2) * ngain;
-                nz[3] = (float)__builtin_bit_cast(T, (unsigned short)r3) * ngain;
-            }
+        for (int e = 0; e < 8; ++e) {
+            bb[e] = bq[e];
+            dd[e] = has_d ? dq[e] * a.gain : a.gain;
         }
+        // pixel (WR wr + (i >> 1)) * 32 + (i & 1) * 16 + l16 of the table: byte offset 32 i from na
+        const unsigned na = et + (WR * wr * R_TW + l16) * (unsigned)sizeof(T);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = 2 * wr + (i >> 1), px = (i & 1) * 16 + l16;
+        for (int g = 0; g < NF / 4; ++g) {
+            unsigned r0, r1, r2, r3;
+            asm volatile("ds_read_u16 %0, %4\n\tds_read_u16 %1, %4 offset:32\n\tds_read_u16 %2, %4 offset:64\n\t"
+                         "ds_read_u16 %3, %4 offset:96\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3) : "v"(na + 128 * g));
+            const unsigned rr[4] = {r0, r1, r2, r3};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                nz[4 * g + j] = has_noise ? (float)__builtin_bit_cast(T, (unsigned short)rr[j]) * ngain : 0.f;
+        }
+    };
+    // the epilogue math and stores of one tile from its accumulators: pure VALU + buffer stores, no branch, so
+    // in the pipelined form it shares a basic block (and the scheduler's interleave) with the next tile's MFMAs
+    auto epi_store = [&](f32x4 (&A)[NF][2], int n, int ty, int tx, const float (&bb)[8], const float (&dd)[8],
+                         const float (&nz)[NF]) {
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int r = WR * wr + (i >> 1), px = (i & 1) * 16 + l16;
             const int pix = (n * a.H + ty + r) * a.W + tx + px;
-            const float nv = has_noise ? nz[i] : 0.f;
             vec8 yv, rv;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                const float cv = acc[i][e >> 2][e & 3];
+                const float cv = A[i][e >> 2][e & 3];
                 if (RAW) rv[e] = (T)cv;
                 float v = cv;
                 if (EPI) {
-                    v = fmaf(v, dd[e], nv + bb[e]);
+                    v = fmaf(v, dd[e], nz[i] + bb[e]);
                     v = fmaxf(v, v * lr_alpha);
                     v = __builtin_amdgcn_fmed3f(v, -clampv, clampv);
                 }
                 yv[e] = (T)v;
             }
-            const int dst = (pix * 64 + ch0) * (int)sizeof(T) | -(int)((SG2_RDIAG & 32) != 0);   // timing-only build: dropped
+            int dst = (pix * 64 + ch0) * (int)sizeof(T) | -(int)((SG2_RDIAG & 32) != 0);   // timing-only build: dropped
+            if (SG2_RDIAG & 256)   // timing-only build: the same bytes as whole-line stores (8 px x 128 B an instruction)
+                dst = (((n * a.H + ty + WR * wr + h) * a.W + tx + i * 8 + (lane >> 3)) * 64 + (lane & 7) * 8) * (int)sizeof(T);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, dst, 0, 0);
             if (RAW) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, dst, 0, 0);
         }
+    };
+    // STG: the same epilogue with whole-line stores.  The tile's outputs go through the slot its MFMAs just
+    // consumed (free until the next iteration's DMA into it, which follows the loop's last barrier): each wave
+    // writes its 16-byte pieces (8 channels of a pixel) into a [128 px][128 B] image, piece c of pixel P at
+    // c ^ (P & 7) (conflict-free ds_write_b128 and ds_read_b128), then reads back whole 128-byte pixel lines, 8
+    // pixels per wave-instruction, and stores those.  Measured with a timing build (RDIAG 256): the half-line
+    // stores' texture-address cost beside the halo DMAs was 11 % of the launch.  Two more barriers (four with
+    // the raw output, staged in a second round).
+    auto epi_store_staged = [&](f32x4 (&A)[NF][2], int slot, int n, int ty, int tx, const float (&bb)[8],
+                                const float (&dd)[8], const float (&nz)[NF]) {
+        if constexpr (WR == 2) {                      // (staged stores: two rows per wave pair)
+        const unsigned sb = lds_addr(smem_raw + slot * R_SLOT);
+        u32x4 yq[NF], rq[NF];
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            vec8 yv, rv;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float cv = A[i][e >> 2][e & 3];
+                if (RAW) rv[e] = (T)cv;
+                float v = cv;
+                if (EPI) {
+                    v = fmaf(v, dd[e], nz[i] + bb[e]);
+                    v = fmaxf(v, v * lr_alpha);
+                    v = __builtin_amdgcn_fmed3f(v, -clampv, clampv);
+                }
+                yv[e] = (T)v;
+            }
+            yq[i] = __builtin_bit_cast(u32x4, yv);
+            rq[i] = __builtin_bit_cast(u32x4, rv);
+        }
+        auto stage_store = [&](const u32x4 (&v)[NF], const __amdgpu_buffer_rsrc_t& rout) {
+#pragma unroll
+            for (int i = 0; i < NF; ++i) {
+                const int P = (2 * wr + (i >> 1)) * R_TW + (i & 1) * 16 + l16;
+                const unsigned off = sb + P * 128 + (((4 * h + q) ^ (P & 7)) << 4);
+                asm volatile("ds_write_b128 %0, %1" :: "v"(off), "v"(v[i]) : "memory");
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_s_barrier();
+            const int c = lane & 7, row = 2 * wr + h;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int px = 8 * j + (lane >> 3), P = row * R_TW + px;
+                u32x4 w;
+                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(w) : "v"(sb + P * 128 + ((c ^ (P & 7)) << 4)));
+                const int pix = (n * a.H + ty + row) * a.W + tx + px;
+                __builtin_amdgcn_raw_buffer_store_b128(w, rout, (pix * 64 + c * 8) * (int)sizeof(T), 0, 0);
+            }
+        };
+        __builtin_amdgcn_s_waitcnt(0xc07f);           // every wave is done reading the slot's halo
+        __builtin_amdgcn_s_barrier();
+        stage_store(yq, ryb);
+        if (RAW) {
+            __builtin_amdgcn_s_barrier();             // the y image has been read back
+            stage_store(rq, ryr);
+        }
+        }
+    };
+    auto mfma_tile = [&](f32x4 (&A)[NF][2], const char* hb) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    v8<T> pf[NF];
+#pragma unroll
+                    for (int i = 0; i < NF; ++i)
+                        pf[i] = *(const v8<T>*)(hb + boff[kx][c] + (((i >> 1) + ky) * R_PITCH + (i & 1) * 16) * 128);
+                    const bool first = c == 0 && ky == 0 && kx == 0;   // the tile's first tap starts each chain at 0
+#pragma unroll
+                    for (int i = 0; i < NF; ++i)
+#pragma unroll
+                        for (int jj = 0; jj < 2; ++jj) {
+                            if (SG2_RDIAG & 64) A[i][jj][0] = (first ? 0.f : A[i][jj][0]) + (float)pf[i][jj] * (float)wf[jj][ky * 3 + kx][c][i];   // timing-only build
+                            else A[i][jj] = mma<T>(wf[jj][ky * 3 + kx][c], pf[i], first ? f32x4{0.f, 0.f, 0.f, 0.f} : A[i][jj]);
+                        }
+                }
     };
 
     // ---- prologue: tiles 0 .. NSLOT - 2 in flight, wait for tile 0 ----
@@ -959,73 +1042,115 @@ __global__ __launch_bounds__(Ring<R_TH>::NW * 64, Ring<R_TH>::WGS_PER_CU) void c
     __builtin_amdgcn_s_barrier();
 
     int k = 0;
-    for (int t = t_begin; t < t_end; ++t, ++k) {
-        const int slot = k % R_NSLOT;
-        issue(min(t + R_NSLOT - 1, t_end - 1), (k + R_NSLOT - 1) % R_NSLOT, (k + R_NSLOT - 1) % R_NEPI);
-        int n, ty, tx;
-        tile_of(t, n, ty, tx);
-        if (SI && n != cur_n) {                       // a new sample: re-modulate the weights (rare)
-            cur_n = n;
-            load_weights(n);
+    if constexpr (!PIPE) {
+        f32x4 acc[NF][2];
+        for (int t = t_begin; t < t_end; ++t, ++k) {
+            const int slot = k % R_NSLOT;
+            issue(min(t + R_NSLOT - 1, t_end - 1), (k + R_NSLOT - 1) % R_NSLOT, (k + R_NSLOT - 1) % R_NEPI);
+            int n, ty, tx;
+            tile_of(t, n, ty, tx);
+            if (SI && n != cur_n) {                   // a new sample: re-modulate the weights (rare)
+                cur_n = n;
+                load_weights(n);
+            }
+            mfma_tile(acc, smem_raw + slot * R_SLOT);
+            float bb[8], dd[8], nz[NF];
+            epi_table(k % R_NEPI, bb, dd, nz);
+            if constexpr (STG) epi_store_staged(acc, slot, n, ty, tx, bb, dd, nz);
+            else epi_store(acc, n, ty, tx, bb, dd, nz);
+            // tile t + 1's DMAs must have landed: everything but the youngest ops of this wave.  3 slots: t + 1
+            // was issued one iteration ago, younger are this iteration's DMAs and stores and the previous
+            // iteration's stores; 2 slots: t + 1 was issued at the top of this iteration, younger are this
+            // iteration's stores
+            if (R_NSLOT == 2) wait_vm<S>();
+            else if (k == 0) wait_vm<R_DMA + S>();
+            else wait_vm<R_DMA + 2 * S>();
+            __builtin_amdgcn_s_waitcnt(0xc07f);       // lgkmcnt(0): this tile's LDS reads are done
+            __builtin_amdgcn_s_barrier();
         }
-        const char* hb = smem_raw + slot * R_SLOT;
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < 3; ++kx) {
-                    v8<T> pf[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        pf[i] = *(const v8<T>*)(hb + boff[kx][c] + (((i >> 1) + ky) * R_PITCH + (i & 1) * 16) * 128);
-                    const bool first = c == 0 && ky == 0 && kx == 0;   // the tile's first tap starts each chain at 0
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int jj = 0; jj < 2; ++jj) {
-                            if (SG2_RDIAG & 64) acc[i][jj][0] = (first ? 0.f : acc[i][jj][0]) + (float)pf[i][jj] * (float)wf[jj][ky * 3 + kx][c][i];   // timing-only build
-                            else acc[i][jj] = mma<T>(wf[jj][ky * 3 + kx][c], pf[i], first ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][jj]);
-                        }
-                }
-        epilogue(t, k % R_NEPI);
-        // tile t + 1's DMAs must have landed: everything but the youngest ops of this wave.  3 slots: t + 1 was
-        // issued one iteration ago, younger are this iteration's DMAs and stores and the previous iteration's
-        // stores; 2 slots: t + 1 was issued at the top of this iteration, younger are this iteration's stores
-        if (R_NSLOT == 2) wait_vm<S>();
-        else if (k == 0) wait_vm<R_DMA + S>();
-        else wait_vm<R_DMA + 2 * S>();
-        __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): this tile's LDS reads are done
-        __builtin_amdgcn_s_barrier();
+    } else {
+        // Pipelined epilogue (3-slot form): iteration k runs tile k's MFMAs into one accumulator set and tile
+        // k - 1's epilogue from the other in the same basic block, so the epilogue's VALU and stores issue
+        // between MFMAs instead of after them.  The epilogue table of tile k - 1 (its epilogue-ring slot is
+        // rewritten three iterations later) is read at the top of the iteration.
+        static_assert(!PIPE || R_NSLOT == 3, "pipelined epilogue: 3-slot ring");
+        f32x4 acc0[NF][2], acc1[NF][2];
+        int t = t_begin, pn = 0, pty = 0, ptx = 0;
+        auto step = [&](auto has_prev, f32x4 (&Acur)[NF][2], f32x4 (&Aprev)[NF][2]) {
+            constexpr bool HP = decltype(has_prev)::value;
+            const int slot = k % R_NSLOT;
+            issue(min(t + R_NSLOT - 1, t_end - 1), (k + R_NSLOT - 1) % R_NSLOT, (k + R_NSLOT - 1) % R_NEPI);
+            int n, ty, tx;
+            tile_of(t, n, ty, tx);
+            if (SI && n != cur_n) {
+                cur_n = n;
+                load_weights(n);
+            }
+            float bb[8], dd[8], nz[NF];
+            if (HP) epi_table((k + R_NEPI - 1) % R_NEPI, bb, dd, nz);
+            mfma_tile(Acur, smem_raw + slot * R_SLOT);
+            if (HP) epi_store(Aprev, pn, pty, ptx, bb, dd, nz);
+            // tile t + 1's DMAs (issued one iteration ago) must have landed; younger: the stores of the previous
+            // iteration (none at k = 1), this iteration's DMAs and its stores (none at k = 0)
+            if (k == 0) wait_vm<R_DMA>();
+            else if (k == 1) wait_vm<R_DMA + S>();
+            else wait_vm<R_DMA + 2 * S>();
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_s_barrier();
+            pn = n; pty = ty; ptx = tx;
+            ++k; ++t;
+        };
+        step(std::false_type{}, acc0, acc1);
+        bool last0 = true;                            // which set holds the last tile's sums
+        while (t < t_end) {
+            step(std::true_type{}, acc1, acc0);
+            last0 = false;
+            if (t >= t_end) break;
+            step(std::true_type{}, acc0, acc1);
+            last0 = true;
+        }
+        float bb[8], dd[8], nz[NF];
+        epi_table((k + R_NEPI - 1) % R_NEPI, bb, dd, nz);
+        if (last0) epi_store(acc0, pn, pty, ptx, bb, dd, nz);
+        else epi_store(acc1, pn, pty, ptx, bb, dd, nz);
     }
     wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
 }
 
-template <typename T, bool SI, bool EPI, bool RAW, int TH>
+template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, bool STG>
 int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
-    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW, TH>;
+    typedef Ring<TH, WR> RG;
+    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW, TH, WR, PIPE, STG>;
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)Ring<TH>::LDS);
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RG::LDS);
         attr_set = true;
     }
-    kern<<<grid, Ring<TH>::NW * 64, Ring<TH>::LDS, s>>>(a, tiles, band);
+    kern<<<grid, RG::NW * 64, RG::LDS, s>>>(a, tiles, band);
     return launch_status("sg2_conv3x3 (c64 ring)");
 }
 
-template <typename T, bool SI, bool EPI, int TH>
+template <typename T, bool SI, bool EPI, int TH, int WR, bool PIPE = false, bool STG = false>
 int launch_c64r_raw(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
-    return a.y_raw ? launch_c64r<T, SI, EPI, true, TH>(a, s, tiles, grid, band)
-                   : launch_c64r<T, SI, EPI, false, TH>(a, s, tiles, grid, band);
+    return a.y_raw ? launch_c64r<T, SI, EPI, true, TH, WR, PIPE, STG>(a, s, tiles, grid, band)
+                   : launch_c64r<T, SI, EPI, false, TH, WR, PIPE, STG>(a, s, tiles, grid, band);
 }
 
+// form: 4 = 32 x 4 tiles, two workgroups of 4 waves per CU; 8 = 32 x 8 tiles, one workgroup of 8 waves;
+// 44 = form 4 with whole-line stores staged through the consumed slot; 84 = 32 x 8 tiles, one workgroup of 4
+// waves with 4 rows each (one wave per SIMD, 512 registers).  (The PIPE
+// template form -- tile k - 1's epilogue beside tile k's MFMAs -- spills at 512 registers with the weights in
+// VGPRs and is not instantiated.)
 template <typename T, bool SI, bool EPI>
-int launch_c64r_th(const Conv3Args& a, hipStream_t s, int th) {
+int launch_c64r_form(const Conv3Args& a, hipStream_t s, int form) {
+    const int th = (form == 4 || form == 44) ? 4 : 8;
     const int tiles = a.N * (a.H / th) * (a.W / R_TW);
     const int ty = a.H / th;
     const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
-    if (th == 4) return launch_c64r_raw<T, SI, EPI, 4>(a, s, tiles, 2 * num_cus(), band);
-    return launch_c64r_raw<T, SI, EPI, 8>(a, s, tiles, num_cus(), band);
+    if (form == 4) return launch_c64r_raw<T, SI, EPI, 4, 2>(a, s, tiles, 2 * num_cus(), band);
+    if (form == 44) return launch_c64r_raw<T, SI, EPI, 4, 2, false, true>(a, s, tiles, 2 * num_cus(), band);
+    if (form == 84) return launch_c64r_raw<T, SI, EPI, 8, 4>(a, s, tiles, num_cus(), band);
+    return launch_c64r_raw<T, SI, EPI, 8, 2>(a, s, tiles, num_cus(), band);
 }
 
 template <typename T>
@@ -1044,10 +1169,10 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         return launch3<T, 32, false, false, 1, 2>(a, s);
     }
     static const bool persist = [] { const char* e = getenv("SG2_HALO_PERSIST"); return !e || atoi(e) != 0; }();
-    // SG2_C64_RING: 0 off, 8 the one-workgroup 32 x 8 form, 4 (default) the two-workgroup 32 x 4 form
+    // SG2_C64_RING: 0 off, else the ring form (launch_c64r_form: 4 default, 8, 84)
     const char* ring_env = getenv("SG2_C64_RING");   // read per launch: tests switch forms in one process
     const int ring = ring_env ? atoi(ring_env) : 4;
-    const int rth = ring == 8 ? 8 : 4;
+    const int rth = (ring == 4 || ring == 44) ? 4 : 8;
     if (ring && !a.dot_out && a.Cin == P_C && a.Cout == P_C && a.H % rth == 0 && a.W % R_TW == 0 &&
         ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 && ((uintptr_t)a.noise % 16) == 0 &&
         ((uintptr_t)a.out_scale % 16) == 0 && ((uintptr_t)a.in_scale % 16) == 0 &&
@@ -1055,9 +1180,10 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         const int tiles = a.N * (a.H / rth) * (a.W / R_TW);
         const int grid = (rth == 4 ? 2 : 1) * num_cus();
         if (tiles >= 2 * grid && tiles <= 128 * grid && a.N < 4096 && a.H / rth < 1024 && a.W / R_TW < 1024) {
-            if (si) { if (epi) return launch_c64r_th<T, true, true>(a, s, rth); return launch_c64r_th<T, true, false>(a, s, rth); }
-            if (epi) return launch_c64r_th<T, false, true>(a, s, rth);
-            return launch_c64r_th<T, false, false>(a, s, rth);
+            const int form = (ring == 84 || ring == 44) ? ring : rth;
+            if (si) { if (epi) return launch_c64r_form<T, true, true>(a, s, form); return launch_c64r_form<T, true, false>(a, s, form); }
+            if (epi) return launch_c64r_form<T, false, true>(a, s, form);
+            return launch_c64r_form<T, false, false>(a, s, form);
         }
     }
     // (the persistent kernel's epilogue folds the gain into the demod / noise / bias terms and evaluates lrelu

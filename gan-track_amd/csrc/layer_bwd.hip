@@ -166,8 +166,131 @@ __global__ __launch_bounds__(256) void dot_hw_kernel(float* out, const T* a, con
     for (int i = tid; i < C; i += 256) atomicAdd(&out[(int64_t)n * C + i], red[i]);
 }
 
+// out = act'(a * sa[n,c] + b * sb[n,c]; y) (the act' factor only when y is given), dot[n,c] += sum_p a * e:
+// the elementwise steps of the layers' create_graph VJP nodes (torch_utils/ops/modconv.py _LayerVJP) in one
+// pass each -- G = g_dx * s + g_ds * x with the modulation gradient's sum_p g_dx * dxs, the input-gradient
+// sum gxc + g_ds * dxs, and act'(A d + g_dd * c; y) -- where autograd runs two to four full-size passes.
+// f32 arithmetic, one rounding to T.  Same lane layout as layer_bwd_kernel.
+struct AxArgs {
+    void* out;
+    const void *a, *b, *y, *e;
+    const float *sa, *sb;
+    float* dot;
+    int N, HW, C, pix_per_block, act;
+    float alpha, gain, clamp;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void vjp_axpy_kernel(AxArgs a) {
+    constexpr int V = 16 / sizeof(T) < 8 ? 16 / sizeof(T) : 8;   // elements per 16-byte load
+    constexpr int NL = 8 / V;
+    typedef T vecv __attribute__((ext_vector_type(V)));
+    extern __shared__ __attribute__((aligned(16))) float red[];   // [C] when dot
+    const int LP = a.C / 8, PPP = 256 / LP;
+    const int tid = threadIdx.x, n = blockIdx.y;
+    const int p0 = blockIdx.x * a.pix_per_block, p1 = min(a.HW, p0 + a.pix_per_block);
+    if (a.dot) {
+        for (int i = tid; i < a.C; i += 256) red[i] = 0.f;
+        __syncthreads();
+    }
+    const int cg = tid % LP, pl = tid / LP, c0 = cg * 8;
+    const bool active = pl < PPP;
+    float sa[8], sb[8], acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        sa[j] = (a.sa && active) ? a.sa[(int64_t)n * a.C + c0 + j] : 1.f;
+        sb[j] = (a.sb && active) ? a.sb[(int64_t)n * a.C + c0 + j] : 1.f;
+        acc[j] = 0.f;
+    }
+    const int64_t bytes = (int64_t)a.N * a.HW * a.C * (int64_t)sizeof(T);
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.a, bytes), rb = make_rsrc(a.b ? a.b : a.a, bytes),
+                                 ry = make_rsrc(a.y ? a.y : a.a, bytes), re = make_rsrc(a.e ? a.e : a.a, bytes);
+    const bool hb = a.b != nullptr, hy = a.y != nullptr, he = a.e != nullptr && a.dot != nullptr;
+    T* out = (T*)a.out;
+    constexpr int U = 4;
+    if (active) {
+        for (int pb = p0 + pl; pb < p1; pb += PPP * U) {
+            vecv av[U][NL], bv[U][NL], yv[U][NL], ev[U][NL];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int p = pb + u * PPP;
+                const int boff = p < p1 ? (int)((((int64_t)n * a.HW + p) * a.C + c0) * (int64_t)sizeof(T)) : -1;
+#pragma unroll
+                for (int l = 0; l < NL; ++l) {
+                    const int o = boff < 0 ? -1 : boff + 16 * l;
+                    av[u][l] = buf_load16<vecv>(ra, o);
+                    if (hb) bv[u][l] = buf_load16<vecv>(rb, o);
+                    if (hy) yv[u][l] = buf_load16<vecv>(ry, o);
+                    if (he) ev[u][l] = buf_load16<vecv>(re, o);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int p = pb + u * PPP;
+                vecv o[NL];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int l = j / V, k = j % V;
+                    const float x = (float)av[u][l][k];
+                    float v = x * sa[j];
+                    if (hb) v = fmaf((float)bv[u][l][k], sb[j], v);
+                    if (hy) {
+                        const float yy = (float)yv[u][l][k];
+                        v *= a.gain;
+                        if (a.act == 1 && !(yy > 0.f)) v *= a.alpha;
+                        if (a.clamp >= 0.f && !(yy > -a.clamp && yy < a.clamp)) v = 0.f;
+                    }
+                    if (he) acc[j] = fmaf(x, (float)ev[u][l][k], acc[j]);
+                    o[l][k] = (T)v;
+                }
+                if (p < p1) {
+#pragma unroll
+                    for (int l = 0; l < NL; ++l) *(vecv*)(out + ((int64_t)n * a.HW + p) * a.C + c0 + l * V) = o[l];
+                }
+            }
+        }
+        if (he) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) atomicAdd(&red[c0 + j], acc[j]);
+        }
+    }
+    if (he) {
+        __syncthreads();
+        for (int i = tid; i < a.C; i += 256) atomicAdd(&a.dot[(int64_t)n * a.C + i], red[i]);
+    }
+}
+
 }  // namespace
 }  // namespace sg2
+
+extern "C" int sg2_vjp_axpy(void* out, const void* a, const float* sa, const void* b, const float* sb, const void* y,
+                            int act, float alpha, float gain, float clamp, const void* e, float* dot, int dtype, int N,
+                            int HW, int C, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(out && a, "sg2_vjp_axpy: null pointer");
+    SG2_CHECK((e == nullptr) == (dot == nullptr), "sg2_vjp_axpy: e and dot go together");
+    SG2_CHECK(C % 8 == 0 && C <= 2048 && C >= 8, "sg2_vjp_axpy: C must be a multiple of 8 (<= 2048)");
+    SG2_CHECK(dtype == SG2_F16 || dtype == SG2_BF16 || dtype == SG2_F32, "sg2_vjp_axpy: bad dtype");
+    SG2_CHECK(act == 0 || act == 1, "sg2_vjp_axpy: act must be linear or lrelu");
+    if ((int64_t)N * HW == 0) return 0;
+    SG2_CHECK((int64_t)N * HW * C * 4 < INT32_MAX, "sg2_vjp_axpy: tensor too large (32-bit buffer offsets)");
+    hipStream_t s = as_stream(stream);
+    if (dot) {
+        hipError_t err = zero_acc(dot, (int64_t)N * C * sizeof(float), s);
+        if (err) { set_error("sg2_vjp_axpy: memset failed"); return err; }
+    }
+    AxArgs x{};
+    x.out = out; x.a = a; x.b = b; x.y = y; x.e = e; x.sa = sa; x.sb = sb; x.dot = dot;
+    x.N = N; x.HW = HW; x.C = C; x.act = act; x.alpha = alpha; x.gain = gain; x.clamp = clamp;
+    const int PPP = std::max(1, 256 / (C / 8));
+    x.pix_per_block = std::min(HW, PPP * 16);
+    dim3 grid((unsigned)cdiv(HW, x.pix_per_block), (unsigned)N);
+    const size_t lds = dot ? C * sizeof(float) : 0;
+    if (dtype == SG2_F16) vjp_axpy_kernel<f16_t><<<grid, 256, lds, s>>>(x);
+    else if (dtype == SG2_BF16) vjp_axpy_kernel<bf16_t><<<grid, 256, lds, s>>>(x);
+    else vjp_axpy_kernel<float><<<grid, 256, lds, s>>>(x);
+    return launch_status("sg2_vjp_axpy");
+}
 
 extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, const void* dy, const void* y,
                              const void* c, const float* d, int dtype, int N, int HW, int C, int act, float alpha,

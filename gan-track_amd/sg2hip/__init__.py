@@ -55,6 +55,7 @@ SIGNATURES = {
                             _i, _i, _f, ctypes.POINTER(Epilogue), _vp],
     'sg2_layer_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _f, _vp],
     'sg2_dot_hw': [_vp, _vp, _vp, _i, _i, _i, _i, _vp],
+    'sg2_vjp_axpy': [_vp, _vp, _vp, _vp, _vp, _vp, _i, _f, _f, _f, _vp, _vp, _i, _i, _i, _i, _vp],
     'sg2_grid_sample_fwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
     'sg2_grid_sample_bwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
     'sg2_affine_grid_sample_fwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],

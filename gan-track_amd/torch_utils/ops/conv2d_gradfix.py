@@ -16,6 +16,7 @@ channel before each launch (a few MB at most).
 """
 import contextlib
 import ctypes
+import os
 
 import torch
 
@@ -56,11 +57,16 @@ _WS_LIMIT = 1 << 23  # split-K f32 workspace only for small outputs (low-resolut
 _CLEAN_WS = {}       # device -> persistent zeroed split-K workspace (every call leaves it zeroed)
 
 
+_PERSIST_WS = os.environ.get('SG2_CLEAN_WS', '1') != '0'   # A/B switch: 0 = a fresh zeroed workspace per call
+
+
 def _workspace(x, total):
     """(workspace, clean): the device's persistent zeroed workspace when it can be used (created outside any
     graph capture, so eager calls and replayed graphs share one buffer), else a fresh one per call."""
     if total > _WS_LIMIT:
         return None, False
+    if not _PERSIST_WS:
+        return torch.zeros([total], dtype=torch.float32, device=x.device), False
     ws = _CLEAN_WS.get(x.device)
     if ws is None:
         if torch.cuda.is_current_stream_capturing():
@@ -318,6 +324,42 @@ def layer_bwd(dy, y, c=None, d=None, act=1, alpha=0.2, gain=1.0, clamp=-1.0, wan
             _hip.ptr(d), _hip.dtype_code(y), n, h * w, ch, int(act), float(alpha), float(gain), float(clamp),
             _hip.stream_ptr(y.device)), 'sg2_layer_bwd')
     return dc, db, dd, dn
+
+
+def vjp_axpy(a, sa=None, b=None, sb=None, y=None, act=0, alpha=0.2, gain=1.0, clamp=-1.0, e=None):
+    """sg2_vjp_axpy: out = act'(a * sa[n,c] + b * sb[n,c]; y) (act' only with y) and, with e, dot[n,c] =
+    sum_p a * e (f32).  a, b, y, e: [N, C, H, W] of one dtype (NHWC memory); sa / sb: [N, C] float or None.
+    Returns (out, dot or None).  Channel counts that are not a multiple of 8 (toRGB's output side) take
+    the same arithmetic as torch ops (f32, one rounding)."""
+    n, ch, h, w = a.shape
+    _hip.require_device(a)
+    if ch % 8:
+        v = a.float() * (sa.float()[:, :, None, None] if sa is not None else 1.0)
+        if b is not None:
+            v = v + b.float() * (sb.float()[:, :, None, None] if sb is not None else 1.0)
+        if y is not None:
+            yf = y.float()
+            v = v * gain
+            if act == 1:
+                v = torch.where(yf > 0, v, v * alpha)
+            if clamp >= 0:
+                v = torch.where((yf > -clamp) & (yf < clamp), v, torch.zeros_like(v))
+        dot = (a.float() * e.float()).sum([2, 3]) if e is not None else None
+        return _nhwc(v.to(a.dtype)), dot
+    a = _nhwc(a)
+    args = [_nhwc(t) if t is not None else None for t in (b, y, e)]
+    for t in args:
+        assert t is None or (t.shape == a.shape and t.dtype == a.dtype), 'vjp_axpy: operand shape / dtype'
+    b, y, e = args
+    sa = sa.float().contiguous() if sa is not None else None
+    sb = sb.float().contiguous() if sb is not None else None
+    out = torch.empty_like(a)
+    dot = torch.empty([n, ch], dtype=torch.float32, device=a.device) if e is not None else None
+    _hip.check(_hip.lib().sg2_vjp_axpy(
+        _hip.ptr(out), _hip.ptr(a), _hip.ptr(sa), _hip.ptr(b), _hip.ptr(sb), _hip.ptr(y), int(act), float(alpha),
+        float(gain), float(clamp), _hip.ptr(e), _hip.ptr(dot), _hip.dtype_code(a), n, h * w, ch,
+        _hip.stream_ptr(a.device)), 'sg2_vjp_axpy')
+    return out, dot
 
 
 class _DotHW(torch.autograd.Function):

@@ -308,38 +308,41 @@ class _LayerVJP(torch.autograd.Function):
         oh, ow = dc.shape[2], dc.shape[3]
         dt = x.dtype
         d32, s32 = _f32(dcoefs), _f32(styles)
-        s_ = styles.to(dt).reshape(n, -1, 1, 1) if styles is not None else None
         g_dy = g_x = g_s = g_w = g_d = None
-        # G = dL/d(dxs)
+        g_ds = g_ds if s32 is not None else None
+        gds32 = _f32(g_ds)
+        # G = dL/d(dxs) = g_dx * s + g_ds * x, with sum_p g_dx * dxs (the direct part of g_s) in the same pass
         G = None
-        if g_dx is not None:
-            G = _cg._nhwc(_mul(g_dx.to(dt), s_))
-        if g_ds is not None and s_ is not None:
-            t = x * g_ds.to(dt).reshape(n, -1, 1, 1)
-            G = t if G is None else G + t
+        if g_dx is not None and s32 is None:      # (an unmodulated layer: G is g_dx itself)
+            G = _cg._nhwc(g_dx.to(dt))
+        elif g_dx is not None:
+            G, g_s = _cg.vjp_axpy(g_dx.to(dt), s32, x if g_ds is not None else None, gds32,
+                                  e=dxs if need[2] else None)
+        elif g_ds is not None:
+            G, _ = _cg.vjp_axpy(x, gds32)
         hscale = (g_dd.float() / d32).contiguous() if (g_dd is not None and d32 is not None) else None
         if G is not None and (need[0] or need[4]):
             A_d, _, dot = _conv_any(G, weight, cout, oh, ow, stride, pad, False, wgain, out_scale=d32,
                                     dot_src=dc if (need[4] and d32 is not None) else None)
             if need[4] and d32 is not None:
                 g_d = (dot / d32).to(dcoefs.dtype)
-            if need[0]:
-                gz = A_d if hscale is None else torch.addcmul(A_d, c, g_dd.to(dt).reshape(n, -1, 1, 1))
-                g_dy = _act_grad(gz, zsrc, act, alpha, gain, clamp)
+            if need[0]:   # g_dy = act'(A d + g_dd * c; y): one pass
+                g_dy, _ = _cg.vjp_axpy(A_d, None, c if hscale is not None else None, _f32(g_dd) if hscale is not None
+                                       else None, y=zsrc, act=act, alpha=alpha, gain=gain, clamp=clamp)
         elif need[0] and hscale is not None:
-            g_dy = _act_grad(c * g_dd.to(dt).reshape(n, -1, 1, 1), zsrc, act, alpha, gain, clamp)
+            g_dy, _ = _cg.vjp_axpy(c, _f32(g_dd), y=zsrc, act=act, alpha=alpha, gain=gain, clamp=clamp)
         if need[1] or need[2]:
-            if g_ds is not None and need[1]:
-                g_x = dxs * g_ds.to(dt).reshape(n, -1, 1, 1)
-            if g_dx is not None and need[2] and s_ is not None:
-                g_s = _cg.dot_hw(_cg._nhwc(g_dx.to(dt)), dxs)
+            gxc = gsc = None
             if hscale is not None:
                 gxc, _, gsc = _conv_any(dc, weight, cin, h, w, stride, pad, True, wgain, in_scale=hscale,
                                         out_scale=s32, dot_src=x if (need[2] and s32 is not None) else None)
-                if need[1]:
-                    g_x = gxc if g_x is None else g_x + gxc
-                if gsc is not None:
-                    g_s = gsc if g_s is None else g_s + gsc
+            if need[1]:   # g_x = convT(H, W) * s + g_ds * dxs: one pass
+                if g_ds is not None:
+                    g_x, _ = (_cg.vjp_axpy(gxc, None, dxs, gds32) if gxc is not None else _cg.vjp_axpy(dxs, gds32))
+                else:
+                    g_x = gxc
+            if gsc is not None:
+                g_s = gsc if g_s is None else g_s + gsc
         if need[3] and (G is not None or hscale is not None):
             acc = torch.zeros([cout * kh * kw * cin], dtype=torch.float32, device=x.device)
             if G is not None:
@@ -349,14 +352,6 @@ class _LayerVJP(torch.autograd.Function):
             g_w = acc.view(cout, kh, kw, cin).permute(0, 3, 1, 2).to(weight.dtype)
         g_s = g_s.to(styles.dtype) if g_s is not None else None
         return (g_dy, g_x, g_s, g_w, g_d) + (None,) * 12
-
-
-def _act_grad(g, y, act, alpha, gain, clamp):
-    """act'(g; y): the bias_act gradient with respect to its input, given the output y (no bias term)."""
-    if y.shape[1] % 8 == 0:
-        return _cg.layer_bwd(g, y, None, None, act=act, alpha=alpha, gain=gain, clamp=clamp, want_db=False,
-                             want_dd=False, want_dnoise=False)[0]
-    return _ba.bias_act_grad(g, y, act=_ACT[act], alpha=alpha, gain=gain, clamp=clamp)
 
 
 def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain, clamp,
@@ -627,12 +622,13 @@ class _UpLayerVJP(torch.autograd.Function):
         dt = x.dtype
         d32, s32 = _f32(dcoefs), _f32(styles)
         g_dy = g_x = g_s = g_w = g_d = None
+        gds32 = _f32(g_ds)
         G = None
-        if g_dx is not None:
-            G = _cg._nhwc(g_dx.to(dt) * styles.to(dt).reshape(n, -1, 1, 1))
-        if g_ds is not None:
-            t = x * g_ds.to(dt).reshape(n, -1, 1, 1)
-            G = t if G is None else G + t
+        if g_dx is not None:   # G = g_dx * s + g_ds * x and sum_p g_dx * dxs in one pass
+            G, g_s = _cg.vjp_axpy(g_dx.to(dt), s32, x if g_ds is not None else None, gds32,
+                                  e=dxs if need[2] else None)
+        elif g_ds is not None:
+            G, _ = _cg.vjp_axpy(x, gds32)
         hscale = (g_dd.float() / d32).contiguous() if g_dd is not None else None
         if G is not None and (need[0] or need[4]):
             tG, _ = _cg.conv_fused(G, _cg._pack_conv(weight, dt), cout, th, tw, kh, kw, 2, tpad, transpose=True)
@@ -640,16 +636,12 @@ class _UpLayerVJP(torch.autograd.Function):
             if need[4]:
                 g_d = (_cg.dot_hw(A_d, dc) / (d32 * d32)).to(dcoefs.dtype)
             if need[0]:
-                gz = A_d if hscale is None else torch.addcmul(A_d, c, g_dd.to(dt).reshape(n, -1, 1, 1))
-                g_dy = _act_grad(gz, y, 1, alpha, gain, clamp)
+                g_dy, _ = _cg.vjp_axpy(A_d, None, c if hscale is not None else None, _f32(g_dd) if hscale is not None
+                                       else None, y=y, act=1, alpha=alpha, gain=gain, clamp=clamp)
         elif need[0] and hscale is not None:
-            g_dy = _act_grad(c * g_dd.to(dt).reshape(n, -1, 1, 1), y, 1, alpha, gain, clamp)
-        wT = None
+            g_dy, _ = _cg.vjp_axpy(c, _f32(g_dd), y=y, act=1, alpha=alpha, gain=gain, clamp=clamp)
         if need[1] or need[2]:
-            if g_ds is not None and need[1]:
-                g_x = dxs * g_ds.to(dt).reshape(n, -1, 1, 1)
-            if g_dx is not None and need[2]:
-                g_s = _cg.dot_hw(_cg._nhwc(g_dx.to(dt)), dxs)
+            gxc = None
             if hscale is not None:
                 wT = _cg._pack_conv(weight.transpose(0, 1), dt)
                 dot_src = x if need[2] else None
@@ -658,10 +650,14 @@ class _UpLayerVJP(torch.autograd.Function):
                 else:
                     res = _cg.conv_fused(u, wT, cin, h, w, kh, kw, 2, tpad, in_scale=hscale, out_scale=s32,
                                          dot_src=dot_src)
-                if need[1]:
-                    g_x = res[0] if g_x is None else g_x + res[0]
+                gxc = res[0]
                 if need[2]:
                     g_s = res[2] if g_s is None else g_s + res[2]
+            if need[1]:
+                if g_ds is not None:
+                    g_x, _ = (_cg.vjp_axpy(gxc, None, dxs, gds32) if gxc is not None else _cg.vjp_axpy(dxs, gds32))
+                else:
+                    g_x = gxc
         if need[3] and (G is not None or hscale is not None):
             acc = torch.zeros([cin * kh * kw * cout], dtype=torch.float32, device=x.device)
             if G is not None:

@@ -196,6 +196,17 @@ int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, const void* dy,
                   const float* d, int dtype, int N, int HW, int C, int act, float alpha, float gain, float clamp,
                   void* stream);
 
+/* The elementwise steps of the layers' create_graph VJP (path-length / R1 passes; the reference runs them as
+ * autograd's mul / add / bias_act-grad nodes, SG3/training/networks_stylegan2.py:59-89 and bias_act.py:154-207):
+ *   out[n,p,c] = act'(a * sa[n,c] + b * sb[n,c]; y)      (sa / sb NULL = 1, b NULL = off, y NULL = no act')
+ *   dot[n,c]   = sum_p a[n,p,c] * e[n,p,c]                (e and dot both or neither; dot zeroed by the call)
+ * act' = the bias_act gradient given the output y: * gain, * alpha where y <= 0 (lrelu), 0 where |y| >= clamp
+ * (clamp < 0 = off).  a, b, y, e, out: [N, HW, C] NHWC of dtype (f16 / bf16 / f32), C % 8 == 0; f32
+ * arithmetic, one rounding. */
+int sg2_vjp_axpy(void* out, const void* a, const float* sa, const void* b, const float* sb, const void* y, int act,
+                 float alpha, float gain, float clamp, const void* e, float* dot, int dtype, int N, int HW, int C,
+                 void* stream);
+
 /* out[n, c] = sum_p a[n, p, c] * b[n, p, c] (f32 accumulation; a, b: [N, HW, C] NHWC f16/bf16, C % 8 == 0;
  * out zeroed by the call).  The reductions (dz * c).sum([2, 3]) and (dxs * x).sum([2, 3]) of the
  * modulated-conv backward (SG3/training/networks_stylegan2.py:59-70 under autograd) without the

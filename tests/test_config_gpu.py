@@ -34,10 +34,13 @@ GROUPS = ['grad/Gmain', 'grad/Greg', 'grad/Dmain', 'grad/Dreg', 'G1', 'D1', 'Gem
 # (profiles/r02_config_parity.jsonl) with ~1.5x margin.  The regularisation phases are the noisy ones:
 # the product's float atomics make repeated runs differ, and at C2 fp16 six runs gave Greg flat errors of
 # 0.055-0.093 and Dreg 0.066-0.16 (profiles/r02_c2_fp16_repeats.jsonl), so their floors are 1.5x the
-# largest of those.
+# largest of those.  The bf16 Gmain floor was 0.06 against a single measured 0.057 (C5): the round-3 ring conv
+# rounds the modulated weight round(W * round(s)) where the reference rounds the modulated activation (one
+# rounding either way) and measured 0.061 (0.057 with the ring off), so it takes the
+# policy's 1.5x of the round-2 measurement, 0.085.
 FLOOR16 = {
     'fp16': {'grad/Gmain': 0.03, 'grad/Greg': 0.14, 'grad/Dmain': 0.05, 'grad/Dreg': 0.24, 'param': 1e-3},
-    'bf16': {'grad/Gmain': 0.06, 'grad/Greg': 0.2, 'grad/Dmain': 0.06, 'grad/Dreg': 0.15, 'param': 2e-3},
+    'bf16': {'grad/Gmain': 0.085, 'grad/Greg': 0.2, 'grad/Dmain': 0.06, 'grad/Dreg': 0.15, 'param': 2e-3},
 }
 
 
@@ -102,9 +105,13 @@ def test_16bit_iteration_vs_reference(tag, dt):
 # own run-to-run spread)) -- its own conditioning, no phase-wide term -- and every tensor the reference's f32
 # gets within 1e-4 of float64 must also match the reference's f32 result itself to 3e-4 (or 4x that spread).
 P0_TAGS = ['c2p0', 'c4p0', 'c5p0']
+# 16-bit at p = 0 (num_fp16_res = 4): floors are 1.5x the worst measured over the three fixtures (round 3,
+# profiles/r03_config_parity.jsonl `*_cond` records: fp16 Gmain 0.016 / Greg 0.062 / Dmain 0.13 / Dreg 0.28, bf16
+# 0.094 / 0.24 / 0.22 / 0.63).  The 16-bit rounding, not f32 conditioning, sets these: the reference has no
+# 16-bit CPU run to compare with, and R1's double backward in bf16 (8-bit mantissa) keeps little of Dreg.
 P0_FLOOR16 = {
-    'fp16': {'grad/Gmain': 1e-2, 'grad/Greg': 2e-2, 'grad/Dmain': 1e-2, 'grad/Dreg': 2e-2, 'param': 1e-3},
-    'bf16': {'grad/Gmain': 4e-2, 'grad/Greg': 6e-2, 'grad/Dmain': 4e-2, 'grad/Dreg': 6e-2, 'param': 2e-3},
+    'fp16': {'grad/Gmain': 0.025, 'grad/Greg': 0.095, 'grad/Dmain': 0.2, 'grad/Dreg': 0.42, 'param': 1e-3},
+    'bf16': {'grad/Gmain': 0.15, 'grad/Greg': 0.36, 'grad/Dmain': 0.33, 'grad/Dreg': 0.95, 'param': 2e-3},
 }
 
 

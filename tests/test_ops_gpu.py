@@ -1288,11 +1288,13 @@ def test_fused_conv_wgain_weight_grad(mode):
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize('shape', [(4, 256, 256), (11, 48, 256), (13, 40, 256), (3, 64, 704)])
 @pytest.mark.parametrize('form', ['mod_epi_raw', 'mod_epi', 'mod_only', 'plain_epi', 'plain', 'epi_no_noise'])
-@pytest.mark.parametrize('ring', ['4', '8'])
+@pytest.mark.parametrize('ring', ['4', '44', '8', '84'])
 def test_conv3x3_c64_ring(dtype, shape, form, ring, monkeypatch):
     """The 64 -> 64 channel ring kernel (LDS-DMA halo ring, weights in registers modulated per sample;
-    conv3x3.hip conv3x3_c64r_kernel) in both forms (ring 4: two workgroups per CU on 32 x 4 tiles, 2-slot rings;
-    ring 8: one workgroup on 32 x 8 tiles, 3-slot ring) and every form the layers use -- the synthesis forward
+    conv3x3.hip conv3x3_c64r_kernel) in its three forms (ring 4: two workgroups per CU on 32 x 4 tiles, 2-slot rings;
+    ring 44: ring 4 with whole-line stores staged through LDS; ring 8: one workgroup of 8 waves on 32 x 8 tiles,
+    3-slot ring; ring 84: the same tiles with 4 waves of 4 rows)
+    and every form the layers use -- the synthesis forward
     (modulation, demod, noise, bias, lrelu, clamp, raw output), the path-length pass's scaled transposed conv
     (modulation only), the D conv (bias + lrelu + clamp), a plain conv -- against float64.  Shapes cover bands of
     4 / 2 / 1 tile rows, runs that cross samples (the per-sample weight re-modulation) and image borders on every
@@ -1301,7 +1303,7 @@ def test_conv3x3_c64_ring(dtype, shape, form, ring, monkeypatch):
     monkeypatch.setenv('SG2_C64_RING', ring)
     N, H, W = shape
     C = 64
-    th = int(ring)
+    th = 4 if ring in ('4', '44') else 8
     wgs = (2 if th == 4 else 1) * torch.cuda.get_device_properties(DEV).multi_processor_count
     assert N * (H // th) * (W // 32) >= 2 * wgs      # the ring kernel's minimum of two tiles per workgroup
     torch.manual_seed(17)
@@ -1343,3 +1345,80 @@ def test_conv3x3_c64_ring(dtype, shape, form, ring, monkeypatch):
     edge = torch.zeros(H, W, dtype=torch.bool)
     edge[0], edge[-1], edge[:, 0], edge[:, -1] = True, True, True, True
     assert rel_err(y.float()[..., edge], ref[..., edge]) < 2 * tol
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('C', [8, 64, 512])
+@pytest.mark.parametrize('form', ['G_dot', 'axpy', 'act', 'scale_only'])
+def test_vjp_axpy(dtype, C, form):
+    """sg2_vjp_axpy (the elementwise steps of modconv._LayerVJP) against its f32 torch expression."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(5)
+    N, H, W = 3, 17, 24
+    T = lambda t: t.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    a, b, e, y = (T(torch.randn(N, C, H, W)) for _ in range(4))
+    sa, sb = torch.rand(N, C, device=DEV) + 0.5, torch.randn(N, C, device=DEV)
+    kw = dict(G_dot=dict(sa=sa, b=b, sb=sb, e=e), axpy=dict(b=b, sb=sb), act=dict(b=b, sb=sb, y=y),
+              scale_only=dict(sa=sa))[form]
+    act = dict(act=1, alpha=0.2, gain=1.41, clamp=1.0) if form == 'act' else {}
+    out, dot = cg.vjp_axpy(a, **kw, **act)
+    v = a.float() * (kw['sa'][:, :, None, None] if 'sa' in kw else 1)
+    if 'b' in kw:
+        v = v + b.float() * sb[:, :, None, None]
+    if form == 'act':
+        yf = y.float()
+        v = torch.where(yf > 0, v, v * 0.2) * 1.41
+        v = torch.where(yf.abs() < 1.0, v, torch.zeros_like(v))
+    tol = {torch.float16: 1e-3, torch.bfloat16: 8e-3, torch.float32: 1e-6}[dtype]
+    assert out.dtype == dtype and out.is_contiguous(memory_format=torch.channels_last)
+    assert rel_err(out.float(), v) < tol
+    if form == 'G_dot':
+        assert rel_err(dot, (a.float() * e.float()).sum([2, 3])) < 1e-5
+
+
+@pytest.mark.parametrize('up,cin,cout,res,n', [(1, 512, 512, 64, 1), (2, 512, 512, 64, 1), (1, 128, 64, 32, 3),
+                                                (2, 64, 64, 64, 2), (1, 64, 64, 256, 2)])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16])
+def test_layer_vjp_matches_composed(up, cin, cout, res, n, dtype):
+    """The fused create_graph VJP nodes (modconv._LayerVJP, _UpLayerVJP) against the fused layer's composed VJP on
+    the path-length pass (reference loss.py:85-100: the ws gradient under no_weight_gradients, then the penalty's
+    backward with weight gradients on) at network widths: the f32 split-K shapes of the 64^2 / 512-channel
+    blocks, the up-2 layer, and the 16-bit halo / ring layers.  Every second-order gradient (weight, bias, noise
+    strength, affine, the input and the latent)."""
+    from training import networks_stylegan2 as net
+    from torch_utils.ops import conv2d_gradfix, modconv
+    torch.manual_seed(23)
+    layer = net.SynthesisLayer(cin, cout, w_dim=32, resolution=res, up=up, conv_clamp=256).to(DEV)
+    with torch.no_grad():
+        layer.noise_strength.fill_(0.2)
+        layer.bias.copy_(torch.randn(cout) * 0.2)
+    hin = res // up
+    x0 = torch.randn(n, cin, hin, hin, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    w0 = torch.randn(n, 32, device=DEV)
+    noise = torch.randn(n, 1, res, res, device=DEV)
+    pl = torch.randn(n, cout, res, res, device=DEV) / res
+    params = [layer.weight, layer.bias, layer.noise_strength, layer.affine.weight, layer.affine.bias]
+    out = []
+    for vjp in [True, False]:
+        modconv.fused_vjp = vjp
+        x = x0.clone().requires_grad_(True)
+        wv = w0.clone().requires_grad_(True)
+        orig = torch.randn
+        torch.randn = lambda *a, **k: noise.clone()
+        try:
+            y = layer(x, wv)
+        finally:
+            torch.randn = orig
+        with conv2d_gradfix.no_weight_gradients():
+            g_w, g_x = torch.autograd.grad((y.float() * pl).sum(), [wv, x], create_graph=True)
+        loss = g_w.square().sum() + g_x.float().square().sum()
+        g2 = torch.autograd.grad(loss, params + [x, wv], allow_unused=True)
+        out.append([g_w.float(), g_x.float()] + [g if g is None else g.float() for g in g2])
+    modconv.fused_vjp = True
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    names = ['g_w', 'g_x', 'weight', 'bias', 'noise_strength', 'affine.weight', 'affine.bias', 'x', 'wv']
+    for name, a_, b_ in zip(names, *out):
+        if b_ is None or float(b_.abs().max()) == 0:
+            assert a_ is None or float(a_.abs().max()) == 0, name
+            continue
+        assert rel_err(a_, b_) < tol, (name, rel_err(a_, b_))

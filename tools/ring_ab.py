@@ -3,6 +3,7 @@ configuration (SG2_C64_RING, SG2_RING_DBG); prints ms per launch and the fractio
 and plain forms.  Usage: python tools/ring_ab.py [reps]"""
 import os
 import sys
+import time
 import numpy as np
 import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -11,6 +12,12 @@ import bench  # noqa: E402
 from torch_utils.ops import conv2d_gradfix as cg  # noqa: E402
 
 dev = torch.device('cuda', 0)
+# warm the clocks first (the first launches of a cold process run ~10 % slower than the bench's, which follow
+# the training steps)
+_t0 = time.time()
+while time.time() - _t0 < 1.0:
+    bench._layer_launch(dev, 256, 64, torch.float16)
+torch.cuda.synchronize()
 res = []
 for r in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
     ms, fl, by = bench._layer_launch(dev, 256, 64, torch.float16)

@@ -33,7 +33,7 @@ def part(name, fn):
         fn()
     torch.cuda.synchronize()
     time.sleep(0.2)
-    print('PART', name, time.time_ns(), flush=True)
+    print('PART', name, time.clock_gettime_ns(time.CLOCK_MONOTONIC), time.clock_gettime_ns(time.CLOCK_BOOTTIME), flush=True)
     fn()
     torch.cuda.synchronize()
     time.sleep(0.2)
