@@ -21,6 +21,7 @@ import sg2hip as _hip
 from torch_utils import misc
 from torch_utils import persistence
 from torch_utils.ops import bias_act
+from torch_utils.ops import conv2d_gradfix
 from torch_utils.ops import conv2d_resample
 from torch_utils.ops import fma
 from torch_utils.ops import modconv
@@ -104,6 +105,11 @@ class _Demod(torch.autograd.Function):
         w, s, d, wsq = ctx.saved_tensors
         need_w, need_s = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         if torch.is_grad_enabled():
+            # Inside no_weight_gradients (the path-length / R1 first pass, which asks autograd.grad for the latent
+            # or image gradient only) the weight's gradient is never used: autograd's engine would prune it for
+            # the reference's composed expression; a custom Function's needs_input_grad cannot tell, so skip it
+            # here instead of building its double-backward graph.
+            need_w = need_w and not conv2d_gradfix.weight_gradients_disabled
             gu = dd * d.pow(3) * -0.5
             gs = 2 * s * (gu @ w.square().sum([2, 3])) if need_s else None
             gw = 2 * w * (gu.t() @ s.square())[:, :, None, None] if need_w else None
@@ -167,8 +173,9 @@ class _Addmm(torch.autograd.Function):
         beta, alpha = ctx.beta, ctx.alpha
         nb, nx, nw = ctx.needs_input_grad[:3]
         if torch.is_grad_enabled():
-            return ((dy.sum(0) * beta) if nb else None, (dy @ w) * alpha if nx else None,
-                    (dy.t() @ x) * alpha if nw else None, None, None)
+            pg = not conv2d_gradfix.weight_gradients_disabled   # (see _Demod.backward: parameter grads unused)
+            return ((dy.sum(0) * beta) if nb and pg else None, (dy @ w) * alpha if nx else None,
+                    (dy.t() @ x) * alpha if nw and pg else None, None, None)
         z = _zero_scalar(dy)
         db = None
         if nb:   # beta * sum_rows(dy) as ONE GEMV (a sum and a scale otherwise)

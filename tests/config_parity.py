@@ -304,12 +304,14 @@ def judge_cond(got, fix, floors=F32_FLOORS, factor=4.0, groups=('grad/', 'G1/', 
     return worst, sorted(rows, reverse=True)
 
 
-def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True,
-                       rerun=None):
+def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/',), check=True, rerun=None):
     """Direct product-vs-reference-f32 check on every tensor the reference's f32 result gets right (both its
     norm and its sampled entries within `well` of the float64 answer): the product must then agree with the
     reference itself to `tol` (or 4x the product's own run-to-run difference on that tensor, when `rerun` is
-    given) on both measures.  Returns (number of tensors checked, worst error, its key)."""
+    given) on both measures.  Gradients only: a parameter after Adam's first step (beta1 = 0) moves each entry by
+    about lr * sign(g), so an entry whose gradient is zero up to rounding lands 2 lr apart in two correct
+    evaluations (measured: D1/b512.conv1.bias at C4 / p = 0); the parameters are held by the flat check.
+    Returns (number of tensors checked, worst error, its key)."""
     truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
     keys = sorted(set(_keys(truth, groups)) & set(_keys(got, groups)))
     n, worst, wk, fails = 0, 0.0, '', []
@@ -346,9 +348,11 @@ def judge_flat(got_flat, ref_flat, floor, factor=3.0):
 REG_STATS = ('Loss/pl_penalty', 'Loss/G/reg', 'Loss/r1_penalty', 'Loss/D/reg')
 
 
-def judge_stats_f32(got, fix, floor=1e-4, reg_floor=3e-3, factor=4.0, group_factor=3.0, check=True):
+def judge_stats_f32(got, fix, floor=1e-4, reg_floor=3e-3, factor=4.0, group_factor=3.0, check=True,
+                    rerun_stats=()):
     """Reported loss statistics against f64: each within max(floor, factor x the reference f32's error on it,
-    group_factor x the reference's worst statistic error) -- the same chance argument as judge_f32."""
+    group_factor x the reference's worst statistic error, factor x the product's own run-to-run difference on it
+    when reruns are given) -- the same chance argument as judge_f32 / judge_cond."""
     names, ref_vals = fixture_stats(fix)
     assert [n for n, _ in got] == names, 'reported statistics differ in name or order'
     rows = []
@@ -357,14 +361,16 @@ def judge_stats_f32(got, fix, floor=1e-4, reg_floor=3e-3, factor=4.0, group_fact
             continue
         t = np.asarray(fix[f'f64/stats/{j}'], np.float64)
         den = max(np.linalg.norm(t), 1e-30)
+        spread = max([0.0] + [float(np.linalg.norm(np.asarray(rs[j][1], np.float64) - np.asarray(v, np.float64)))
+                              / den for rs in rerun_stats])
         rows.append((n, np.linalg.norm(np.asarray(v, np.float64) - t) / den,
-                     np.linalg.norm(np.asarray(r, np.float64) - t) / den))
-    gmax = max(er for _, _, er in rows)
-    for n, e, er in rows:
+                     np.linalg.norm(np.asarray(r, np.float64) - t) / den, spread))
+    gmax = max(er for _, _, er, _ in rows)
+    for n, e, er, sp in rows:
         fl = reg_floor if n in REG_STATS else floor
-        assert not check or e <= max(fl, factor * er, group_factor * gmax), \
-            f'stat {n}: rel err vs f64 {e:.3g} (reference f32 {er:.3g}, worst reference stat {gmax:.3g})'
-    return max(e for _, e, _ in rows)
+        assert not check or e <= max(fl, factor * er, group_factor * gmax, factor * sp), \
+            f'stat {n}: rel err vs f64 {e:.3g} (reference f32 {er:.3g}, worst reference stat {gmax:.3g}, rerun {sp:.3g})'
+    return max(e for _, e, _, _ in rows)
 
 
 def judge_pl_mean(got, fix, floor=3e-3, factor=4.0, check=True):

@@ -130,5 +130,12 @@ def test_graph_exchange_overlap_simulated_ranks(monkeypatch):
         if mode == 'graph':
             assert tr._graphs['Gmain'].overlapped > 0, 'no bucket was exchanged from inside the captured backward'
         res.append(torch.cat([p.detach().double().flatten() for m in (G, D, G_ema) for p in m.parameters()]))
-    assert rel_err(res[1], res[0]) < 1e-6
-    assert rel_err(res[2], res[0]) < 1e-5
+        if mode == 'flat':
+            names = [f'{mn}.{n}' for mn, m in (('G', G), ('D', D), ('G_ema', G_ema)) for n, _ in m.named_parameters()]
+            sizes = [p.numel() for m in (G, D, G_ema) for p in m.parameters()]
+
+    def worst(a, b):
+        d = [(float((x - y).abs().max()), n) for x, y, n in zip(a.split(sizes), b.split(sizes), names)]
+        return sorted(d, reverse=True)[:4]
+    assert rel_err(res[1], res[0]) < 1e-6, worst(res[1], res[0])
+    assert rel_err(res[2], res[0]) < 1e-5, worst(res[2], res[0])
