@@ -43,6 +43,7 @@ template <bool SWZ> struct Lay {
 };
 
 struct PTap { int8_t dy, dx, out, pad_; };   // shift on the phase grid, output tap index
+typedef __attribute__((address_space(3))) void* lds_ptr_w;
 
 struct W3Args {
     const void* g;        // [N,GH,GW,A]
@@ -213,6 +214,198 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
     }
 }
 
+// LDS-DMA form of the stride-1 kernel (round 3).  The kernel above stages each tile through registers
+// (19 16-byte loads a lane, then a ds_write pass behind a barrier, during which the matrix pipe idles) and
+// reads a padded 144-byte-pitch image whose ds_read_b64_tr_b16 row quads conflict 2-way (SQ_LDS_BANK_CONFLICT
+// 0.45 of the LDS cycles).  Here:
+//   * g and the x halo arrive by LDS-DMA (buffer_load ... lds, 1 KiB = 8 whole 128-byte pixel rows a
+//     wave-instruction) into a double-buffered image: tile t + 1 is in flight while tile t's MFMAs run, one
+//     barrier a tile, no staging registers (2 x 77 KB of LDS, one workgroup per CU as before);
+//   * rows are unpadded and their 32-channel halves swap when bit 1 of the row is set (Lay<true>): the four rows
+//     of a transposing read hit four disjoint bank quarters.  The DMA destination is lane-linear, so the swap
+//     sits in the SOURCE address: lane l loads piece (l & 7) ^ (4 ((l >> 4) & 1)) of its row.  The halo rows
+//     have a pitch of TW + 4 pixels (a multiple of 4; two pad columns never read), so bit 1 of a fragment row is
+//     a function of the lane and the tap column only and every fragment read is a per-lane base plus an
+//     immediate offset (the k-step loop is fully unrolled);
+//   * the modulation (g_scale / x_scale, one value per channel and sample) is constant over a tile (one sample),
+//     so it leaves the inner loop: the MFMAs accumulate the unscaled products of the current sample and, when the
+//     workgroup's tile run moves to the next sample (and at the end), the partial sums are folded into a second
+//     f32 set as tot += u[n, a] s[n, b] acc.  The reference rounds x * round(s) to 16 bits before its GEMM;
+//     this keeps the product in f32 (the difference is below the 16-bit rounding of the inputs).
+// Stride 1, one phase holding every tap (3x3 pad 1, or 1x1 pad 0).
+template <int TW> struct WDma {
+    static constexpr int TH = 256 / TW, HWD = TW + 4, HP = HWD * (TH + 2);
+    static_assert(HP % 8 == 0, "whole DMA instructions");
+    static constexpr int GI = 256 / 8, XI = HP / 8;            // DMA wave-instructions per tile (g, x)
+    static constexpr int GB = 256 * 128, STAGE = GB + HP * 128;
+    static constexpr size_t LDS = 2 * (size_t)STAGE;
+    static_assert(LDS <= 160 * 1024, "wgrad DMA LDS");
+};
+
+__device__ __forceinline__ unsigned lds_off_w(const void* p) {
+    return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
+
+template <typename T>
+__device__ __forceinline__ v8w<T> ld_frag(unsigned addr) {     // rows r .. r + 3 at addr, r + 4 .. r + 7 at + 512
+    typedef __attribute__((address_space(3))) s16x4* lp;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(uintptr_t)addr);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(uintptr_t)(addr + 512));
+    s16x8w r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(v8w<T>, r);
+}
+
+template <typename T, int TW, int NT, bool SC>
+__global__ __launch_bounds__(256) void wgrad3x3_dma_kernel(W3Args a) {
+    typedef WDma<TW> L;
+    constexpr int TH = L::TH, HWD = L::HWD, HP = L::HP;
+    constexpr int SZ = (int)sizeof(T);
+    static_assert(SZ == 2, "16-bit");
+    extern __shared__ __attribute__((aligned(16))) char wsm[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wa = wave >> 1, wb = wave & 1;
+    const int a0 = blockIdx.x * BC, b0 = blockIdx.y * BC;
+    const int t_begin = blockIdx.z * a.tiles_per_block;
+    const int t_end = min(a.tiles, t_begin + a.tiles_per_block);
+    if (t_begin >= t_end) return;
+    const int GH = a.GH, GW = a.GW, XH = a.XH, XW = a.XW, A = a.A, B = a.B, tiles_x = a.tiles_x;
+    const int per = tiles_x * a.tiles_y;
+    const __amdgpu_buffer_rsrc_t rgb = make_rsrc(a.g, (int64_t)a.N * GH * GW * A * SZ);
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(a.x, (int64_t)a.N * XH * XW * B * SZ);
+    const int l3 = lane >> 3;
+    const int pj = (lane & 7) ^ (((lane >> 4) & 1) << 2);      // source piece of this lane (swizzle, see above)
+    const bool gok = a0 + 8 * pj < A, xok = b0 + 8 * pj < B;   // out-of-block channels read zeros
+    const int gch = (a0 + 8 * pj) * SZ, xch = (b0 + 8 * pj) * SZ;
+    const unsigned lbase = lds_off_w(wsm);
+
+    auto issue = [&](int t, int stage) {
+        const int n = t / per, r = t - n * per;
+        const int ty0 = (r / tiles_x) * TH, tx0 = (r - (r / tiles_x) * tiles_x) * TW;
+        char* sb = wsm + stage * L::STAGE;
+#pragma unroll
+        for (int u = 0; u < L::GI / 4; ++u) {
+            const int px = 8 * (u * 4 + wave) + l3;
+            const int oy = ty0 + px / TW, ox = tx0 + px % TW;
+            int off = ((n * GH + oy) * GW + ox) * A * SZ + gch;
+            off = (gok && oy < GH && ox < GW) ? off : -1;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rgb, (lds_ptr_w)(sb + (u * 4 + wave) * 1024), 16, off, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < (L::XI + 3) / 4; ++u) {
+            const int i = u * 4 + wave;                        // wave-uniform
+            if (u < L::XI / 4 || i < L::XI) {
+                const int hp = 8 * i + l3, hy = hp / HWD, hx = hp - hy * HWD;
+                const int iy = ty0 - 1 + hy, ix = tx0 - 1 + hx;
+                int off = ((n * XH + iy) * XW + ix) * B * SZ + xch;
+                off = (xok && hx < TW + 2 && (unsigned)iy < (unsigned)XH && (unsigned)ix < (unsigned)XW) ? off : -1;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rxb, (lds_ptr_w)(sb + L::GB + i * 1024), 16, off, 0, 0, 0);
+            }
+        }
+    };
+
+    // fragment addressing (frag32 above, with the row arithmetic taken out): a 16-lane group G reads a 4-row
+    // quad, lane li = 4 q + p at row + q, columns 4 p .. + 3 of its 16-column block.  Bit 1 of the row is bit 1
+    // of q for g (rows k0 + 8 (lane >> 5) + q, k0 a multiple of 16) and of q + tap column for x (rows
+    // (py + dy) HWD + px + dx + q with HWD and px multiples of 4).
+    const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, hh = lane >> 5;
+    const unsigned colA = ((wa * 32 + 16 * (G & 1) + 4 * p) * SZ) ^ (((q >> 1) & 1) << 6);
+    const unsigned abase = (8 * hh + q) * 128 + colA;
+    unsigned bbase[3];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+        bbase[dx] = L::GB + (8 * hh + dx + q) * 128 + (((wb * 32 + 16 * (G & 1) + 4 * p) * SZ) ^ ((((dx + q) >> 1) & 1) << 6));
+    auto tap_dy = [](int tp) { return NT == 9 ? tp / 3 : 1; };
+    auto tap_dx = [](int tp) { return NT == 9 ? tp % 3 : 1; };
+
+    f32x16 acc[NT], tot[SC ? NT : 1];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
+    if (SC) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) tot[t][j] = 0.f;
+    }
+    const int b = b0 + wb * 32 + (lane & 31);
+    // tot += u[n, a] s[n, b] acc; acc = 0   (a = a0 + 32 wa + 8 (j / 4) + 4 (lane >> 5) + j % 4)
+    auto fold = [&](int n) {
+        if constexpr (SC) {
+            const float sx = a.xscale ? a.xscale[n * B + min(b, B - 1)] : 1.f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int ar = min(a0 + wa * 32 + 8 * (j >> 2) + 4 * hh + (j & 3), A - 1);
+                const float su = (a.gscale ? a.gscale[n * A + ar] : 1.f) * sx;
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    tot[t][j] = fmaf(acc[t][j], su, tot[t][j]);
+                    acc[t][j] = 0.f;
+                }
+            }
+        }
+    };
+
+    issue(t_begin, 0);
+    __builtin_amdgcn_s_waitcnt(0x0f70);                        // vmcnt(0): this wave's DMAs of the first tile
+    __builtin_amdgcn_s_barrier();
+    int k = 0, cur_n = t_begin / per;
+    for (int t = t_begin; t < t_end; ++t, ++k) {
+        const int stage = k & 1;
+        if (t + 1 < t_end) issue(t + 1, stage ^ 1);            // the other stage was released by the last barrier
+        const int n = t / per;
+        if (SC && n != cur_n) {
+            fold(cur_n);
+            cur_n = n;
+        }
+        const unsigned sa = lbase + stage * L::STAGE + abase;
+        unsigned sb[3];
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) sb[dx] = lbase + stage * L::STAGE + bbase[dx];
+        // k-step ks: g rows 16 ks.., x rows (py + dy) HWD + px0 + ...; next step's fragments read before this
+        // step's MFMAs
+        auto xoff = [&](int ks, int tp) {
+            const int k0 = 16 * ks, py = k0 / TW, px0 = k0 % TW;
+            return ((py + tap_dy(tp)) * HWD + px0) * 128;
+        };
+        // rolling prefetch: fragment tp of step ks + 1 is read as soon as step ks's MFMA tp has consumed it
+        v8w<T> fa = ld_frag<T>(sa), fb[NT];
+#pragma unroll
+        for (int tp = 0; tp < NT; ++tp) fb[tp] = ld_frag<T>(sb[tap_dx(tp)] + xoff(0, tp));
+        // (fully unrolled: every fragment read is base + immediate, and the compiler keeps the x fragments that a
+        // later step reads again at another tap row in registers)
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) {
+            const int kn = ks + 1 < 16 ? ks + 1 : ks;
+            const v8w<T> fan = ld_frag<T>(sa + 16 * kn * 128);
+#pragma unroll
+            for (int tp = 0; tp < NT; ++tp) {
+                acc[tp] = mma32<T>(fa, fb[tp], acc[tp]);
+                if (ks + 1 < 16) fb[tp] = ld_frag<T>(sb[tap_dx(tp)] + xoff(kn, tp));
+            }
+            fa = fan;
+        }
+        // the next tile's DMAs (this wave's only outstanding vector-memory ops) have landed, and every wave is
+        // done reading this stage before the next iteration's DMAs overwrite it
+        __builtin_amdgcn_s_waitcnt(0x0070);                    // vmcnt(0) lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+    }
+    fold(cur_n);
+
+    if (b < B) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int ar = a0 + wa * 32 + 8 * (j >> 2) + 4 * hh + (j & 3);
+            if (ar >= A) continue;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                atomicAdd(a.dw + ((int64_t)ar * a.KK + (NT == 9 ? t : 0)) * B + b, (SC ? tot[t][j] : acc[t][j]) * a.alpha);
+        }
+    }
+}
+
 // Stride-2 / pad-0 3x3 weight gradient in ONE launch (the discriminator's down-2 layers after their FIR
 // and the transposed convs of the up layers): x coordinate = 2 g + k.  Where the phase split above runs
 // four launches that each re-stage the whole of g and feed 1-4 MFMAs per A fragment, this kernel stages
@@ -351,6 +544,17 @@ void launch_w3(const W3Args& a, dim3 grid, hipStream_t s) {
     else wgrad3x3_kernel<T, TW, NT, false><<<grid, 256, 0, s>>>(a);
 }
 
+template <typename T, int TW, int NT, bool SC>
+void launch_wdma(const W3Args& a, dim3 grid, hipStream_t s) {
+    auto kern = wgrad3x3_dma_kernel<T, TW, NT, SC>;
+    static bool attr_set = false;   // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WDma<TW>::LDS);
+        attr_set = true;
+    }
+    kern<<<grid, 256, WDma<TW>::LDS, s>>>(a);
+}
+
 template <typename T, int TW>
 int dispatch_nt(const W3Args& a, dim3 grid, int nt, hipStream_t s) {
     switch (nt) {
@@ -425,6 +629,31 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
     a.tiles_per_block = (int)cdiv(a.tiles, splits);
     splits = (int)cdiv(a.tiles, a.tiles_per_block);
     dim3 grid((unsigned)cdiv(A, BC), (unsigned)cdiv(B, BC), (unsigned)splits);
+    // stride 1 with every tap in one phase: the LDS-DMA kernel (SG2_WGRAD_DMA=0 keeps the register-staged one)
+    // (with a modulation scale the second sum set spills: SG2_WGRAD_DMA=2 runs it anyway, for A/B timing)
+    static const int dma_on = [] { const char* e = getenv("SG2_WGRAD_DMA"); return e ? atoi(e) : 1; }();
+    if (dma_on && (dma_on == 2 || (!gscale && !xscale)) && stride == 1 && ((KH == 3 && pad_y == 1 && pad_x == 1) || (KH == 1 && pad_y == 0 && pad_x == 0))) {
+        for (int ky = 0; ky < KH; ++ky)
+            for (int kx = 0; kx < KW; ++kx)
+                a.taps[ky * KW + kx] = PTap{(int8_t)(ky - pad_y), (int8_t)(kx - pad_x), (int8_t)(ky * KW + kx), 0};
+        a.PY = 0; a.PX = 0;
+        const int sel = ((gscale || xscale) ? 1 : 0) | (KH == 3 ? 2 : 0) | (TW == 32 ? 4 : 0) | (dtype == SG2_F16 ? 8 : 0);
+        switch (sel) {
+#define SG2_WDMA_2(B_, T_, TW_, NT_)                                   \
+            case B_: launch_wdma<T_, TW_, NT_, false>(a, grid, s); break; \
+            case B_ + 1: launch_wdma<T_, TW_, NT_, true>(a, grid, s); break;
+            SG2_WDMA_2(0, bf16_t, 16, 1)
+            SG2_WDMA_2(2, bf16_t, 16, 9)
+            SG2_WDMA_2(4, bf16_t, 32, 1)
+            SG2_WDMA_2(6, bf16_t, 32, 9)
+            SG2_WDMA_2(8, f16_t, 16, 1)
+            SG2_WDMA_2(10, f16_t, 16, 9)
+            SG2_WDMA_2(12, f16_t, 32, 1)
+            SG2_WDMA_2(14, f16_t, 32, 9)
+#undef SG2_WDMA_2
+        }
+        return launch_status("sg2_conv2d_wgrad (halo, LDS-DMA)");
+    }
     for (int py = 0; py < stride; ++py)
         for (int px = 0; px < stride; ++px) {
             int nt = 0;
