@@ -152,13 +152,13 @@ def _layer_launch(device, res, C, dtype, N=32):
     return ms, flops, byts
 
 
-def _measured_traffic(key):
+def _measured_traffic(key, kernel):
     """HBM bytes per launch of the roofline launch from the committed PMC passes (tools/pmc_traffic.py ->
-    profiles/roofline_traffic.json), if they were taken on this exact launch configuration."""
+    profiles/roofline_traffic.json), if they were taken on this exact launch configuration and kernel."""
     try:
         with open(os.path.join(ROOT, 'profiles', 'roofline_traffic.json')) as f:
             t = json.load(f)
-        if t.get('config') != key:
+        if t.get('config') != key or kernel not in t.get('kernel', ''):
             return None, None
         return t['hbm_bytes_per_launch'], t.get('hbm_bytes_per_launch_x2_rule')
     except (OSError, ValueError, KeyError):
@@ -188,7 +188,7 @@ def roofline(device, res, cbase, dtype, N=32):
     else:
         out.update({'bound': 'mfma', 'achieved': round(tflops, 2), 'peak': MFMA_PEAK_FP16, 'unit': 'TFLOP/s',
                     'frac': round(tflops / MFMA_PEAK_FP16, 4)})
-    traffic, traffic_x2 = _measured_traffic(key)
+    traffic, traffic_x2 = _measured_traffic(key, kname.split()[0] if C == 64 else 'conv3x3_halo_kernel')
     out.update({'traffic': traffic, 'traffic_fetch_x2_rule': traffic_x2, 'ms_per_launch': round(ms, 4),
                 'algorithmic_flops_per_launch': flops, 'algorithmic_hbm_bytes_per_launch': byts,
                 'arithmetic_intensity': round(ai, 1), 'ridge': round(ridge, 1),

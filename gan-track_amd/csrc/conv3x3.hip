@@ -744,7 +744,7 @@ __device__ __forceinline__ void wait_vm() {           // s_waitcnt vmcnt(N) (gfx
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <typename T, bool SI, bool EPI, bool RAW, int R_TH, int WR, bool PIPE, bool STG>
+template <typename T, bool SI, bool EPI, bool RAW, int R_TH, int WR, bool PIPE, bool STG, bool ROLL>
 __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER_CU)) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
     typedef Ring<R_TH, WR> RG;
@@ -818,6 +818,7 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
                         }
                     }
                     wf[jj][tap][c] = v;
+                    if (PIPE && c == 1 && (tap % 3) == 2) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight
                 }
         }
     };
@@ -873,6 +874,42 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
         }
     };
 
+    // ROLL (round 3, form 46): the two slots are one ring of 2 (TH + 2) halo rows (row r at r * 5120 B) and a
+    // workgroup's run goes down whole image columns (band = the column), so a tile whose upper neighbour came just
+    // before it loads only its TH new halo rows; the TH + 2 rows of tile k sit at ring rows pos_k .. + TH + 1
+    // (mod 2 (TH + 2)), pos_{k+1} = pos_k + TH after a vertical neighbour, + TH + 2 after a jump (new column or
+    // sample: all rows fresh).  The rows a DMA overwrites are the complement of the current tile's (its
+    // predecessor's, released by the last barrier).  HBM reads of the halo drop from ~1.33x (the band's re-reads
+    // that miss in L2) toward the 34 / 32 of the side columns, and a third fewer DMA instructions per tile.
+    constexpr int RR = 2 * (R_TH + 2), ROWB = R_PITCH * 128;
+    auto issue_roll = [&](int t, bool succ, int pos, int eslot) {
+        if (SG2_RDIAG & 16) return;
+        int n, ty, tx;
+        tile_of(t, n, ty, tx);
+        const int hy0 = succ ? 2 : 0, n_i = (R_TH + 2 - hy0) * 5;
+#pragma unroll
+        for (int u = 0; u < (R_HALO_I + 1 + NW - 1) / NW; ++u) {
+            const int i = u * NW + wave;              // wave-uniform
+            if (i < n_i) {
+                const int hy = hy0 + i / 5, cg = i - (i / 5) * 5;
+                const int iy = ty - 1 + hy, ix0 = tx - 1 + cg * 8;
+                int rr = pos + hy;
+                rr = rr >= RR ? rr - RR : rr;
+                const int base = (unsigned)iy < (unsigned)a.H ? ((n * a.H + iy) * a.W + ix0) * 128 : -(1 << 30);
+                const bool kill = ((tx == 0) & (cg == 0) & (lx == 0)) | ((tx + R_TW == a.W) & (cg == 4) & (lx == 1)) |
+                                  ((cg == 4) & (lx >= 2));
+                const int off = kill ? -1 : base + hlane;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rxb, (lds_ptr_t)(smem_raw + rr * ROWB + cg * 1024), 16, off, 0, 0, 0);
+            } else if (i == n_i) {
+                const char* nb = has_noise ? epi_src0 + (int64_t)((n * a.H + ty) * a.W + tx) * (int)sizeof(T) : epi_src0;
+                const char* db = has_d ? epi_src1 + n * 256 : epi_src1;
+                const char* src = (lane < 32 ? nb : db) + elane;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                 (lds_ptr_t)(epil + eslot * R_EPI), 16, 0, 0);
+            }
+        }
+    };
+
     // MFMA B-fragment addressing: pixel fragment i of the wave at tap (ky, kx), chunk c reads position
     // (2 wr + (i >> 1) + ky) * 40 + (i & 1) * 16 + l16 + kx, piece c * 4 + q (swizzled as at the DMA)
     int boff[3][2];
@@ -881,7 +918,7 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int x = l16 + kx;
-            boff[kx][c] = (WR * wr * R_PITCH + x) * 128 + 16 * ((c * 4 + q) ^ (((x >> 1) & 3) << 1));
+            boff[kx][c] = ((ROLL ? 0 : WR * wr * R_PITCH) + x) * 128 + 16 * ((c * 4 + q) ^ (((x >> 1) & 3) << 1));
         }
 
     const float lr_alpha = (EPI && a.act == 1) ? a.alpha : 1.f;
@@ -1029,9 +1066,87 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
                         }
                 }
     };
+    // ROLL: halo row j of the wave (tile row 2 wr + j) at ring row pos + 2 wr + j
+    auto mfma_tile_roll = [&](f32x4 (&A)[NF][2], int pos) {
+        const char* rb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int rr = pos + WR * wr + j;
+            rr = rr >= RR ? rr - RR : rr;
+            rb[j] = smem_raw + rr * ROWB;
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    v8<T> pf[NF];
+#pragma unroll
+                    for (int i = 0; i < NF; ++i)
+                        pf[i] = *(const v8<T>*)(rb[(i >> 1) + ky] + boff[kx][c] + (i & 1) * 16 * 128);
+                    const bool first = c == 0 && ky == 0 && kx == 0;
+#pragma unroll
+                    for (int i = 0; i < NF; ++i)
+#pragma unroll
+                        for (int jj = 0; jj < 2; ++jj)
+                            A[i][jj] = mma<T>(wf[jj][ky * 3 + kx][c], pf[i], first ? f32x4{0.f, 0.f, 0.f, 0.f} : A[i][jj]);
+                }
+    };
+
+    // (half-tile pipeline) the MFMAs of pixel fragments I0, I0 + 1 (one tile row of the wave) and their epilogue
+    auto mfma_half = [&](f32x4 (&A)[NF][2], const char* hb, auto i0c) {
+        constexpr int I0 = decltype(i0c)::value;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    v8<T> pf[2];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int i = I0 + u;
+                        pf[u] = *(const v8<T>*)(hb + boff[kx][c] + (((i >> 1) + ky) * R_PITCH + (i & 1) * 16) * 128);
+                    }
+                    const bool first = c == 0 && ky == 0 && kx == 0;
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int jj = 0; jj < 2; ++jj)
+                            A[I0 + u][jj] = mma<T>(wf[jj][ky * 3 + kx][c], pf[u], first ? f32x4{0.f, 0.f, 0.f, 0.f} : A[I0 + u][jj]);
+                }
+    };
+    auto epi_half = [&](f32x4 (&A)[NF][2], auto i0c, int n, int ty, int tx, const float (&bb)[8], const float (&dd)[8],
+                        const float (&nz)[NF]) {
+        constexpr int I0 = decltype(i0c)::value;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = I0 + u;
+            const int r = WR * wr + (i >> 1), px = (i & 1) * 16 + l16;
+            const int pix = (n * a.H + ty + r) * a.W + tx + px;
+            vec8 yv, rv;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float cv = A[i][e >> 2][e & 3];
+                if (RAW) rv[e] = (T)cv;
+                float v = cv;
+                if (EPI) {
+                    v = fmaf(v, dd[e], nz[i] + bb[e]);
+                    v = fmaxf(v, v * lr_alpha);
+                    v = __builtin_amdgcn_fmed3f(v, -clampv, clampv);
+                }
+                yv[e] = (T)v;
+            }
+            const int dst = (pix * 64 + ch0) * (int)sizeof(T);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, dst, 0, 0);
+            if (RAW) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, dst, 0, 0);
+        }
+    };
 
     // ---- prologue: tiles 0 .. NSLOT - 2 in flight, wait for tile 0 ----
-    issue(t_begin, 0, 0);
+    if (ROLL) issue_roll(t_begin, false, 0, 0);
+    else issue(t_begin, 0, 0);
     if (R_NSLOT == 3) {
         issue(min(t_begin + 1, t_end - 1), 1, 1);
         wait_vm<R_DMA>();
@@ -1042,7 +1157,36 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     __builtin_amdgcn_s_barrier();
 
     int k = 0;
-    if constexpr (!PIPE) {
+    if constexpr (ROLL) {
+        static_assert(!ROLL || (R_NSLOT == 2 && !PIPE && !STG), "rolling rows: the plain 2-slot form");
+        f32x4 acc[NF][2];
+        int pos = 0;
+        for (int t = t_begin; t < t_end; ++t, ++k) {
+            int n, ty, tx;
+            tile_of(t, n, ty, tx);
+            int pos1 = pos;
+            if (t + 1 < t_end) {                      // tile t + 1 into the ring rows tile t does not use
+                int n1, ty1, tx1;
+                tile_of(t + 1, n1, ty1, tx1);
+                const bool succ = n1 == n && tx1 == tx && ty1 == ty + R_TH;
+                pos1 = pos + (succ ? R_TH : R_TH + 2);
+                pos1 = pos1 >= RR ? pos1 - RR : pos1;
+                issue_roll(t + 1, succ, pos1, (k + 1) % R_NEPI);
+            }
+            if (SI && n != cur_n) {
+                cur_n = n;
+                load_weights(n);
+            }
+            mfma_tile_roll(acc, pos);
+            float bb[8], dd[8], nz[NF];
+            epi_table(k % R_NEPI, bb, dd, nz);
+            epi_store(acc, n, ty, tx, bb, dd, nz);
+            wait_vm<S>();                             // tile t + 1's DMAs: younger are this iteration's stores
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_s_barrier();
+            pos = pos1;
+        }
+    } else if constexpr (!PIPE) {
         f32x4 acc[NF][2];
         for (int t = t_begin; t < t_end; ++t, ++k) {
             const int slot = k % R_NSLOT;
@@ -1069,15 +1213,18 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
             __builtin_amdgcn_s_barrier();
         }
     } else {
-        // Pipelined epilogue (3-slot form): iteration k runs tile k's MFMAs into one accumulator set and tile
-        // k - 1's epilogue from the other in the same basic block, so the epilogue's VALU and stores issue
-        // between MFMAs instead of after them.  The epilogue table of tile k - 1 (its epilogue-ring slot is
-        // rewritten three iterations later) is read at the top of the iteration.
-        static_assert(!PIPE || R_NSLOT == 3, "pipelined epilogue: 3-slot ring");
-        f32x4 acc0[NF][2], acc1[NF][2];
-        int t = t_begin, pn = 0, pty = 0, ptx = 0;
-        auto step = [&](auto has_prev, f32x4 (&Acur)[NF][2], f32x4 (&Aprev)[NF][2]) {
-            constexpr bool HP = decltype(has_prev)::value;
+        // Half-tile pipeline (round 3, PIPE, the 2-slot form): the wave's 4 pixel fragments are two halves (its two
+        // tile rows).  Each iteration runs in two phases, each one basic block of MFMAs for one half beside the
+        // epilogue of the other: phase 1 -- tile k's first half (fragments 0, 1) MFMAs | tile k - 1's second half
+        // epilogue; phase 2 -- tile k's second half (fragments 2, 3) MFMAs | tile k's first half epilogue.  The
+        // epilogue VALU and stores issue between MFMAs and the stores spread over the tile instead of bunching at
+        // its end, with the one accumulator set (a second set does not fit beside the 144 weight registers).
+        // Tile k's epilogue table (ring slot k % 4, rewritten by the DMAs of iteration k + 3) is read in both of
+        // its epilogue phases.
+        static_assert(!PIPE || (R_NSLOT == 2 && NF == 4), "half-tile pipeline: the 2-slot form");
+        f32x4 acc[NF][2];
+        int pn = 0, pty = 0, ptx = 0;
+        for (int t = t_begin; t < t_end; ++t, ++k) {
             const int slot = k % R_NSLOT;
             issue(min(t + R_NSLOT - 1, t_end - 1), (k + R_NSLOT - 1) % R_NSLOT, (k + R_NSLOT - 1) % R_NEPI);
             int n, ty, tx;
@@ -1086,378 +1233,37 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
                 cur_n = n;
                 load_weights(n);
             }
-            float bb[8], dd[8], nz[NF];
-            if (HP) epi_table((k + R_NEPI - 1) % R_NEPI, bb, dd, nz);
-            mfma_tile(Acur, smem_raw + slot * R_SLOT);
-            if (HP) epi_store(Aprev, pn, pty, ptx, bb, dd, nz);
-            // tile t + 1's DMAs (issued one iteration ago) must have landed; younger: the stores of the previous
-            // iteration (none at k = 1), this iteration's DMAs and its stores (none at k = 0)
-            if (k == 0) wait_vm<R_DMA>();
-            else if (k == 1) wait_vm<R_DMA + S>();
-            else wait_vm<R_DMA + 2 * S>();
+            {   // phase 1
+                float bb[8], dd[8], nz[NF];
+                if (k > 0) epi_table((k + R_NEPI - 1) % R_NEPI, bb, dd, nz);
+                mfma_half(acc, smem_raw + slot * R_SLOT, std::integral_constant<int, 0>{});
+                if (k > 0) epi_half(acc, std::integral_constant<int, 2>{}, pn, pty, ptx, bb, dd, nz);
+            }
+            {   // phase 2
+                float bb[8], dd[8], nz[NF];
+                epi_table(k % R_NEPI, bb, dd, nz);
+                mfma_half(acc, smem_raw + slot * R_SLOT, std::integral_constant<int, 2>{});
+                epi_half(acc, std::integral_constant<int, 0>{}, n, ty, tx, bb, dd, nz);
+            }
+            // tile t + 1 (issued at the top of this iteration) must have landed; younger: this iteration's stores
+            // (half of them at k = 0)
+            if (k == 0) wait_vm<S / 2>();
+            else wait_vm<S>();
             __builtin_amdgcn_s_waitcnt(0xc07f);
             __builtin_amdgcn_s_barrier();
             pn = n; pty = ty; ptx = tx;
-            ++k; ++t;
-        };
-        step(std::false_type{}, acc0, acc1);
-        bool last0 = true;                            // which set holds the last tile's sums
-        while (t < t_end) {
-            step(std::true_type{}, acc1, acc0);
-            last0 = false;
-            if (t >= t_end) break;
-            step(std::true_type{}, acc0, acc1);
-            last0 = true;
         }
         float bb[8], dd[8], nz[NF];
         epi_table((k + R_NEPI - 1) % R_NEPI, bb, dd, nz);
-        if (last0) epi_store(acc0, pn, pty, ptx, bb, dd, nz);
-        else epi_store(acc1, pn, pty, ptx, bb, dd, nz);
+        epi_half(acc, std::integral_constant<int, 2>{}, pn, pty, ptx, bb, dd, nz);
     }
     wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
 }
 
-// Form W of the ring kernel (SG2_C64_RING=16, round 3): ONE wave per SIMD owning ALL 64 output channels.
-// In the forms above a wave holds 32 of a pixel's 64 channels, so every output store writes half of each
-// 128-byte pixel line, and a pair of waves per SIMD shares the 256 registers.  Here a 4-wave workgroup per CU
-// (512 registers a wave) works on 32 x 4 tiles, wave w on tile row w:
-//   * weights: 4 A fragments (16 channels each) x 9 taps x 2 chunks = 288 registers, modulated per sample;
-//     A row m of fragment jj is channel 16 (m >> 2) + 4 jj + (m & 3), so lane group q ends with the 16
-//     consecutive channels 16 q .. + 15 of its pixel (32 bytes);
-//   * per tap and chunk 2 pixel fragments (ds_read_b128) feed 8 MFMAs: 144 per wave and tile, 36 reads;
-//   * the epilogue of tile k - 1 runs in the same basic block as tile k's MFMAs (a second accumulator set),
-//     so its VALU and stores issue between MFMAs of the same wave;
-//   * whole-line stores: each wave transposes its 32 x 128-byte output row through 4 KB of wave-private LDS
-//     (ds_write_b128 of its 32-byte channel quarters, ds_read_b128 of whole lines, XOR-swizzled, no barrier:
-//     a wave's LDS operations complete in order) and stores 1 KiB of 8 consecutive pixels per instruction;
-//   * a 4-slot halo ring (three tiles in flight) and an 8-deep epilogue-table ring.
-constexpr int W_NSLOT = 4, W_NEPI = 8, W_TH = 4, W_NW = 4;
-constexpr int W_SLOT = (W_TH + 2) * R_PITCH * 128;                        // 30,720 B
-constexpr int W_HALO_I = (W_TH + 2) * R_PITCH / 8;                        // 30 halo DMA instructions per tile
-constexpr int W_DMA = (W_HALO_I + 1 + W_NW - 1) / W_NW;                   // 8 per wave (the last round: the table)
-constexpr size_t W_LDS = (size_t)W_NSLOT * W_SLOT + W_NEPI * R_EPI + 64 * 4 + W_NW * 4096;   // 147,712 B
-static_assert(W_LDS <= 160 * 1024, "form W LDS");
-static_assert((W_DMA - 1) * W_NW <= W_HALO_I && W_DMA * W_NW > W_HALO_I, "the last DMA round holds the epilogue table");
-
-template <typename T, bool SI, bool EPI, bool RAW>
-__global__ __launch_bounds__(256, 1) void conv3x3_c64w_kernel(Conv3Args a, int tiles_total, int band) {
-    typedef T vec8 __attribute__((ext_vector_type(8)));
-    constexpr int S = RAW ? 8 : 4;                    // buffer stores per wave and tile
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    char* epil = smem_raw + W_NSLOT * W_SLOT;
-    float* blds = (float*)(epil + W_NEPI * R_EPI);
-    char* xpose = (char*)(blds + 64);
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int l16 = lane & 15, q = lane >> 4;
-    const int t_begin = (int)((int64_t)blockIdx.x * tiles_total / gridDim.x);
-    const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles_total / gridDim.x);
-    if (t_begin >= t_end) return;
-    auto pack_tile = [&](int t) -> int {
-        const int tiles_x = a.W / R_TW, per_n = tiles_x * (a.H / W_TH), per_band = band * tiles_x;
-        const int n = t / per_n, r = t - n * per_n, b = r / per_band, rb = r - b * per_band, col = rb / band;
-        return (n << 20) | ((b * band + rb - col * band) << 10) | col;
-    };
-    const int tinfo0 = t_begin + lane < t_end ? pack_tile(t_begin + lane) : 0;
-    const int tinfo1 = t_begin + 64 + lane < t_end ? pack_tile(t_begin + 64 + lane) : 0;
-    auto tile_of = [&](int t, int& n, int& ty, int& tx) {
-        const int j = t - t_begin;
-        const int v = j < 64 ? __builtin_amdgcn_readlane(tinfo0, j) : __builtin_amdgcn_readlane(tinfo1, j - 64);
-        n = v >> 20;
-        ty = ((v >> 10) & 1023) * W_TH;
-        tx = (v & 1023) * R_TW;
-    };
-    const int xbytes = __builtin_amdgcn_readfirstlane(a.N * a.H * a.W * 64 * (int)sizeof(T));
-    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(a.x, xbytes);
-    const __amdgpu_buffer_rsrc_t rwb = make_rsrc(a.w, 64 * 9 * 64 * (int)sizeof(T));
-    const __amdgpu_buffer_rsrc_t rsc = make_rsrc(a.in_scale, SI ? __builtin_amdgcn_readfirstlane(a.N * 64 * 4) : 0);
-    const __amdgpu_buffer_rsrc_t ryb = make_rsrc(a.y, xbytes);
-    const __amdgpu_buffer_rsrc_t ryr = make_rsrc(a.y_raw, RAW ? xbytes : 0);
-
-    // ---- weights: 4 x 9 x 2 A fragments, modulated by the sample's styles ----
-    vec8 wf[4][9][2];
-    auto load_weights = [&](int n) {
-        float4 s4[2][2];
-        if (SI) {
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) s4[c][hh] = buf_load16<float4>(rsc, (n * 64 + c * 32 + q * 8 + hh * 4) * 4);
-        }
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int o = 16 * (l16 >> 2) + 4 * jj + (l16 & 3);
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    vec8 v = buf_load16<vec8>(rwb, ((o * 9 + tap) * 64 + c * 32 + q * 8) * (int)sizeof(T));
-                    if (SI) {
-                        const float4 x0 = s4[c][0], x1 = s4[c][1];
-                        const vec8 sv = vec8{(T)x0.x, (T)x0.y, (T)x0.z, (T)x0.w, (T)x1.x, (T)x1.y, (T)x1.z, (T)x1.w};
-                        if constexpr (std::is_same<T, f16_t>::value) {
-                            v = v * sv;
-                        } else {
-#pragma unroll
-                            for (int e = 0; e < 8; ++e) v[e] = (T)((float)v[e] * (float)sv[e]);
-                        }
-                    }
-                    wf[jj][tap][c] = v;
-                    if (c == 1 && (tap % 3) == 2) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight
-                }
-        }
-    };
-    int cur_n;
-    {
-        int ty, tx;
-        tile_of(t_begin, cur_n, ty, tx);
-    }
-    load_weights(cur_n);
-    if (tid < 64) blds[tid] = (EPI && a.bias) ? (float)(T)a.bias[tid] * a.gain : 0.f;
-
-    // ---- LDS-DMA issue (as the 32 x 4 form above; wave w owns instructions u * 4 + w) ----
-    const bool has_noise = EPI && a.noise != nullptr, has_d = EPI && a.out_scale != nullptr;
-    const char* epi_src0 = has_noise ? (const char*)a.noise : (has_d ? (const char*)a.out_scale : (const char*)a.x);
-    const char* epi_src1 = has_d ? (const char*)a.out_scale : epi_src0;
-    const int lx = lane >> 3;
-    const int hlane = lx * 128 + (((lane & 7) ^ (((lx >> 1) & 3) << 1)) * 16);
-    const int elane = lane < 32 ? (has_noise ? (((lane >> 2) % W_TH) * a.W + (lane & 3) * 8) * (int)sizeof(T) : 0)
-                                : ((lane - 32) & 15) * 16;
-    auto issue = [&](int t, int slot, int eslot) {
-        int n, ty, tx;
-        tile_of(t, n, ty, tx);
-#pragma unroll
-        for (int u = 0; u < W_DMA; ++u) {
-            const int i = u * W_NW + wave;
-            if (u < W_DMA - 1 || i < W_HALO_I) {
-                const int hy = i / 5, cg = i - hy * 5;
-                const int iy = ty - 1 + hy, ix0 = tx - 1 + cg * 8;
-                const int base = (unsigned)iy < (unsigned)a.H ? ((n * a.H + iy) * a.W + ix0) * 128 : -(1 << 30);
-                const bool kill = ((tx == 0) & (cg == 0) & (lx == 0)) | ((tx + R_TW == a.W) & (cg == 4) & (lx == 1)) |
-                                  ((cg == 4) & (lx >= 2));
-                const int off = kill ? -1 : base + hlane;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rxb, (lds_ptr_t)(smem_raw + slot * W_SLOT + i * 1024), 16, off, 0, 0, 0);
-            } else {
-                const char* nb = has_noise ? epi_src0 + (int64_t)((n * a.H + ty) * a.W + tx) * (int)sizeof(T) : epi_src0;
-                const char* db = has_d ? epi_src1 + n * 256 : epi_src1;
-                const char* src = (lane < 32 ? nb : db) + elane;
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                                 (lds_ptr_t)(epil + eslot * R_EPI), 16, 0, 0);
-            }
-        }
-    };
-
-    // B fragment i (pixels 16 i .. + 15 of row w) at tap (ky, kx), chunk c: position (w + ky) * 40 + 16 i + l16 + kx
-    int boff[3][2];
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const int x = l16 + kx;
-            boff[kx][c] = (wave * R_PITCH + x) * 128 + 16 * ((c * 4 + q) ^ (((x >> 1) & 3) << 1));
-        }
-
-    const float lr_alpha = (EPI && a.act == 1) ? a.alpha : 1.f;
-    const float clampv = (EPI && a.clamp >= 0.f) ? a.clamp : __builtin_inff();
-    const float ngain = a.noise_gain * a.gain;
-    const int ch0 = 16 * q;                           // this lane's 16 output channels
-
-    // epilogue tables of a tile (inline-asm reads: see the 32 x 4 form)
-    auto epi_table = [&](int eslot, float (&bb)[16], float (&dd)[16], float (&nz)[2]) {
-        if (!EPI) return;
-        const unsigned et = lds_addr(epil + eslot * R_EPI);
-        const unsigned bt = lds_addr(blds + ch0);
-        float4 b0, b1, b2, b3, d0, d1, d2, d3;
-        asm volatile("ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:16\n\t"
-                     "ds_read_b128 %2, %8 offset:32\n\tds_read_b128 %3, %8 offset:48\n\t"
-                     "ds_read_b128 %4, %9 offset:512\n\tds_read_b128 %5, %9 offset:528\n\t"
-                     "ds_read_b128 %6, %9 offset:544\n\tds_read_b128 %7, %9 offset:560\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(b0), "=&v"(b1), "=&v"(b2), "=&v"(b3), "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3)
-                     : "v"(bt), "v"(et + ch0 * 4));
-        const float bq[16] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
-        const float dq[16] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w, d2.x, d2.y, d2.z, d2.w, d3.x, d3.y, d3.z, d3.w};
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            bb[e] = bq[e];
-            dd[e] = has_d ? dq[e] * a.gain : a.gain;
-        }
-        // pixel w * 32 + 16 i + l16 of the table
-        const unsigned na = et + (wave * R_TW + l16) * (unsigned)sizeof(T);
-        unsigned r0, r1;
-        asm volatile("ds_read_u16 %0, %2\n\tds_read_u16 %1, %2 offset:32\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(r0), "=&v"(r1) : "v"(na));
-        nz[0] = has_noise ? (float)__builtin_bit_cast(T, (unsigned short)r0) * ngain : 0.f;
-        nz[1] = has_noise ? (float)__builtin_bit_cast(T, (unsigned short)r1) * ngain : 0.f;
-    };
-    // wave-private transpose image: pixel P (0..31) at P * 128, 16-byte piece j at slot j ^ (P & 7)
-    const unsigned xp = lds_addr(xpose + wave * 4096);
-    auto row_store = [&](const u32x4 (&v)[2][2], const __amdgpu_buffer_rsrc_t& rout, int n, int ty, int tx) {
-        // lane (q, l16) holds pieces 2q, 2q + 1 of pixels l16 (v[0]) and 16 + l16 (v[1])
-        unsigned wa[4];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int P = 16 * i + l16;
-                wa[2 * i + k] = xp + P * 128 + (((2 * q + k) ^ (P & 7)) << 4);
-            }
-        // reads: instruction s covers pixels 8 s .. + 7, lane L piece L & 7 of pixel 8 s + (L >> 3)
-        const int pj = lane & 7, pp = lane >> 3;
-        const unsigned ra = xp + pp * 128 + ((pj ^ pp) << 4);   // (8 s + pp) & 7 = pp
-        u32x4 o0, o1, o2, o3;
-        asm volatile("ds_write_b128 %4, %8\n\tds_write_b128 %5, %9\n\tds_write_b128 %6, %10\n\tds_write_b128 %7, %11\n\t"
-                     "ds_read_b128 %0, %12\n\tds_read_b128 %1, %12 offset:1024\n\t"
-                     "ds_read_b128 %2, %12 offset:2048\n\tds_read_b128 %3, %12 offset:3072\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3)
-                     : "v"(wa[0]), "v"(wa[1]), "v"(wa[2]), "v"(wa[3]),
-                       "v"(v[0][0]), "v"(v[0][1]), "v"(v[1][0]), "v"(v[1][1]), "v"(ra)
-                     : "memory");
-        const int rowpix = (n * a.H + ty + wave) * a.W + tx;
-        const int off = (rowpix + pp) * 128 + pj * 16;
-        __builtin_amdgcn_raw_buffer_store_b128(o0, rout, off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(o1, rout, off + 8 * 128, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(o2, rout, off + 16 * 128, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(o3, rout, off + 24 * 128, 0, 0);
-    };
-    // the tile's conv result rounded to T (the reference's conv2d output dtype), packed: lane (q, l16) holds
-    // channels 16 q .. + 15 of pixels l16 (C[0]) and 16 + l16 (C[1]) -- the state carried into the next iteration
-    auto pack_c = [&](const f32x4 (&A)[2][4], u32x4 (&C)[2][2]) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int k2 = 0; k2 < 2; ++k2) {
-                vec8 v;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = (T)A[i][(8 * k2 + e) >> 2][e & 3];
-                C[i][k2] = __builtin_bit_cast(u32x4, v);
-            }
-    };
-    auto epi_store = [&](const u32x4 (&C)[2][2], int n, int ty, int tx, const float (&bb)[16], const float (&dd)[16],
-                         const float (&nz)[2]) {
-        if (RAW) row_store(C, ryr, n, ty, tx);
-        if (!EPI) {
-            row_store(C, ryb, n, ty, tx);
-            return;
-        }
-        u32x4 yq[2][2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int k2 = 0; k2 < 2; ++k2) {
-                const vec8 cv = __builtin_bit_cast(vec8, C[i][k2]);
-                vec8 yv;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int ce = 8 * k2 + e;
-                    float v = fmaf((float)cv[e], dd[ce], nz[i] + bb[ce]);
-                    v = fmaxf(v, v * lr_alpha);
-                    v = __builtin_amdgcn_fmed3f(v, -clampv, clampv);
-                    yv[e] = (T)v;
-                }
-                yq[i][k2] = __builtin_bit_cast(u32x4, yv);
-            }
-        row_store(yq, ryb, n, ty, tx);
-    };
-    auto mfma_tile = [&](f32x4 (&A)[2][4], const char* hb) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < 3; ++kx) {
-                    v8<T> pf[2];
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) pf[i] = *(const v8<T>*)(hb + boff[kx][c] + (ky * R_PITCH + 16 * i) * 128);
-                    const bool first = c == 0 && ky == 0 && kx == 0;
-#pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int jj = 0; jj < 4; ++jj)
-                            A[i][jj] = mma<T>(wf[jj][ky * 3 + kx][c], pf[i], first ? f32x4{0.f, 0.f, 0.f, 0.f} : A[i][jj]);
-                }
-    };
-
-    // ---- prologue: tiles 0 .. 2 in flight, wait for tile 0 ----
-    issue(t_begin, 0, 0);
-    issue(min(t_begin + 1, t_end - 1), 1, 1);
-    issue(min(t_begin + 2, t_end - 1), 2, 2);
-    wait_vm<2 * W_DMA>();
-    __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0): the bias table
-    __builtin_amdgcn_s_barrier();
-
-    // Iteration k: tile k's MFMAs and tile k - 1's epilogue (tables, math, transposes, stores) from its packed
-    // 16-bit conv result, in one basic block.  Tile k's epilogue table lives in epilogue slot k % 8, which the
-    // DMAs of iteration k + 5 rewrite: read at iteration k + 1.
-    f32x4 acc[2][4];
-    u32x4 cprev[2][2];
-    int k = 0, t = t_begin, pn = 0, pty = 0, ptx = 0;
-    auto step = [&](auto has_prev) {
-        constexpr bool HP = decltype(has_prev)::value;
-        issue(min(t + W_NSLOT - 1, t_end - 1), (k + W_NSLOT - 1) % W_NSLOT, (k + W_NSLOT - 1) % W_NEPI);
-        int n, ty, tx;
-        tile_of(t, n, ty, tx);
-        if (HP) {
-            float bb[16], dd[16], nz[2];
-            epi_table((k + W_NEPI - 1) % W_NEPI, bb, dd, nz);
-            mfma_tile(acc, smem_raw + (k % W_NSLOT) * W_SLOT);
-            epi_store(cprev, pn, pty, ptx, bb, dd, nz);
-        } else {
-            mfma_tile(acc, smem_raw + (k % W_NSLOT) * W_SLOT);
-        }
-        pack_c(acc, cprev);
-        // tile k + 1's DMAs (issued in iteration k - 2, or the prologue) must have landed.  Younger vector-memory ops
-        // of this wave: the DMAs of tiles k + 2 and k + 3 and the stores of iterations k - 2 .. k (iteration 0 stores
-        // nothing)
-        if (k == 0) wait_vm<2 * W_DMA>();
-        else if (k == 1) wait_vm<2 * W_DMA + S>();
-        else if (k == 2) wait_vm<2 * W_DMA + 2 * S>();
-        else wait_vm<2 * W_DMA + 3 * S>();
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_s_barrier();
-        pn = n; pty = ty; ptx = tx;
-        ++k; ++t;
-    };
-    auto drain = [&]() {                              // the last tile's epilogue, outside the pipeline
-        float bb[16], dd[16], nz[2];
-        epi_table((k + W_NEPI - 1) % W_NEPI, bb, dd, nz);
-        epi_store(cprev, pn, pty, ptx, bb, dd, nz);
-    };
-    step(std::false_type{});
-    while (t < t_end) {
-        if (SI) {                                     // a new sample (rare): drain the pipeline, re-modulate
-            int n, ty, tx;
-            tile_of(t, n, ty, tx);
-            if (n != cur_n) {
-                drain();
-                cur_n = n;
-                load_weights(n);
-                step(std::false_type{});
-                continue;
-            }
-        }
-        step(std::true_type{});
-    }
-    drain();
-    wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
-}
-
-template <typename T, bool SI, bool EPI, bool RAW>
-int launch_c64w(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
-    auto kern = conv3x3_c64w_kernel<T, SI, EPI, RAW>;
-    static bool attr_set = false;   // benign race: idempotent attribute
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)W_LDS);
-        attr_set = true;
-    }
-    kern<<<grid, 256, W_LDS, s>>>(a, tiles, band);
-    return launch_status("sg2_conv3x3 (c64 ring, form W)");
-}
-
-template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, bool STG>
+template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, bool STG, bool ROLL>
 int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
     typedef Ring<TH, WR> RG;
-    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW, TH, WR, PIPE, STG>;
+    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW, TH, WR, PIPE, STG, ROLL>;
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RG::LDS);
@@ -1467,27 +1273,25 @@ int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band
     return launch_status("sg2_conv3x3 (c64 ring)");
 }
 
-template <typename T, bool SI, bool EPI, int TH, int WR, bool PIPE = false, bool STG = false>
+template <typename T, bool SI, bool EPI, int TH, int WR, bool PIPE = false, bool STG = false, bool ROLL = false>
 int launch_c64r_raw(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
-    return a.y_raw ? launch_c64r<T, SI, EPI, true, TH, WR, PIPE, STG>(a, s, tiles, grid, band)
-                   : launch_c64r<T, SI, EPI, false, TH, WR, PIPE, STG>(a, s, tiles, grid, band);
+    return a.y_raw ? launch_c64r<T, SI, EPI, true, TH, WR, PIPE, STG, ROLL>(a, s, tiles, grid, band)
+                   : launch_c64r<T, SI, EPI, false, TH, WR, PIPE, STG, ROLL>(a, s, tiles, grid, band);
 }
 
 // form: 4 = 32 x 4 tiles, two workgroups of 4 waves per CU; 8 = 32 x 8 tiles, one workgroup of 8 waves;
 // 44 = form 4 with whole-line stores staged through the consumed slot; 84 = 32 x 8 tiles, one workgroup of 4
-// waves with 4 rows each (one wave per SIMD, 512 registers).  (The PIPE
-// template form -- tile k - 1's epilogue beside tile k's MFMAs -- spills at 512 registers with the weights in
-// VGPRs and is not instantiated.)
+// waves with 4 rows each (one wave per SIMD, 512 registers); 42 = form 4 with the half-tile pipeline (PIPE: each
+// half tile's MFMAs beside the other half's epilogue); 46 = form 4 with the rolling halo-row ring (ROLL).
 template <typename T, bool SI, bool EPI>
 int launch_c64r_form(const Conv3Args& a, hipStream_t s, int form) {
-    const int th = (form == 4 || form == 44 || form == 16) ? 4 : 8;
+    const int th = (form == 4 || form == 44 || form == 42 || form == 46) ? 4 : 8;
     const int tiles = a.N * (a.H / th) * (a.W / R_TW);
     const int ty = a.H / th;
     const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
-    if (form == 16)
-        return a.y_raw ? launch_c64w<T, SI, EPI, true>(a, s, tiles, num_cus(), band)
-                       : launch_c64w<T, SI, EPI, false>(a, s, tiles, num_cus(), band);
     if (form == 4) return launch_c64r_raw<T, SI, EPI, 4, 2>(a, s, tiles, 2 * num_cus(), band);
+    if (form == 42) return launch_c64r_raw<T, SI, EPI, 4, 2, true>(a, s, tiles, 2 * num_cus(), band);
+    if (form == 46) return launch_c64r_raw<T, SI, EPI, 4, 2, false, false, true>(a, s, tiles, 2 * num_cus(), ty);   // whole columns
     if (form == 44) return launch_c64r_raw<T, SI, EPI, 4, 2, false, true>(a, s, tiles, 2 * num_cus(), band);
     if (form == 84) return launch_c64r_raw<T, SI, EPI, 8, 4>(a, s, tiles, num_cus(), band);
     return launch_c64r_raw<T, SI, EPI, 8, 2>(a, s, tiles, num_cus(), band);
@@ -1512,15 +1316,15 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     // SG2_C64_RING: 0 off, else the ring form (launch_c64r_form: 4 default, 8, 84)
     const char* ring_env = getenv("SG2_C64_RING");   // read per launch: tests switch forms in one process
     const int ring = ring_env ? atoi(ring_env) : 4;
-    const int rth = (ring == 4 || ring == 44 || ring == 16) ? 4 : 8;
+    const int rth = (ring == 4 || ring == 44 || ring == 42 || ring == 46) ? 4 : 8;
     if (ring && !a.dot_out && a.Cin == P_C && a.Cout == P_C && a.H % rth == 0 && a.W % R_TW == 0 &&
         ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 && ((uintptr_t)a.noise % 16) == 0 &&
         ((uintptr_t)a.out_scale % 16) == 0 && ((uintptr_t)a.in_scale % 16) == 0 &&
         (!epi || (a.gain > 0.f && (a.act == 0 || (a.alpha >= 0.f && a.alpha <= 1.f))))) {
         const int tiles = a.N * (a.H / rth) * (a.W / R_TW);
-        const int grid = (rth == 4 && ring != 16 ? 2 : 1) * num_cus();
+        const int grid = (rth == 4 ? 2 : 1) * num_cus();
         if (tiles >= 2 * grid && tiles <= 128 * grid && a.N < 4096 && a.H / rth < 1024 && a.W / R_TW < 1024) {
-            const int form = (ring == 84 || ring == 44 || ring == 16) ? ring : rth;
+            const int form = (ring == 84 || ring == 44 || ring == 42 || ring == 46) ? ring : rth;
             if (si) { if (epi) return launch_c64r_form<T, true, true>(a, s, form); return launch_c64r_form<T, true, false>(a, s, form); }
             if (epi) return launch_c64r_form<T, false, true>(a, s, form);
             return launch_c64r_form<T, false, false>(a, s, form);

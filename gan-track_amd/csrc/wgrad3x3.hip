@@ -227,11 +227,10 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
 //     have a pitch of TW + 4 pixels (a multiple of 4; two pad columns never read), so bit 1 of a fragment row is
 //     a function of the lane and the tap column only and every fragment read is a per-lane base plus an
 //     immediate offset (the k-step loop is fully unrolled);
-//   * the modulation (g_scale / x_scale, one value per channel and sample) is constant over a tile (one sample),
-//     so it leaves the inner loop: the MFMAs accumulate the unscaled products of the current sample and, when the
-//     workgroup's tile run moves to the next sample (and at the end), the partial sums are folded into a second
-//     f32 set as tot += u[n, a] s[n, b] acc.  The reference rounds x * round(s) to 16 bits before its GEMM;
-//     this keeps the product in f32 (the difference is below the 16-bit rounding of the inputs).
+//   * the modulation (g_scale / x_scale, one value per channel and sample) leaves the inner loop: with a scale the
+//     host gives each workgroup tiles of ONE sample, and the partial sums are multiplied by u[n, a] s[n, b] at
+//     the final atomics.  The reference rounds x * round(s) to 16 bits before its GEMM; this keeps the product
+//     in f32 (the difference is below the 16-bit rounding of the inputs).
 // Stride 1, one phase holding every tap (3x3 pad 1, or 1x1 pad 0).
 template <int TW> struct WDma {
     static constexpr int TH = 256 / TW, HWD = TW + 4, HP = HWD * (TH + 2);
@@ -319,47 +318,20 @@ __global__ __launch_bounds__(256) void wgrad3x3_dma_kernel(W3Args a) {
     auto tap_dy = [](int tp) { return NT == 9 ? tp / 3 : 1; };
     auto tap_dx = [](int tp) { return NT == 9 ? tp % 3 : 1; };
 
-    f32x16 acc[NT], tot[SC ? NT : 1];
+    f32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
-    if (SC) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) tot[t][j] = 0.f;
-    }
     const int b = b0 + wb * 32 + (lane & 31);
-    // tot += u[n, a] s[n, b] acc; acc = 0   (a = a0 + 32 wa + 8 (j / 4) + 4 (lane >> 5) + j % 4)
-    auto fold = [&](int n) {
-        if constexpr (SC) {
-            const float sx = a.xscale ? a.xscale[n * B + min(b, B - 1)] : 1.f;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int ar = min(a0 + wa * 32 + 8 * (j >> 2) + 4 * hh + (j & 3), A - 1);
-                const float su = (a.gscale ? a.gscale[n * A + ar] : 1.f) * sx;
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    tot[t][j] = fmaf(acc[t][j], su, tot[t][j]);
-                    acc[t][j] = 0.f;
-                }
-            }
-        }
-    };
 
     issue(t_begin, 0);
     __builtin_amdgcn_s_waitcnt(0x0f70);                        // vmcnt(0): this wave's DMAs of the first tile
     __builtin_amdgcn_s_barrier();
-    int k = 0, cur_n = t_begin / per;
+    int k = 0;
     for (int t = t_begin; t < t_end; ++t, ++k) {
         const int stage = k & 1;
         if (t + 1 < t_end) issue(t + 1, stage ^ 1);            // the other stage was released by the last barrier
-        const int n = t / per;
-        if (SC && n != cur_n) {
-            fold(cur_n);
-            cur_n = n;
-        }
         const unsigned sa = lbase + stage * L::STAGE + abase;
         unsigned sb[3];
 #pragma unroll
@@ -392,16 +364,19 @@ __global__ __launch_bounds__(256) void wgrad3x3_dma_kernel(W3Args a) {
         __builtin_amdgcn_s_waitcnt(0x0070);                    // vmcnt(0) lgkmcnt(0)
         __builtin_amdgcn_s_barrier();
     }
-    fold(cur_n);
-
+    // SC: the host keeps every workgroup's tiles inside one sample, so the modulation u[n, a] s[n, b] is one
+    // factor per (a, b) on the whole sum
+    const int n0 = t_begin / per;
+    const float sx = (SC && a.xscale) ? a.xscale[n0 * B + min(b, B - 1)] : 1.f;
     if (b < B) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int ar = a0 + wa * 32 + 8 * (j >> 2) + 4 * hh + (j & 3);
             if (ar >= A) continue;
+            const float f = a.alpha * sx * ((SC && a.gscale) ? a.gscale[n0 * A + ar] : 1.f);
 #pragma unroll
             for (int t = 0; t < NT; ++t)
-                atomicAdd(a.dw + ((int64_t)ar * a.KK + (NT == 9 ? t : 0)) * B + b, (SC ? tot[t][j] : acc[t][j]) * a.alpha);
+                atomicAdd(a.dw + ((int64_t)ar * a.KK + (NT == 9 ? t : 0)) * B + b, acc[t][j] * f);
         }
     }
 }
@@ -630,9 +605,22 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
     splits = (int)cdiv(a.tiles, a.tiles_per_block);
     dim3 grid((unsigned)cdiv(A, BC), (unsigned)cdiv(B, BC), (unsigned)splits);
     // stride 1 with every tap in one phase: the LDS-DMA kernel (SG2_WGRAD_DMA=0 keeps the register-staged one)
-    // (with a modulation scale the second sum set spills: SG2_WGRAD_DMA=2 runs it anyway, for A/B timing)
+    // With a modulation scale every workgroup's tile range must lie inside one sample: tiles_per_block a divisor
+    // of the tiles per sample (at most doubling the workgroups), else the register-staged kernel runs.
     static const int dma_on = [] { const char* e = getenv("SG2_WGRAD_DMA"); return e ? atoi(e) : 1; }();
-    if (dma_on && (dma_on == 2 || (!gscale && !xscale)) && stride == 1 && ((KH == 3 && pad_y == 1 && pad_x == 1) || (KH == 1 && pad_y == 0 && pad_x == 0))) {
+    const bool scaled = gscale || xscale;
+    const int per_n = a.tiles_x * a.tiles_y;
+    bool sc_ok = !scaled;
+    if (scaled && dma_on) {
+        int tpb = std::min(a.tiles_per_block, per_n);
+        while (tpb > 1 && per_n % tpb) --tpb;
+        if (tpb * 2 >= a.tiles_per_block && tpb >= 4) {
+            a.tiles_per_block = tpb;
+            grid.z = (unsigned)cdiv(a.tiles, tpb);
+            sc_ok = true;
+        }
+    }
+    if (dma_on && sc_ok && stride == 1 && ((KH == 3 && pad_y == 1 && pad_x == 1) || (KH == 1 && pad_y == 0 && pad_x == 0))) {
         for (int ky = 0; ky < KH; ++ky)
             for (int kx = 0; kx < KW; ++kx)
                 a.taps[ky * KW + kx] = PTap{(int8_t)(ky - pad_y), (int8_t)(kx - pad_x), (int8_t)(ky * KW + kx), 0};

@@ -6,9 +6,9 @@ from collections import defaultdict
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
 ms = float(sys.argv[2])
-# the roofline measures 23 launches of the 256^2 layer (the persistent C=64 kernel since r02; the halo
-# kernel before) then 23 of the 32^2 layer (halo kernel) at the end of the run
-c64 = [r for r in rows if 'conv3x3_c64p' in r['Kernel_Name']]
+# the roofline measures 23 launches of the 256^2 layer (the ring C=64 kernel since r03, the persistent one in
+# r02, the halo kernel before) then 23 of the 32^2 layer (halo kernel) at the end of the run
+c64 = [r for r in rows if 'conv3x3_c64r' in r['Kernel_Name']] or [r for r in rows if 'conv3x3_c64p' in r['Kernel_Name']]
 halo = [r for r in rows if 'conv3x3_halo' in r['Kernel_Name']]
 if len(c64) > 23:
     t_end = int(c64[-23]['Start_Timestamp'])
@@ -19,7 +19,7 @@ win = [r for r in rows if t0 <= int(r['Start_Timestamp']) < t_end]
 
 
 def cat(n):
-    for key, name in [('conv3x3_c64p', 'halo conv 16-bit C=64 persistent'), ('conv3x3_halo', 'halo conv 16-bit'), ('wgrad3x3', 'halo wgrad 16-bit'),
+    for key, name in [('conv3x3_c64p', 'halo conv 16-bit C=64 persistent'), ('conv3x3_c64r', 'ring conv 16-bit C=64'), ('conv3x3_halo', 'halo conv 16-bit'), ('wgrad3x3', 'halo wgrad 16-bit'),
                       ('conv_fwd_kernel<float', 'generic conv f32'), ('conv_fwd_kernel', 'generic conv 16-bit'),
                       ('conv_wgrad_kernel<float', 'generic wgrad f32'), ('conv_wgrad_kernel', 'generic wgrad 16-bit'),
                       ('layer_bwd', 'layer_bwd'), ('bias_act', 'bias_act'), ('demod', 'demod'), ('Cijk', 'GEMM'),

@@ -48,7 +48,7 @@ if step pmc; then
     # HBM bytes of the roofline kernel: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots).
     for c in FETCH_SIZE WRITE_SIZE; do
         echo "== pmc $c"
-        timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex 'conv3x3_(halo|c64p)' -d "$O/pmc_$c" -o run \
+        timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex 'conv3x3_(halo|c64p|c64r)' -d "$O/pmc_$c" -o run \
             --output-format csv -- python3 "$R/tools/roofline_only.py" > "$O/pmc_$c.log" 2>&1
         rc=$?; tail -1 "$O/pmc_$c.log"; [ $rc -eq 0 ] || exit $rc
     done
