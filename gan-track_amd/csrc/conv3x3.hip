@@ -744,7 +744,7 @@ __device__ __forceinline__ void wait_vm() {           // s_waitcnt vmcnt(N) (gfx
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <typename T, bool SI, bool EPI, bool RAW, int R_TH, int WR, bool PIPE, bool STG, bool ROLL>
+template <typename T, bool SI, bool EPI, bool RAW, int R_TH, int WR, bool PIPE, bool STG>
 __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER_CU)) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
     typedef Ring<R_TH, WR> RG;
@@ -818,7 +818,6 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
                         }
                     }
                     wf[jj][tap][c] = v;
-                    if (PIPE && c == 1 && (tap % 3) == 2) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight
                 }
         }
     };
@@ -874,42 +873,6 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
         }
     };
 
-    // ROLL (round 3, form 46): the two slots are one ring of 2 (TH + 2) halo rows (row r at r * 5120 B) and a
-    // workgroup's run goes down whole image columns (band = the column), so a tile whose upper neighbour came just
-    // before it loads only its TH new halo rows; the TH + 2 rows of tile k sit at ring rows pos_k .. + TH + 1
-    // (mod 2 (TH + 2)), pos_{k+1} = pos_k + TH after a vertical neighbour, + TH + 2 after a jump (new column or
-    // sample: all rows fresh).  The rows a DMA overwrites are the complement of the current tile's (its
-    // predecessor's, released by the last barrier).  HBM reads of the halo drop from ~1.33x (the band's re-reads
-    // that miss in L2) toward the 34 / 32 of the side columns, and a third fewer DMA instructions per tile.
-    constexpr int RR = 2 * (R_TH + 2), ROWB = R_PITCH * 128;
-    auto issue_roll = [&](int t, bool succ, int pos, int eslot) {
-        if (SG2_RDIAG & 16) return;
-        int n, ty, tx;
-        tile_of(t, n, ty, tx);
-        const int hy0 = succ ? 2 : 0, n_i = (R_TH + 2 - hy0) * 5;
-#pragma unroll
-        for (int u = 0; u < (R_HALO_I + 1 + NW - 1) / NW; ++u) {
-            const int i = u * NW + wave;              // wave-uniform
-            if (i < n_i) {
-                const int hy = hy0 + i / 5, cg = i - (i / 5) * 5;
-                const int iy = ty - 1 + hy, ix0 = tx - 1 + cg * 8;
-                int rr = pos + hy;
-                rr = rr >= RR ? rr - RR : rr;
-                const int base = (unsigned)iy < (unsigned)a.H ? ((n * a.H + iy) * a.W + ix0) * 128 : -(1 << 30);
-                const bool kill = ((tx == 0) & (cg == 0) & (lx == 0)) | ((tx + R_TW == a.W) & (cg == 4) & (lx == 1)) |
-                                  ((cg == 4) & (lx >= 2));
-                const int off = kill ? -1 : base + hlane;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rxb, (lds_ptr_t)(smem_raw + rr * ROWB + cg * 1024), 16, off, 0, 0, 0);
-            } else if (i == n_i) {
-                const char* nb = has_noise ? epi_src0 + (int64_t)((n * a.H + ty) * a.W + tx) * (int)sizeof(T) : epi_src0;
-                const char* db = has_d ? epi_src1 + n * 256 : epi_src1;
-                const char* src = (lane < 32 ? nb : db) + elane;
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                                 (lds_ptr_t)(epil + eslot * R_EPI), 16, 0, 0);
-            }
-        }
-    };
-
     // MFMA B-fragment addressing: pixel fragment i of the wave at tap (ky, kx), chunk c reads position
     // (2 wr + (i >> 1) + ky) * 40 + (i & 1) * 16 + l16 + kx, piece c * 4 + q (swizzled as at the DMA)
     int boff[3][2];
@@ -918,7 +881,7 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int x = l16 + kx;
-            boff[kx][c] = ((ROLL ? 0 : WR * wr * R_PITCH) + x) * 128 + 16 * ((c * 4 + q) ^ (((x >> 1) & 3) << 1));
+            boff[kx][c] = (WR * wr * R_PITCH + x) * 128 + 16 * ((c * 4 + q) ^ (((x >> 1) & 3) << 1));
         }
 
     const float lr_alpha = (EPI && a.act == 1) ? a.alpha : 1.f;
@@ -1066,87 +1029,9 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
                         }
                 }
     };
-    // ROLL: halo row j of the wave (tile row 2 wr + j) at ring row pos + 2 wr + j
-    auto mfma_tile_roll = [&](f32x4 (&A)[NF][2], int pos) {
-        const char* rb[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            int rr = pos + WR * wr + j;
-            rr = rr >= RR ? rr - RR : rr;
-            rb[j] = smem_raw + rr * ROWB;
-        }
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < 3; ++kx) {
-                    v8<T> pf[NF];
-#pragma unroll
-                    for (int i = 0; i < NF; ++i)
-                        pf[i] = *(const v8<T>*)(rb[(i >> 1) + ky] + boff[kx][c] + (i & 1) * 16 * 128);
-                    const bool first = c == 0 && ky == 0 && kx == 0;
-#pragma unroll
-                    for (int i = 0; i < NF; ++i)
-#pragma unroll
-                        for (int jj = 0; jj < 2; ++jj)
-                            A[i][jj] = mma<T>(wf[jj][ky * 3 + kx][c], pf[i], first ? f32x4{0.f, 0.f, 0.f, 0.f} : A[i][jj]);
-                }
-    };
-
-    // (half-tile pipeline) the MFMAs of pixel fragments I0, I0 + 1 (one tile row of the wave) and their epilogue
-    auto mfma_half = [&](f32x4 (&A)[NF][2], const char* hb, auto i0c) {
-        constexpr int I0 = decltype(i0c)::value;
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < 3; ++kx) {
-                    v8<T> pf[2];
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const int i = I0 + u;
-                        pf[u] = *(const v8<T>*)(hb + boff[kx][c] + (((i >> 1) + ky) * R_PITCH + (i & 1) * 16) * 128);
-                    }
-                    const bool first = c == 0 && ky == 0 && kx == 0;
-#pragma unroll
-                    for (int u = 0; u < 2; ++u)
-#pragma unroll
-                        for (int jj = 0; jj < 2; ++jj)
-                            A[I0 + u][jj] = mma<T>(wf[jj][ky * 3 + kx][c], pf[u], first ? f32x4{0.f, 0.f, 0.f, 0.f} : A[I0 + u][jj]);
-                }
-    };
-    auto epi_half = [&](f32x4 (&A)[NF][2], auto i0c, int n, int ty, int tx, const float (&bb)[8], const float (&dd)[8],
-                        const float (&nz)[NF]) {
-        constexpr int I0 = decltype(i0c)::value;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int i = I0 + u;
-            const int r = WR * wr + (i >> 1), px = (i & 1) * 16 + l16;
-            const int pix = (n * a.H + ty + r) * a.W + tx + px;
-            vec8 yv, rv;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float cv = A[i][e >> 2][e & 3];
-                if (RAW) rv[e] = (T)cv;
-                float v = cv;
-                if (EPI) {
-                    v = fmaf(v, dd[e], nz[i] + bb[e]);
-                    v = fmaxf(v, v * lr_alpha);
-                    v = __builtin_amdgcn_fmed3f(v, -clampv, clampv);
-                }
-                yv[e] = (T)v;
-            }
-            const int dst = (pix * 64 + ch0) * (int)sizeof(T);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, dst, 0, 0);
-            if (RAW) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, dst, 0, 0);
-        }
-    };
 
     // ---- prologue: tiles 0 .. NSLOT - 2 in flight, wait for tile 0 ----
-    if (ROLL) issue_roll(t_begin, false, 0, 0);
-    else issue(t_begin, 0, 0);
+    issue(t_begin, 0, 0);
     if (R_NSLOT == 3) {
         issue(min(t_begin + 1, t_end - 1), 1, 1);
         wait_vm<R_DMA>();
@@ -1157,36 +1042,7 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     __builtin_amdgcn_s_barrier();
 
     int k = 0;
-    if constexpr (ROLL) {
-        static_assert(!ROLL || (R_NSLOT == 2 && !PIPE && !STG), "rolling rows: the plain 2-slot form");
-        f32x4 acc[NF][2];
-        int pos = 0;
-        for (int t = t_begin; t < t_end; ++t, ++k) {
-            int n, ty, tx;
-            tile_of(t, n, ty, tx);
-            int pos1 = pos;
-            if (t + 1 < t_end) {                      // tile t + 1 into the ring rows tile t does not use
-                int n1, ty1, tx1;
-                tile_of(t + 1, n1, ty1, tx1);
-                const bool succ = n1 == n && tx1 == tx && ty1 == ty + R_TH;
-                pos1 = pos + (succ ? R_TH : R_TH + 2);
-                pos1 = pos1 >= RR ? pos1 - RR : pos1;
-                issue_roll(t + 1, succ, pos1, (k + 1) % R_NEPI);
-            }
-            if (SI && n != cur_n) {
-                cur_n = n;
-                load_weights(n);
-            }
-            mfma_tile_roll(acc, pos);
-            float bb[8], dd[8], nz[NF];
-            epi_table(k % R_NEPI, bb, dd, nz);
-            epi_store(acc, n, ty, tx, bb, dd, nz);
-            wait_vm<S>();                             // tile t + 1's DMAs: younger are this iteration's stores
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_s_barrier();
-            pos = pos1;
-        }
-    } else if constexpr (!PIPE) {
+    if constexpr (!PIPE) {
         f32x4 acc[NF][2];
         for (int t = t_begin; t < t_end; ++t, ++k) {
             const int slot = k % R_NSLOT;
@@ -1213,18 +1069,15 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
             __builtin_amdgcn_s_barrier();
         }
     } else {
-        // Half-tile pipeline (round 3, PIPE, the 2-slot form): the wave's 4 pixel fragments are two halves (its two
-        // tile rows).  Each iteration runs in two phases, each one basic block of MFMAs for one half beside the
-        // epilogue of the other: phase 1 -- tile k's first half (fragments 0, 1) MFMAs | tile k - 1's second half
-        // epilogue; phase 2 -- tile k's second half (fragments 2, 3) MFMAs | tile k's first half epilogue.  The
-        // epilogue VALU and stores issue between MFMAs and the stores spread over the tile instead of bunching at
-        // its end, with the one accumulator set (a second set does not fit beside the 144 weight registers).
-        // Tile k's epilogue table (ring slot k % 4, rewritten by the DMAs of iteration k + 3) is read in both of
-        // its epilogue phases.
-        static_assert(!PIPE || (R_NSLOT == 2 && NF == 4), "half-tile pipeline: the 2-slot form");
-        f32x4 acc[NF][2];
-        int pn = 0, pty = 0, ptx = 0;
-        for (int t = t_begin; t < t_end; ++t, ++k) {
+        // Pipelined epilogue (3-slot form): iteration k runs tile k's MFMAs into one accumulator set and tile
+        // k - 1's epilogue from the other in the same basic block, so the epilogue's VALU and stores issue
+        // between MFMAs instead of after them.  The epilogue table of tile k - 1 (its epilogue-ring slot is
+        // rewritten three iterations later) is read at the top of the iteration.
+        static_assert(!PIPE || R_NSLOT == 3, "pipelined epilogue: 3-slot ring");
+        f32x4 acc0[NF][2], acc1[NF][2];
+        int t = t_begin, pn = 0, pty = 0, ptx = 0;
+        auto step = [&](auto has_prev, f32x4 (&Acur)[NF][2], f32x4 (&Aprev)[NF][2]) {
+            constexpr bool HP = decltype(has_prev)::value;
             const int slot = k % R_NSLOT;
             issue(min(t + R_NSLOT - 1, t_end - 1), (k + R_NSLOT - 1) % R_NSLOT, (k + R_NSLOT - 1) % R_NEPI);
             int n, ty, tx;
@@ -1233,37 +1086,41 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
                 cur_n = n;
                 load_weights(n);
             }
-            {   // phase 1
-                float bb[8], dd[8], nz[NF];
-                if (k > 0) epi_table((k + R_NEPI - 1) % R_NEPI, bb, dd, nz);
-                mfma_half(acc, smem_raw + slot * R_SLOT, std::integral_constant<int, 0>{});
-                if (k > 0) epi_half(acc, std::integral_constant<int, 2>{}, pn, pty, ptx, bb, dd, nz);
-            }
-            {   // phase 2
-                float bb[8], dd[8], nz[NF];
-                epi_table(k % R_NEPI, bb, dd, nz);
-                mfma_half(acc, smem_raw + slot * R_SLOT, std::integral_constant<int, 2>{});
-                epi_half(acc, std::integral_constant<int, 0>{}, n, ty, tx, bb, dd, nz);
-            }
-            // tile t + 1 (issued at the top of this iteration) must have landed; younger: this iteration's stores
-            // (half of them at k = 0)
-            if (k == 0) wait_vm<S / 2>();
-            else wait_vm<S>();
+            float bb[8], dd[8], nz[NF];
+            if (HP) epi_table((k + R_NEPI - 1) % R_NEPI, bb, dd, nz);
+            mfma_tile(Acur, smem_raw + slot * R_SLOT);
+            if (HP) epi_store(Aprev, pn, pty, ptx, bb, dd, nz);
+            // tile t + 1's DMAs (issued one iteration ago) must have landed; younger: the stores of the previous
+            // iteration (none at k = 1), this iteration's DMAs and its stores (none at k = 0)
+            if (k == 0) wait_vm<R_DMA>();
+            else if (k == 1) wait_vm<R_DMA + S>();
+            else wait_vm<R_DMA + 2 * S>();
             __builtin_amdgcn_s_waitcnt(0xc07f);
             __builtin_amdgcn_s_barrier();
             pn = n; pty = ty; ptx = tx;
+            ++k; ++t;
+        };
+        step(std::false_type{}, acc0, acc1);
+        bool last0 = true;                            // which set holds the last tile's sums
+        while (t < t_end) {
+            step(std::true_type{}, acc1, acc0);
+            last0 = false;
+            if (t >= t_end) break;
+            step(std::true_type{}, acc0, acc1);
+            last0 = true;
         }
         float bb[8], dd[8], nz[NF];
         epi_table((k + R_NEPI - 1) % R_NEPI, bb, dd, nz);
-        epi_half(acc, std::integral_constant<int, 2>{}, pn, pty, ptx, bb, dd, nz);
+        if (last0) epi_store(acc0, pn, pty, ptx, bb, dd, nz);
+        else epi_store(acc1, pn, pty, ptx, bb, dd, nz);
     }
     wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
 }
 
-template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, bool STG, bool ROLL>
+template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, bool STG>
 int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
     typedef Ring<TH, WR> RG;
-    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW, TH, WR, PIPE, STG, ROLL>;
+    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW, TH, WR, PIPE, STG>;
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RG::LDS);
@@ -1273,25 +1130,24 @@ int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band
     return launch_status("sg2_conv3x3 (c64 ring)");
 }
 
-template <typename T, bool SI, bool EPI, int TH, int WR, bool PIPE = false, bool STG = false, bool ROLL = false>
+template <typename T, bool SI, bool EPI, int TH, int WR, bool PIPE = false, bool STG = false>
 int launch_c64r_raw(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
-    return a.y_raw ? launch_c64r<T, SI, EPI, true, TH, WR, PIPE, STG, ROLL>(a, s, tiles, grid, band)
-                   : launch_c64r<T, SI, EPI, false, TH, WR, PIPE, STG, ROLL>(a, s, tiles, grid, band);
+    return a.y_raw ? launch_c64r<T, SI, EPI, true, TH, WR, PIPE, STG>(a, s, tiles, grid, band)
+                   : launch_c64r<T, SI, EPI, false, TH, WR, PIPE, STG>(a, s, tiles, grid, band);
 }
 
 // form: 4 = 32 x 4 tiles, two workgroups of 4 waves per CU; 8 = 32 x 8 tiles, one workgroup of 8 waves;
 // 44 = form 4 with whole-line stores staged through the consumed slot; 84 = 32 x 8 tiles, one workgroup of 4
-// waves with 4 rows each (one wave per SIMD, 512 registers); 42 = form 4 with the half-tile pipeline (PIPE: each
-// half tile's MFMAs beside the other half's epilogue); 46 = form 4 with the rolling halo-row ring (ROLL).
+// waves with 4 rows each (one wave per SIMD, 512 registers).  (The PIPE
+// template form -- tile k - 1's epilogue beside tile k's MFMAs -- spills at 512 registers with the weights in
+// VGPRs and is not instantiated.)
 template <typename T, bool SI, bool EPI>
 int launch_c64r_form(const Conv3Args& a, hipStream_t s, int form) {
-    const int th = (form == 4 || form == 44 || form == 42 || form == 46) ? 4 : 8;
+    const int th = (form == 4 || form == 44) ? 4 : 8;
     const int tiles = a.N * (a.H / th) * (a.W / R_TW);
     const int ty = a.H / th;
     const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
     if (form == 4) return launch_c64r_raw<T, SI, EPI, 4, 2>(a, s, tiles, 2 * num_cus(), band);
-    if (form == 42) return launch_c64r_raw<T, SI, EPI, 4, 2, true>(a, s, tiles, 2 * num_cus(), band);
-    if (form == 46) return launch_c64r_raw<T, SI, EPI, 4, 2, false, false, true>(a, s, tiles, 2 * num_cus(), ty);   // whole columns
     if (form == 44) return launch_c64r_raw<T, SI, EPI, 4, 2, false, true>(a, s, tiles, 2 * num_cus(), band);
     if (form == 84) return launch_c64r_raw<T, SI, EPI, 8, 4>(a, s, tiles, num_cus(), band);
     return launch_c64r_raw<T, SI, EPI, 8, 2>(a, s, tiles, num_cus(), band);
@@ -1316,7 +1172,7 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     // SG2_C64_RING: 0 off, else the ring form (launch_c64r_form: 4 default, 8, 84)
     const char* ring_env = getenv("SG2_C64_RING");   // read per launch: tests switch forms in one process
     const int ring = ring_env ? atoi(ring_env) : 4;
-    const int rth = (ring == 4 || ring == 44 || ring == 42 || ring == 46) ? 4 : 8;
+    const int rth = (ring == 4 || ring == 44) ? 4 : 8;
     if (ring && !a.dot_out && a.Cin == P_C && a.Cout == P_C && a.H % rth == 0 && a.W % R_TW == 0 &&
         ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 && ((uintptr_t)a.noise % 16) == 0 &&
         ((uintptr_t)a.out_scale % 16) == 0 && ((uintptr_t)a.in_scale % 16) == 0 &&
@@ -1324,7 +1180,7 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         const int tiles = a.N * (a.H / rth) * (a.W / R_TW);
         const int grid = (rth == 4 ? 2 : 1) * num_cus();
         if (tiles >= 2 * grid && tiles <= 128 * grid && a.N < 4096 && a.H / rth < 1024 && a.W / R_TW < 1024) {
-            const int form = (ring == 84 || ring == 44 || ring == 42 || ring == 46) ? ring : rth;
+            const int form = (ring == 84 || ring == 44) ? ring : rth;
             if (si) { if (epi) return launch_c64r_form<T, true, true>(a, s, form); return launch_c64r_form<T, true, false>(a, s, form); }
             if (epi) return launch_c64r_form<T, false, true>(a, s, form);
             return launch_c64r_form<T, false, false>(a, s, form);

@@ -326,6 +326,9 @@ class Trainer:
         """One iteration.  phase_real_img/c: lists of batch_gpu chunks; all_gen_z/c: per phase, lists
         of chunks (the reference's data layout, :317-323)."""
         self._serial += 1
+        if self.graphs and getattr(self.loss, 'blur_fade_kimg', 0) > 0 and getattr(self.loss, 'blur_init_sigma', 0) > 0:
+            # the D-input blur fades with cur_nimg, a host float a captured phase would freeze: stay eager
+            self.graphs = False
         active = [(ph, gz, gc) for ph, gz, gc in zip(self.phases, all_gen_z, all_gen_c)
                   if self.batch_idx % ph.interval == 0]
         ready = self.graphs and self.on_grads is None and all(

@@ -1,0 +1,57 @@
+"""One trainer per process (GPU): the Claro 32^2 test network for 6 iterations (reg intervals 2) in eager or graph
+mode (graphs from iteration 1), parameters saved to gpurun_out/single_<mode>.pt; `compare` prints the largest
+difference between the two files.  Separates a graph replay's own result from interference by another trainer's
+eager work in the same process (tools/graph_replay_check.py).  Usage: python tools/graph_single.py eager|graph|compare"""
+import copy
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, 'tests'), os.path.join(ROOT, 'tests', 'golden'), os.path.join(ROOT, 'gan-track_amd'), ROOT]
+OUT = os.path.join(ROOT, 'gpurun_out')
+mode = sys.argv[1]
+if mode == 'compare':
+    a = torch.load(os.path.join(OUT, 'single_eager.pt'), weights_only=True)
+    b = torch.load(os.path.join(OUT, 'single_graph.pt'), weights_only=True)
+    diffs = sorted(((float((a[k] - b[k]).abs().max()), k) for k in a), reverse=True)
+    num = sum(float((a[k] - b[k]).double().square().sum()) for k in a) ** 0.5
+    den = sum(float(a[k].double().square().sum()) for k in a) ** 0.5
+    print(f'graph vs eager, separate processes: rel L2 {num / den:.3g}; worst {diffs[:4]}')
+    sys.exit(0)
+from golden_util import load  # noqa: E402
+from parity_train import build_product, CLARO_AUG  # noqa: E402
+from training import augment_mi, loss as loss_mod, trainer as trainer_mod  # noqa: E402
+
+dev = torch.device('cuda', 0)
+z = load('train_claro.npz')
+cfg, G, D = build_product(z, dev, False)
+G_ema = copy.deepcopy(G).eval()
+aug = augment_mi.AugmentPipe(run_dir=None, batch_size=cfg['batch'], **CLARO_AUG).train().requires_grad_(False).to(dev)
+aug.p.copy_(torch.as_tensor(0.3))
+loss = loss_mod.StyleGAN2Loss(device=dev, G=G, D=D, augment_pipe=aug, r1_gamma=0.4096, style_mixing_prob=0.9,
+                              pl_weight=2, pl_no_weight_grad=True)
+opt = dict(class_name='torch.optim.Adam', lr=0.0025, betas=[0, 0.99], eps=1e-8)
+tr = trainer_mod.Trainer(G, D, G_ema, loss, opt, opt, G_reg_interval=2, D_reg_interval=2, batch_size=cfg['batch'],
+                         batch_gpu=cfg['batch'], num_gpus=1, rank=0, device=dev, overlap=False, bucket_mb=32)
+gen = torch.Generator(device=dev)
+gen.manual_seed(5)
+BENCH = os.environ.get('BENCH_FLOW') == '1'      # bench.py's flow: all four phases captured in one step
+for it in range(6):
+    if it == 1:
+        tr.graphs = mode == 'graph'
+        if BENCH:
+            tr.batch_idx = 0
+    real = torch.rand([cfg['batch'], 1, 32, 32], device=dev, generator=gen) * 2 - 1
+    c = torch.nn.functional.one_hot(torch.randint(0, 2, [cfg['batch']], device=dev, generator=gen), 2).float()
+    gz = torch.randn([4, cfg['batch'], cfg['z_dim']], device=dev, generator=gen)
+    torch.manual_seed(123 + it)
+    tr.step([real], [c], [[gz[i]] for i in range(4)], [[c] for _ in range(4)])
+torch.cuda.synchronize()
+os.makedirs(OUT, exist_ok=True)
+torch.save({f'{pre}.{n}': p.detach().cpu() for pre, m in (('G', G), ('D', D), ('G_ema', G_ema))
+            for n, p in m.named_parameters()}, os.path.join(OUT, f'single_{mode}.pt'))
+if tr.graphs:
+    print('captured phases:', sorted(tr._graphs), flush=True)
+print(f'{mode}: saved', flush=True)
