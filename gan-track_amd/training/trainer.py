@@ -221,6 +221,8 @@ class Trainer:
         self._real_staged = None       # the step (self._serial) whose real batch is in it
         self._serial = 0               # step() calls so far (batch_idx may be reset by the caller)
 
+    graph_opt = True     # the FlatAdam launch joins the phase graph (False: stepped eagerly after the replay)
+
     @staticmethod
     def _passes(name):
         return 2 if name in ('Dmain', 'Dboth') else 1    # D phases backward once for fakes, once for reals
@@ -256,7 +258,7 @@ class Trainer:
             # the optimiser launch joins the graph when the participation set learned by the eager warm-up
             # step is known: its tables and step-scalar buffer are built here, outside the capture
             part0 = ex.expect.get(phase.name)
-            st.opt_in_graph = fused_opt and part0 is not None
+            st.opt_in_graph = fused_opt and part0 is not None and self.graph_opt
             if st.opt_in_graph:
                 phase.opt._table(flat, ex.offsets, part0, phase.name)
                 if phase.opt.exp_avg is None:
