@@ -59,8 +59,8 @@ def parse():
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--phase-timing', action='store_true')
     ap.add_argument('--graphs', default='auto', choices=['auto', 'on', 'off'],
-                    help='HIP-graph replay of each phase (auto: off -- replayed phase graphs drift from the eager '
-                         'iteration after their first replay, DESIGN.md section 6; on: the captured form for A/B)')
+                    help='HIP-graph replay of each phase (auto: on for one GPU; with several GPUs the eager path, '
+                         'whose bucketed all_reduces overlap the backward from post-accumulate hooks)')
     ap.add_argument('--no-graphs', action='store_true', help='same as --graphs off')
     return ap.parse_args()
 
@@ -273,9 +273,7 @@ def main():
     real, real_c = make_inputs(args, device, rank)
     for _ in range(args.warmup):
         one_step(tr, args, device, real, real_c)
-    # (auto = eager: tools/graph_single.py measured the graph-mode parameters 5.6e-5 (rel L2) off the eager
-    # iteration's after 6 steps, the eager run reproducible across processes -- not a rounding difference)
-    graphs = args.graphs == 'on' and not args.no_graphs
+    graphs = (args.graphs == 'on' or (args.graphs == 'auto' and num_gpus == 1)) and not args.no_graphs
     if graphs:
         # capture: one untimed step at batch_idx 0 runs (and captures) all four phases; afterwards every
         # phase is a single HIP-graph replay (trainer.py Trainer.graphs; with several GPUs the bucket

@@ -1364,7 +1364,7 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
         const bool split = splits > 1;
         const bool clean = workspace_clean();
         if (split && !clean) {
-            hipError_t e = hipMemsetAsync(workspace, 0, total_out * sizeof(float), s);
+            hipError_t e = zero_fill(workspace, total_out * sizeof(float), s);
             if (e != hipSuccess) { set_error("sg2_conv2d: memset failed"); return (int)e; }
         }
         for (int g0 = 0; g0 < nph && rc == 0; g0 += kMaxPhases) {

@@ -217,7 +217,7 @@ int gs_bwd(float* gin, const void* gout, const float* grid, const float* theta, 
         int rc = launch_status("sg2_grid_sample_bwd zero");
         if (rc) return rc;
     } else {
-        hipError_t e = hipMemsetAsync(gin, 0, extent * sizeof(float), s);
+        hipError_t e = zero_fill(gin, extent * sizeof(float), s);
         if (e != hipSuccess) { set_error("sg2_grid_sample_bwd: memset failed"); return (int)e; }
     }
     const int64_t total = (int64_t)p.N * p.Ho * p.Wo;

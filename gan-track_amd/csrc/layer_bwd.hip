@@ -333,7 +333,7 @@ extern "C" int sg2_dot_hw(float* out, const void* a, const void* b, int dtype, i
     SG2_CHECK(((uintptr_t)a % 16) == 0 && ((uintptr_t)b % 16) == 0, "sg2_dot_hw: 16-byte alignment required");
     if ((int64_t)N * HW == 0) return 0;
     hipStream_t s = as_stream(stream);
-    hipError_t e = hipMemsetAsync(out, 0, (int64_t)N * C * sizeof(float), s);
+    hipError_t e = zero_fill(out, (int64_t)N * C * sizeof(float), s);
     if (e) { set_error("sg2_dot_hw: memset failed"); return e; }
     const int PPP = std::max(1, 256 / (C / 8));
     const int ppb = std::min(HW, PPP * 32);

@@ -233,6 +233,25 @@ __global__ __launch_bounds__(256) void infnorm_bwd_kernel(float* __restrict__ dt
 }
 
 }  // namespace
+
+__global__ void zero_fill_kernel(unsigned char* p, size_t bytes) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t head = (16 - ((uintptr_t)p & 15)) & 15;
+    if (head > bytes) head = bytes;
+    for (size_t k = i; k < head; k += stride) p[k] = 0;
+    const size_t nv = (bytes - head) / 16;
+    uint4* v = reinterpret_cast<uint4*>(p + head);
+    for (size_t k = i; k < nv; k += stride) v[k] = make_uint4(0u, 0u, 0u, 0u);
+    for (size_t k = head + nv * 16 + i; k < bytes; k += stride) p[k] = 0;
+}
+
+hipError_t zero_fill(void* p, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    const int g = (int)std::min<int64_t>(cdiv((int64_t)(bytes / 16 + 1), 256), 2048);
+    zero_fill_kernel<<<g, 256, 0, s>>>(static_cast<unsigned char*>(p), bytes);
+    return hipGetLastError();
+}
 }  // namespace sg2
 
 extern "C" int sg2_demod_fwd(float* d, float* wsq, const float* s, const float* w, int N, int O, int I, int KK,

@@ -34,8 +34,14 @@ bool accumulators_prezeroed();
 // sg2_set_clean_workspace(1): the split-K workspace passed to the conv entry points is zero on entry, and the
 // call leaves it zero (its finalize clears what it read) -- no memset per split-K call.
 bool workspace_clean();
+// Zero `bytes` bytes at p on stream s with a kernel.  Not hipMemsetAsync: the library's memsets captured into
+// a phase graph (accumulators allocated inside the capture, memsets issued from the backward) took effect on
+// the first replay only, so every later replay added into the previous one's sums (tools/greg_replay_check.py:
+// second replay inf / NaN, 7e-7 with this kernel).  A stand-alone memset node replays correctly
+// (tools/memset_graph_check.py); kernel nodes replay every time.
+hipError_t zero_fill(void* p, size_t bytes, hipStream_t s);
 inline hipError_t zero_acc(void* p, size_t bytes, hipStream_t s) {
-    return accumulators_prezeroed() ? hipSuccess : hipMemsetAsync(p, 0, bytes, s);
+    return accumulators_prezeroed() ? hipSuccess : zero_fill(p, bytes, s);
 }
 
 inline int launch_status(const char* what) {

@@ -258,7 +258,8 @@ class Trainer:
             # the optimiser launch joins the graph when the participation set learned by the eager warm-up
             # step is known: its tables and step-scalar buffer are built here, outside the capture
             part0 = ex.expect.get(phase.name)
-            st.opt_in_graph = fused_opt and part0 is not None and self.graph_opt
+            # (a phase without gradients -- e.g. Greg with pl_weight 0 -- has no Adam launch to capture)
+            st.opt_in_graph = fused_opt and bool(part0) and self.graph_opt
             if st.opt_in_graph:
                 phase.opt._table(flat, ex.offsets, part0, phase.name)
                 if phase.opt.exp_avg is None:

@@ -91,9 +91,6 @@ class _FakeWork:
         pass
 
 
-@pytest.mark.xfail(strict=False, reason='known issue (DESIGN.md section 6): a replayed phase graph drifts from the '
-                   'eager iteration after its first replay (tools/graph_single.py, tools/graph_replay_check.py); '
-                   'bench.py runs eager by default')
 def test_graph_exchange_overlap_simulated_ranks(monkeypatch):
     """Two ranks simulated on one GPU: all_reduce(t) -> t *= 2 (the sum of two identical ranks) on the
     stream it is issued on.  Eager hook path, graph path (fills and reductions captured from the hooks)

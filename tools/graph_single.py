@@ -2,7 +2,8 @@
 mode (graphs from iteration 1), parameters saved to gpurun_out/single_<mode>.pt; `compare` prints the largest
 difference between the two files.  Separates a graph replay's own result from interference by another trainer's
 eager work in the same process (tools/graph_replay_check.py).  Usage: [TAG=_x] python tools/graph_single.py eager|graph, python tools/graph_single.py compare eager_x graph_x;
-env NO_RNG=1 (no random draws matter), GRAPH_OPT=0 (Adam stepped after the replay), SG2_BLAS=cublas|cublaslt"""
+env OFF=aug,mix,pl,noise (parts switched off), NO_RNG=1 (all four), GRAPH_OPT=0 (Adam stepped after the replay), SG2_BLAS=cublas|cublaslt,
+GRAPH_SKIP=Gmain,... (phases kept eager in graph mode)"""
 import copy
 import os
 import sys
@@ -32,18 +33,36 @@ z = load('train_claro.npz')
 cfg, G, D = build_product(z, dev, False)
 G_ema = copy.deepcopy(G).eval()
 aug = augment_mi.AugmentPipe(run_dir=None, batch_size=cfg['batch'], **CLARO_AUG).train().requires_grad_(False).to(dev)
-NO_RNG = os.environ.get('NO_RNG') == '1'          # results independent of the random draws (RNG suspicion)
-aug.p.copy_(torch.as_tensor(0.0 if NO_RNG else 0.3))
+# OFF: what to switch off, comma-separated from aug (ADA p = 0), mix (no style mixing), pl (pl_weight 0: no Greg),
+# noise (constant synthesis noise); NO_RNG=1 is all four (every random draw then leaves the results unchanged)
+OFF = set(filter(None, os.environ.get('OFF', 'aug,mix,pl,noise' if os.environ.get('NO_RNG') == '1' else '').split(',')))
+aug.p.copy_(torch.as_tensor(0.0 if 'aug' in OFF else 0.3))
 loss = loss_mod.StyleGAN2Loss(device=dev, G=G, D=D, augment_pipe=aug, r1_gamma=0.4096,
-                              style_mixing_prob=0.0 if NO_RNG else 0.9, pl_weight=0 if NO_RNG else 2,
+                              style_mixing_prob=0.0 if 'mix' in OFF else 0.9, pl_weight=0 if 'pl' in OFF else 2,
                               pl_no_weight_grad=True)
-if NO_RNG:
+if os.environ.get('PLCONST') == '1':     # the path-length pass's y = randn_like(img) replaced by a fixed pattern
+    loss_mod.torch = type('T', (), {k: getattr(torch, k) for k in dir(torch) if not k.startswith('__')})()
+    loss_mod.torch.randn_like = lambda t: torch.sin(torch.arange(t.numel(), device=t.device, dtype=t.dtype)).reshape(t.shape)
+if 'noise' in OFF:
     _fwd = G.synthesis.forward
     G.synthesis.forward = lambda ws, **kw: _fwd(ws, **{**kw, 'noise_mode': 'const'})
 opt = dict(class_name='torch.optim.Adam', lr=0.0025, betas=[0, 0.99], eps=1e-8)
 tr = trainer_mod.Trainer(G, D, G_ema, loss, opt, opt, G_reg_interval=2, D_reg_interval=2, batch_size=cfg['batch'],
                          batch_gpu=cfg['batch'], num_gpus=1, rank=0, device=dev, overlap=False, bucket_mb=32)
 tr.graph_opt = os.environ.get('GRAPH_OPT', '1') == '1'
+_skip = set(filter(None, os.environ.get('GRAPH_SKIP', '').split(',')))   # phases kept eager in graph mode
+if _skip:
+    _orig = trainer_mod.Trainer._graph_phase
+
+    def _graph_phase(self, phase, ri, rc, gz, gc):
+        if phase.name not in _skip:
+            return _orig(self, phase, ri, rc, gz, gc)
+        phase.opt.zero_grad(set_to_none=True)
+        phase.module.requires_grad_(True)
+        self._accumulate(phase, ri, rc, gz, gc)
+        phase.module.requires_grad_(False)
+        return phase.exchange.finish(phase.name, None), False
+    trainer_mod.Trainer._graph_phase = _graph_phase
 gen = torch.Generator(device=dev)
 gen.manual_seed(5)
 BENCH = os.environ.get('BENCH_FLOW') == '1'      # bench.py's flow: all four phases captured in one step
