@@ -23,7 +23,7 @@ def cat(n):
                       ('conv_fwd_kernel<float', 'generic conv f32'), ('conv_fwd_kernel', 'generic conv 16-bit'),
                       ('conv_wgrad_kernel<float', 'generic wgrad f32'), ('conv_wgrad_kernel', 'generic wgrad 16-bit'),
                       ('layer_bwd', 'layer_bwd'), ('bias_act', 'bias_act'), ('demod', 'demod'), ('Cijk', 'GEMM'),
-                      ('conv_finalize', 'conv finalize'), ('rocclr', 'memset/copy'), ('multi_tensor', 'optimizer'),
+                      ('conv_finalize', 'conv finalize'), ('rocclr', 'memset/copy'), ('zero_fill', 'memset/copy'), ('multi_tensor', 'optimizer'),
                       ('adam_multi', 'optimizer'), ('lerp_multi', 'optimizer'),
                       ('pack_weight', 'weight pack'), ('infnorm', 'fp16 pre-normalisation')]:
         if key in n:
