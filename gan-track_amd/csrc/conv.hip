@@ -57,6 +57,9 @@ struct Epi {
     void* aux;               // [N, OH, OW, Cout] (T): aux_mode 1 = conv result, 2 = activation before residual
     const void* dot_src;     // [N, OH, OW, Cout] (T): dot_out[n, o] += sum_p c * dot_src
     float* dot_out;          // [N, Cout] float, zeroed by the host
+    float* det_dot;          // deterministic mode: the dot's contributions by slot instead of atomics --
+                             // [N * OH * OW][Cout] per-element products (conv_fwd / finalize), or
+                             // [gridDim.x][N][Cout] workgroup partials (conv1x1_smallk_dot)
     float noise_gain, alpha, gain, clamp;
     int act, aux_mode, on;
 };
@@ -73,6 +76,7 @@ struct ConvArgs {
     int wtaps;               // taps per output channel in the packed weight (KH*KW)
     int nck;                 // ceil(Cin / BK)
     int splits, kper;        // K split: kper chunks per split
+    int64_t det_stride;      // deterministic mode: split s stores its partial sums at acc + s * det_stride
     Phase ph[kMaxPhases];
     Tap taps[kMaxTaps];
 };
@@ -340,6 +344,14 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_dot_kernel(ConvArgs a) {
         *(vec8*)((T*)a.y + pix * a.Cout + o0) = yo;
     }
     __syncthreads();
+    if (a.e.det_dot) {
+        // rows of PPI lanes' partials, summed in row order; one slot per workgroup
+        det_rows_store(red, a.Cout, threadIdx.x / OG, o0, dacc);
+        __syncthreads();
+        for (int i = threadIdx.x; i < a.Cout; i += 256)
+            a.e.det_dot[((int64_t)blockIdx.x * gridDim.y + n) * a.Cout + i] = det_rows_sum(red, a.Cout, PPI, i);
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) atomicAdd(&red[o0 + j], dacc[j]);
     __syncthreads();
@@ -633,12 +645,15 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
                     if (o >= a.Cout) continue;
                     const float c = acc[i][j][r];
                     if (SPLIT) {
-                        atomicAdd(a.acc + pix * a.Cout + o, c);
+                        if (a.det_stride) a.acc[split * a.det_stride + pix * a.Cout + o] = c;
+                        else atomicAdd(a.acc + pix * a.Cout + o, c);
                     } else {
                         float v = c;
-                        if (a.e.dot_out)
-                            atomicAdd(a.e.dot_out + (int64_t)n * a.Cout + o,
-                                      c * (float)((const T*)a.e.dot_src)[pix * a.Cout + o]);
+                        if (a.e.dot_out) {
+                            const float pr = c * (float)((const T*)a.e.dot_src)[pix * a.Cout + o];
+                            if (a.e.det_dot) a.e.det_dot[pix * a.Cout + o] = pr;
+                            else atomicAdd(a.e.dot_out + (int64_t)n * a.Cout + o, pr);
+                        }
                         if (a.e.on) {
                             v = epi_full<T>(a.e, c, n, o, pix, a.Cout);
                             if (a.e.aux_mode == 1) ((T*)a.e.aux)[pix * a.Cout + o] = (T)c;
@@ -660,6 +675,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
     float* red = (float*)(lds + 2 * BM * OS);   // [EH] dot partial sums
     const bool want_aux = a.e.on && a.e.aux_mode != 0;
     const bool want_dot = a.e.dot_out != nullptr;
+    const bool det_dot = a.e.det_dot != nullptr;
     const bool keep_c = want_aux || want_dot;
     // the dot reduction goes through LDS when the whole tile belongs to one sample
     const int n_first = m0 / per, n_last = (min(m0 + BM, M) - 1) / per;
@@ -724,7 +740,8 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
                 const int64_t src = (((int64_t)n * a.OH + oy) * a.OW + ox) * a.Cout + o;
                 for (int e = 0; e < 8 && o + e < a.Cout; ++e) {
                     const float pr = (float)xt[ml * OS + c8 + e] * (float)((const T*)a.e.dot_src)[src + e];
-                    if (dot_uniform) dacc[e] += pr;
+                    if (det_dot) a.e.det_dot[src + e] = pr;
+                    else if (dot_uniform) dacc[e] += pr;
                     else atomicAdd(a.e.dot_out + (int64_t)n * a.Cout + o + e, pr);
                 }
             }
@@ -750,7 +767,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
                 }
             }
         }
-        if (want_dot && dot_uniform) {
+        if (want_dot && dot_uniform && !det_dot) {
             const int c8 = (tid % CPR) * 8;
 #pragma unroll
             for (int e = 0; e < 8; ++e) atomicAdd(&red[c8 + e], dacc[e]);
@@ -771,7 +788,9 @@ __global__ void conv_finalize_kernel(T* y, float* src, Epi e, int64_t n_el, int 
         if (e.dot_out) {
             const int64_t pix = i / Cout;
             const int o = (int)(i - pix * Cout);
-            atomicAdd(e.dot_out + (pix / pix_per_n) * Cout + o, c * (float)((const T*)e.dot_src)[i]);
+            const float pr = c * (float)((const T*)e.dot_src)[i];
+            if (e.det_dot) e.det_dot[i] = pr;
+            else atomicAdd(e.dot_out + (pix / pix_per_n) * Cout + o, pr);
         }
         if (e.on) {
             const int64_t pix = i / Cout;
@@ -843,6 +862,7 @@ struct WgradArgs {
     int kper;        // pixels per split (multiple of BK)
     int splits;
     float alpha;     // dw += alpha * (partial sums): a layer's weight gain folded in
+    float* det;      // deterministic mode: partial sums by slot (split / lane row), summed by det_sum
 };
 
 template <typename T>
@@ -898,6 +918,16 @@ __global__ __launch_bounds__(256) void wgrad1x1_smallb_kernel(WgradArgs a) {
             for (int k = 0; k < 4; ++k) acc[j][k] += gj * xv[k];
         }
     }
+    if (a.det) {
+        // one slot per row of OG lanes (every lane of a row owns 8 distinct a): [row][A][B]
+        const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / OG;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < a.B) a.det[row * a.A * a.B + (a0 + j) * a.B + k] = acc[j][k] * a.alpha;
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
@@ -944,6 +974,15 @@ __global__ __launch_bounds__(256) void wgrad1x1_smalla_kernel(WgradArgs a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) acc[k][j] += gk[k] * xj;
         }
+    }
+    if (a.det) {
+        const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / BG;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (k < a.A) a.det[row * a.A * a.B + k * a.B + b0 + j] = acc[k][j] * a.alpha;
+        return;
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -1195,7 +1234,10 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int bc = b0 + wn * WN + j * 16 + (lane & 15);
-                if (bc < a.B) atomicAdd(a.dw + ((int64_t)ar * KK + tap) * a.B + bc, acc[i][j][r] * a.alpha);
+                if (bc >= a.B) continue;
+                const int64_t di = ((int64_t)ar * KK + tap) * a.B + bc;
+                if (a.det) a.det[(int64_t)split * a.A * KK * a.B + di] = acc[i][j][r] * a.alpha;
+                else atomicAdd(a.dw + di, acc[i][j][r] * a.alpha);
             }
         }
 }
@@ -1214,6 +1256,9 @@ int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
     int splits = (int)std::max<int64_t>(1, std::min<int64_t>(chunks / 8, cdiv(target, (int64_t)mt * nt * KK)));
     a.kper = (int)cdiv(chunks, splits) * BK;
     a.splits = (int)cdiv(a.M, a.kper);
+    DetArena arena;
+    const int64_t nel = (int64_t)a.A * KK * a.B;
+    if (det_on()) SG2_DET_GET(a.det, arena, a.splits * nel, "sg2_conv2d_wgrad");
     dim3 grid(mt, nt, KK * a.splits);
     if (s3) {
         if (vec) conv_wgrad_kernel<T, BM, BN, true, F32><<<grid, 256, 0, s>>>(a);
@@ -1222,7 +1267,11 @@ int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
         if (vec) conv_wgrad_kernel<T, BM, BN, true, false><<<grid, 256, 0, s>>>(a);
         else conv_wgrad_kernel<T, BM, BN, false, false><<<grid, 256, 0, s>>>(a);
     }
-    return launch_status("sg2_conv2d_wgrad");
+    int rc = launch_status("sg2_conv2d_wgrad");
+    if (rc || !a.det) return rc;
+    hipError_t e = det_sum(a.dw, 0, a.det, 0, nel, 1, a.splits, nel, arena, s);
+    if (e) { set_error("sg2_conv2d_wgrad: det_sum"); return (int)e; }
+    return 0;
 }
 
 int floordiv_h(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
@@ -1330,8 +1379,15 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
         if (base.e.dot_out) {
             const int ppb = SK_ITERS * (256 / (Cout / 8));
             dim3 g((unsigned)cdiv((int64_t)H * W, ppb), (unsigned)N);
+            DetArena arena;
+            if (det_on()) SG2_DET_GET(base.e.det_dot, arena, (int64_t)g.x * N * Cout, "sg2_conv2d (1x1, small Cin, dot)");
             SG2_DISPATCH(dtype, T, { conv1x1_smallk_dot_kernel<T><<<g, 256, 0, s>>>(base); });
-            return launch_status("sg2_conv2d (1x1, small Cin, dot)");
+            int rc1 = launch_status("sg2_conv2d (1x1, small Cin, dot)");
+            if (rc1 || !base.e.det_dot) return rc1;
+            hipError_t e = det_sum(base.e.dot_out, 0, base.e.det_dot, 0, (int64_t)N * Cout, 1, g.x, (int64_t)N * Cout,
+                                   arena, s);
+            if (e) { set_error("sg2_conv2d: det_sum"); return (int)e; }
+            return 0;
         }
         const int64_t total = (int64_t)N * H * W * (Cout / 8);
         const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 64);
@@ -1363,13 +1419,26 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
             splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(target, blocks), maxnk / 4));
         const bool split = splits > 1;
         const bool clean = workspace_clean();
-        if (split && !clean) {
-            hipError_t e = zero_fill(workspace, total_out * sizeof(float), s);
+        // deterministic mode: split s writes its partial sums to slot s, det_sum adds the slots in order into a
+        // zeroed arena buffer that the finalize reads; the dot's per-element products go to det_dot
+        DetArena arena;
+        float* det_acc = nullptr;
+        float* acc_src = workspace;
+        if (det_on()) {
+            if (base.e.dot_out) SG2_DET_GET(base.e.det_dot, arena, total_out, "sg2_conv2d");
+            if (split) {
+                SG2_DET_GET(det_acc, arena, (int64_t)splits * total_out, "sg2_conv2d");
+                SG2_DET_GET(acc_src, arena, total_out, "sg2_conv2d");
+            }
+        }
+        if (split && (!clean || det_acc)) {
+            hipError_t e = zero_fill(acc_src, total_out * sizeof(float), s);
             if (e != hipSuccess) { set_error("sg2_conv2d: memset failed"); return (int)e; }
         }
         for (int g0 = 0; g0 < nph && rc == 0; g0 += kMaxPhases) {
             ConvArgs a = base;
-            a.acc = split ? workspace : nullptr;
+            a.acc = split ? (det_acc ? det_acc : workspace) : nullptr;
+            a.det_stride = det_acc ? total_out : 0;
             a.splits = splits;
             a.kper = (int)cdiv(maxnk, splits);
             int nt = 0;
@@ -1388,10 +1457,19 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
             else rc = launch_fwd<T, 128, 64>(a, vec, s);
         }
         if (rc == 0 && split) {
+            if (det_acc) {
+                hipError_t e = det_sum(acc_src, 0, det_acc, 0, total_out, 1, splits, total_out, arena, s);
+                if (e) { set_error("sg2_conv2d: det_sum"); return (int)e; }
+            }
             const int g = (int)std::min<int64_t>(cdiv(total_out, 256), 4096);
-            conv_finalize_kernel<T><<<g, 256, 0, s>>>((T*)y, workspace, base.e, total_out, Cout, (int64_t)OH * OW,
-                                                      (int)clean);
+            conv_finalize_kernel<T><<<g, 256, 0, s>>>((T*)y, acc_src, base.e, total_out, Cout, (int64_t)OH * OW,
+                                                      (int)(clean && !det_acc));
             rc = launch_status("sg2_conv2d finalize");
+        }
+        if (rc == 0 && base.e.det_dot) {
+            hipError_t e = det_sum(base.e.dot_out, Cout, base.e.det_dot, (int64_t)OH * OW * Cout, Cout, N,
+                                   (int64_t)OH * OW, Cout, arena, s);
+            if (e) { set_error("sg2_conv2d: det_sum"); return (int)e; }
         }
     });
     return rc;
@@ -1424,14 +1502,28 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W && B <= 4 &&
         A % 8 == 0 && 256 % (A / 8) == 0 && A * B <= 2048 && (uintptr_t)g % 16 == 0) {
         const int g_ = (int)std::min<int64_t>(cdiv((int64_t)a.M * (A / 8), 256), 1024);
+        DetArena arena;
+        const int64_t rows = (int64_t)g_ * 256 / (A / 8);
+        if (det_on()) SG2_DET_GET(a.det, arena, rows * A * B, "sg2_conv2d_wgrad (1x1, small B)");
         SG2_DISPATCH(dtype, T, { wgrad1x1_smallb_kernel<T><<<g_, 256, 0, s>>>(a); });
-        return launch_status("sg2_conv2d_wgrad (1x1, small B)");
+        int rc1 = launch_status("sg2_conv2d_wgrad (1x1, small B)");
+        if (rc1 || !a.det) return rc1;
+        e = det_sum(dw, 0, a.det, 0, (int64_t)A * B, 1, rows, (int64_t)A * B, arena, s);
+        if (e) { set_error("sg2_conv2d_wgrad: det_sum"); return (int)e; }
+        return 0;
     }
     if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W && A <= 4 &&
         B % 8 == 0 && 256 % (B / 8) == 0 && A * B <= 2048 && (uintptr_t)x % 16 == 0) {
         const int g_ = (int)std::min<int64_t>(cdiv((int64_t)a.M * (B / 8), 256), 1024);
+        DetArena arena;
+        const int64_t rows = (int64_t)g_ * 256 / (B / 8);
+        if (det_on()) SG2_DET_GET(a.det, arena, rows * A * B, "sg2_conv2d_wgrad (1x1, small A)");
         SG2_DISPATCH(dtype, T, { wgrad1x1_smalla_kernel<T><<<g_, 256, 0, s>>>(a); });
-        return launch_status("sg2_conv2d_wgrad (1x1, small A)");
+        int rc1 = launch_status("sg2_conv2d_wgrad (1x1, small A)");
+        if (rc1 || !a.det) return rc1;
+        e = det_sum(dw, 0, a.det, 0, (int64_t)A * B, 1, rows, (int64_t)A * B, arena, s);
+        if (e) { set_error("sg2_conv2d_wgrad: det_sum"); return (int)e; }
+        return 0;
     }
     const bool halo = wgrad_halo_ok(dtype, KH, KW, stride, pad_y, pad_x, OW, A, B) && (uintptr_t)x % 16 == 0 &&
                       (uintptr_t)g % 16 == 0;

@@ -53,6 +53,7 @@ struct Conv3Args {
     const void* residual;   // optional [N,OH,OW,Cout] (dtype T): y = round(act(...)) + residual (the D resnet add)
     int raw_act;            // y_raw receives the activated value before the residual add (the activation
                             // gradient's input) instead of the raw conv output
+    float* det_dot;         // deterministic mode: [N, OH, OW, Cout] per-element dot products (det_sum adds them)
 };
 
 template <typename T>
@@ -295,8 +296,13 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
             if (want_dot) {
                 const vec8o sv = *(const vec8o*)(dsrc + dst);
                 const vec8o rv = *(const vec8o*)(rt + m * OS + c8);
+                if (a.det_dot) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) dacc[e] += (float)rv[e] * (float)sv[e];
+                    for (int e = 0; e < 8; ++e) a.det_dot[dst + e] = (float)rv[e] * (float)sv[e];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) dacc[e] += (float)rv[e] * (float)sv[e];
+                }
             }
         } else {
             for (int e = 0; e < 8 && o + e < a.Cout; ++e) {
@@ -304,11 +310,15 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
                 if (want_raw) yr[dst + e] = a.raw_act ? yo : rt[m * OS + c8 + e];
                 if (a.residual) yo = (T)((float)yo + (float)((const T*)a.residual)[dst + e]);
                 y[dst + e] = yo;
-                if (want_dot) dacc[e] += (float)rt[m * OS + c8 + e] * (float)dsrc[dst + e];
+                if (want_dot) {
+                    const float pr = (float)rt[m * OS + c8 + e] * (float)dsrc[dst + e];
+                    if (a.det_dot) a.det_dot[dst + e] = pr;
+                    else dacc[e] += pr;
+                }
             }
         }
     }
-    if (want_dot) {
+    if (want_dot && !a.det_dot) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) atomicAdd(&red[c8 + e], dacc[e]);
         __syncthreads();
@@ -776,7 +786,7 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     auto tile_of = [&](int t, int& n, int& ty, int& tx) {
         const int j = t - t_begin;
         const int v = j < 64 ? __builtin_amdgcn_readlane(tinfo0, j) : __builtin_amdgcn_readlane(tinfo1, j - 64);
-        n = v >> 20;
+        n = (int)((unsigned)v >> 20);      // unsigned: a sample index >= 2048 sets bit 31
         ty = ((v >> 10) & 1023) * R_TH;
         tx = (v & 1023) * R_TW;
     };
@@ -1188,7 +1198,7 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     }
     // (the persistent kernel's epilogue folds the gain into the demod / noise / bias terms and evaluates lrelu
     // as max(v, alpha v): it needs gain > 0 and 0 <= alpha <= 1, the StyleGAN2 settings)
-    if (persist && a.Cin == P_C && a.Cout == P_C && a.H % P_TH == 0 && a.W % P_TW == 0 &&
+    if (persist && !(a.dot_out && a.det_dot) && a.Cin == P_C && a.Cout == P_C && a.H % P_TH == 0 && a.W % P_TW == 0 &&
         (!epi || (a.gain > 0.f && (a.act == 0 || (a.alpha >= 0.f && a.alpha <= 1.f))))) {
         const int tiles = a.N * (a.H / P_TH) * (a.W / P_TW);
         if (tiles >= 2 * num_cus()) {
@@ -1437,8 +1447,16 @@ int conv3x3_entry(void* y, void* y_raw, const void* x, const void* w, int dtype,
     a.OH = stride == 1 ? H : (H - 3) / 2 + 1;
     a.OW = stride == 1 ? W : (W - 3) / 2 + 1;
     hipStream_t s = as_stream(stream);
-    if (dtype == SG2_F16) return dispatch<f16_t>(a, s, stride);
-    return dispatch<bf16_t>(a, s, stride);
+    // deterministic mode: the dot's per-element products by slot, summed per sample in a fixed order (the
+    // persistent C = 64 kernel's wave-level atomics are bypassed: the halo kernel takes the call)
+    DetArena arena;
+    if (dot_out && det_on()) SG2_DET_GET(a.det_dot, arena, (int64_t)N * a.OH * a.OW * Cout, "sg2_conv3x3");
+    int rc = dtype == SG2_F16 ? dispatch<f16_t>(a, s, stride) : dispatch<bf16_t>(a, s, stride);
+    if (rc || !a.det_dot) return rc;
+    hipError_t e = det_sum(dot_out, Cout, a.det_dot, (int64_t)a.OH * a.OW * Cout, Cout, N, (int64_t)a.OH * a.OW, Cout,
+                           arena, s);
+    if (e) { set_error("sg2_conv3x3: det_sum"); return (int)e; }
+    return 0;
 }
 }  // namespace
 }  // namespace sg2

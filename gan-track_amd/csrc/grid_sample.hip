@@ -107,6 +107,61 @@ __global__ __launch_bounds__(256) void grid_sample_bwd_kernel(GSParams p) {
     }
 }
 
+// Deterministic form of grid_sample_bwd_kernel for the affine grid (sg2_set_deterministic): one lane per INPUT
+// pixel gathers, in a fixed order, the output pixels whose bilinear footprint covers it.  The affine map
+// ix = a00 ox + a01 oy + c0, iy = a10 ox + a11 oy + c1 (input pixels per output pixel, from theta) is inverted
+// per sample; the output pixels with floor(ix) in {X - 1, X} and floor(iy) in {Y - 1, Y} lie in the preimage of
+// [X - 1, X + 1) x [Y - 1, Y + 1), whose bounding box (plus a 2-pixel margin for rounding) is scanned row by
+// row.  Each candidate's corners are recomputed with the forward's own float arithmetic (corners()), so the
+// contributions are exactly the scatter kernel's products, summed in scan order.
+template <typename T>
+__global__ __launch_bounds__(256) void grid_sample_bwd_gather_kernel(GSParams p) {
+    const int Hi = p.dyn_hw ? p.dyn_hw[0] : p.Hi, Wi = p.dyn_hw ? p.dyn_hw[1] : p.Wi;
+    const int hl = p.dyn_hw ? min(p.Hi, Hi + 96) : p.Hi, wl = p.dyn_hw ? min(p.Wi, Wi + 96) : p.Wi;
+    const int64_t total = (int64_t)p.N * hl * wl;
+    const T* gout = (const T*)p.in;
+    float* gin = (float*)p.out;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int X = (int)(idx % wl);
+        const int Y = (int)((idx / wl) % hl);
+        const int n = (int)(idx / ((int64_t)wl * hl));
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        if (X < Wi && Y < Hi) {
+            const float* t = p.theta + n * 6;
+            // d(ix)/d(ox) etc. and the offset, in double for the inversion only
+            const double a00 = (double)t[0] * Wi / p.Wo, a01 = (double)t[1] * Wi / p.Ho;
+            const double a10 = (double)t[3] * Hi / p.Wo, a11 = (double)t[4] * Hi / p.Ho;
+            // ix at (ox, oy) = ((t0 bx + t1 by + t2 + 1) Wi - 1) / 2 with bx = (2 ox + 1) / Wo - 1
+            const double c0 = (((double)t[0] * (1.0 / p.Wo - 1.0) + (double)t[1] * (1.0 / p.Ho - 1.0) + t[2] + 1.0) * Wi - 1.0) * 0.5;
+            const double c1 = (((double)t[3] * (1.0 / p.Wo - 1.0) + (double)t[4] * (1.0 / p.Ho - 1.0) + t[5] + 1.0) * Hi - 1.0) * 0.5;
+            const double det = a00 * a11 - a01 * a10;
+            double oxmin = 1e30, oxmax = -1e30, oymin = 1e30, oymax = -1e30;
+            if (fabs(det) > 1e-12) {
+                for (int cy = 0; cy < 2; ++cy)
+                    for (int cx = 0; cx < 2; ++cx) {
+                        const double u = (X - 1 + 2 * cx) - c0, v = (Y - 1 + 2 * cy) - c1;
+                        const double ox = (a11 * u - a01 * v) / det, oy = (-a10 * u + a00 * v) / det;
+                        oxmin = fmin(oxmin, ox); oxmax = fmax(oxmax, ox);
+                        oymin = fmin(oymin, oy); oymax = fmax(oymax, oy);
+                    }
+            }
+            const int ox0 = max(0, (int)floor(oxmin) - 2), ox1 = min(p.Wo - 1, (int)ceil(oxmax) + 2);
+            const int oy0 = max(0, (int)floor(oymin) - 2), oy1 = min(p.Ho - 1, (int)ceil(oymax) + 2);
+            for (int oy = oy0; oy <= oy1; ++oy)
+                for (int ox = ox0; ox <= ox1; ++ox) {
+                    const Corners k = corners(p, n, oy, ox, Hi, Wi);
+                    const int dx = X - k.x0, dy = Y - k.y0;           // 0 or 1 when (X, Y) is a corner
+                    if ((unsigned)dx > 1u || (unsigned)dy > 1u) continue;
+                    const float w = dy ? (dx ? k.w11 : k.w10) : (dx ? k.w01 : k.w00);
+                    for (int c = 0; c < p.C && c < 4; ++c)
+                        acc[c] += (float)gout[n * p.os_n + c * p.os_c + (int64_t)oy * p.os_h + (int64_t)ox * p.os_w] * w;
+                }
+        }
+        for (int c = 0; c < p.C && c < 4; ++c) gin[n * p.is_n + c * p.is_c + (int64_t)Y * p.is_h + (int64_t)X * p.is_w] = acc[c];
+    }
+}
+
 // Reflect padding with margins held in device memory (so the ADA pipe needs no host sync): the
 // padded image of logical size (H + my0 + my1) x (W + mx0 + mx1) is written at the origin of a static
 // [N, C, Hs, Ws] buffer, zeros elsewhere (exactly what upfirdn2d's implicit zero padding sees).
@@ -222,6 +277,13 @@ int gs_bwd(float* gin, const void* gout, const float* grid, const float* theta, 
     }
     const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
     if (total == 0 || p.C == 0) return 0;
+    if (det_on() && theta) {
+        SG2_CHECK(p.C <= 4, "sg2_affine_grid_sample_bwd: deterministic mode supports C <= 4");
+        const int64_t tot_in = (int64_t)p.N * p.Hi * p.Wi;
+        const int gi = (int)std::min<int64_t>(cdiv(tot_in, 256), 256 * 64);
+        SG2_DISPATCH(dtype, T, { grid_sample_bwd_gather_kernel<T><<<gi, 256, 0, s>>>(p); });
+        return launch_status("sg2_affine_grid_sample_bwd (deterministic gather)");
+    }
     const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 32);
     SG2_DISPATCH(dtype, T, { grid_sample_bwd_kernel<T><<<g, 256, 0, s>>>(p); });
     return launch_status("sg2_grid_sample_bwd");

@@ -29,6 +29,8 @@ struct LBArgs {
     int pix_per_block;
     float alpha, gain, clamp;
     int act;             // 0 linear, 1 lrelu
+    float* det_db;       // deterministic mode: [gridDim.y * gridDim.x][C] slot partials of db
+    float* det_dd;       // deterministic mode: [gridDim.x][N * C] slot partials of dd
 };
 
 template <typename T>
@@ -40,6 +42,8 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(LBArgs a) {
     float* s_db = sm;                             // [C]
     float* s_dd = sm + a.C;                       // [C]
     float* s_dn = sm + 2 * a.C;                   // [pix_per_block]
+    float* part = sm + 2 * a.C + a.pix_per_block; // deterministic mode: [PPP][C] per-thread partials
+    const bool det = a.det_db || a.det_dd;
     const int tid = threadIdx.x;
     const int n = blockIdx.y;
     const int p0 = blockIdx.x * a.pix_per_block;
@@ -118,18 +122,36 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(LBArgs a) {
             }
         }
     }
-    if (a.db || a.dd) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (!active) break;
-            if (a.db) atomicAdd(&s_db[c0 + j], adb[j]);
-            if (a.dd) atomicAdd(&s_dd[c0 + j], add[j]);
+    if (det) {
+        // fixed order: thread partials by row, rows in order, then one slot per workgroup (det_sum)
+        const int slot = blockIdx.y * gridDim.x + blockIdx.x;
+        if (a.db) {
+            if (active) det_rows_store(part, a.C, pl, c0, adb);
+            __syncthreads();
+            for (int i = tid; i < a.C; i += 256) a.det_db[(int64_t)slot * a.C + i] = det_rows_sum(part, a.C, PPP, i);
+            __syncthreads();
         }
-    }
-    __syncthreads();
-    for (int i = tid; i < a.C; i += 256) {
-        if (a.db) atomicAdd(&a.db[i], s_db[i]);
-        if (a.dd) atomicAdd(&a.dd[(int64_t)n * a.C + i], s_dd[i]);
+        if (a.dd) {
+            if (active) det_rows_store(part, a.C, pl, c0, add);
+            __syncthreads();
+            for (int i = tid; i < a.C; i += 256)
+                a.det_dd[((int64_t)blockIdx.x * a.N + n) * a.C + i] = det_rows_sum(part, a.C, PPP, i);
+        }
+        __syncthreads();
+    } else {
+        if (a.db || a.dd) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (!active) break;
+                if (a.db) atomicAdd(&s_db[c0 + j], adb[j]);
+                if (a.dd) atomicAdd(&s_dd[c0 + j], add[j]);
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < a.C; i += 256) {
+            if (a.db) atomicAdd(&a.db[i], s_db[i]);
+            if (a.dd) atomicAdd(&a.dd[(int64_t)n * a.C + i], s_dd[i]);
+        }
     }
     if (a.dnoise && !shfl)
         for (int p = p0 + tid; p < p1; p += 256) a.dnoise[(int64_t)n * a.HW + p] = s_dn[p - p0];
@@ -140,9 +162,9 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(LBArgs a) {
 // would run as a full-size multiply plus a reduction.  Same lane layout as layer_bwd_kernel.
 template <typename T>
 __global__ __launch_bounds__(256) void dot_hw_kernel(float* out, const T* a, const T* b, int HW, int C,
-                                                     int pix_per_block) {
+                                                     int pix_per_block, float* det_ws) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
-    extern __shared__ __attribute__((aligned(16))) float red[];   // [C]
+    extern __shared__ __attribute__((aligned(16))) float red[];   // [C] (deterministic mode: [PPP][C])
     const int LP = C / 8, PPP = 256 / LP;
     const int tid = threadIdx.x, n = blockIdx.y;
     const int p0 = blockIdx.x * pix_per_block, p1 = min(HW, p0 + pix_per_block);
@@ -159,10 +181,20 @@ __global__ __launch_bounds__(256) void dot_hw_kernel(float* out, const T* a, con
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[j] += (float)(T)((float)av[j] * (float)bv[j]);   // product rounded as torch's
         }
+        if (det_ws) {
+            det_rows_store(red, C, pl, cg * 8, acc);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) atomicAdd(&red[cg * 8 + j], acc[j]);
+            for (int j = 0; j < 8; ++j) atomicAdd(&red[cg * 8 + j], acc[j]);
+        }
     }
     __syncthreads();
+    if (det_ws) {
+        // slot per workgroup: [blockIdx.x][N][C]
+        for (int i = tid; i < C; i += 256)
+            det_ws[((int64_t)blockIdx.x * gridDim.y + n) * C + i] = det_rows_sum(red, C, PPP, i);
+        return;
+    }
     for (int i = tid; i < C; i += 256) atomicAdd(&out[(int64_t)n * C + i], red[i]);
 }
 
@@ -178,6 +210,7 @@ struct AxArgs {
     float* dot;
     int N, HW, C, pix_per_block, act;
     float alpha, gain, clamp;
+    float* det_dot;      // deterministic mode: [gridDim.x][N][C] slot partials of dot
 };
 
 template <typename T>
@@ -185,7 +218,7 @@ __global__ __launch_bounds__(256) void vjp_axpy_kernel(AxArgs a) {
     constexpr int V = 16 / sizeof(T) < 8 ? 16 / sizeof(T) : 8;   // elements per 16-byte load
     constexpr int NL = 8 / V;
     typedef T vecv __attribute__((ext_vector_type(V)));
-    extern __shared__ __attribute__((aligned(16))) float red[];   // [C] when dot
+    extern __shared__ __attribute__((aligned(16))) float red[];   // [C] when dot (deterministic mode: [PPP][C])
     const int LP = a.C / 8, PPP = 256 / LP;
     const int tid = threadIdx.x, n = blockIdx.y;
     const int p0 = blockIdx.x * a.pix_per_block, p1 = min(a.HW, p0 + a.pix_per_block);
@@ -250,12 +283,21 @@ __global__ __launch_bounds__(256) void vjp_axpy_kernel(AxArgs a) {
             }
         }
         if (he) {
+            if (a.det_dot) {
+                det_rows_store(red, a.C, pl, c0, acc);
+            } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) atomicAdd(&red[c0 + j], acc[j]);
+                for (int j = 0; j < 8; ++j) atomicAdd(&red[c0 + j], acc[j]);
+            }
         }
     }
     if (he) {
         __syncthreads();
+        if (a.det_dot) {
+            for (int i = tid; i < a.C; i += 256)
+                a.det_dot[((int64_t)blockIdx.x * a.N + n) * a.C + i] = det_rows_sum(red, a.C, PPP, i);
+            return;
+        }
         for (int i = tid; i < a.C; i += 256) atomicAdd(&a.dot[(int64_t)n * a.C + i], red[i]);
     }
 }
@@ -285,11 +327,17 @@ extern "C" int sg2_vjp_axpy(void* out, const void* a, const float* sa, const voi
     const int PPP = std::max(1, 256 / (C / 8));
     x.pix_per_block = std::min(HW, PPP * 16);
     dim3 grid((unsigned)cdiv(HW, x.pix_per_block), (unsigned)N);
-    const size_t lds = dot ? C * sizeof(float) : 0;
+    DetArena arena;
+    if (dot && det_on()) SG2_DET_GET(x.det_dot, arena, (int64_t)grid.x * N * C, "sg2_vjp_axpy");
+    const size_t lds = dot ? (x.det_dot ? (size_t)PPP * C : (size_t)C) * sizeof(float) : 0;
     if (dtype == SG2_F16) vjp_axpy_kernel<f16_t><<<grid, 256, lds, s>>>(x);
     else if (dtype == SG2_BF16) vjp_axpy_kernel<bf16_t><<<grid, 256, lds, s>>>(x);
     else vjp_axpy_kernel<float><<<grid, 256, lds, s>>>(x);
-    return launch_status("sg2_vjp_axpy");
+    int rc = launch_status("sg2_vjp_axpy");
+    if (rc || !x.det_dot) return rc;
+    hipError_t err = det_sum(dot, 0, x.det_dot, 0, (int64_t)N * C, 1, grid.x, (int64_t)N * C, arena, s);
+    if (err) { set_error("sg2_vjp_axpy: det_sum"); return err; }
+    return 0;
 }
 
 extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, const void* dy, const void* y,
@@ -318,11 +366,22 @@ extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, cons
     // ~16 passes per workgroup; enough workgroups to cover the chip
     a.pix_per_block = std::min(HW, PPP * 16);
     dim3 grid((unsigned)cdiv(HW, a.pix_per_block), (unsigned)N);
-    const size_t lds = (2 * C + a.pix_per_block) * sizeof(float);
+    DetArena arena;
+    const bool det = det_on() && (db || dd);
+    if (det_on() && dnoise) SG2_CHECK(LP <= 64, "sg2_layer_bwd: deterministic mode needs C <= 512 with dnoise");
+    if (det && db) SG2_DET_GET(a.det_db, arena, (int64_t)grid.x * N * C, "sg2_layer_bwd");
+    if (det && dd) SG2_DET_GET(a.det_dd, arena, (int64_t)grid.x * N * C, "sg2_layer_bwd");
+    const size_t lds = (2 * C + a.pix_per_block + (det ? PPP * C : 0)) * sizeof(float);
     if (dtype == SG2_F16) layer_bwd_kernel<f16_t><<<grid, 256, lds, s>>>(a);
     else if (dtype == SG2_BF16) layer_bwd_kernel<bf16_t><<<grid, 256, lds, s>>>(a);
     else layer_bwd_kernel<float><<<grid, 256, lds, s>>>(a);
-    return launch_status("sg2_layer_bwd");
+    int rc = launch_status("sg2_layer_bwd");
+    if (rc || !det) return rc;
+    hipError_t err = hipSuccess;
+    if (db) err = det_sum(db, 0, a.det_db, 0, C, 1, (int64_t)grid.x * N, C, arena, s);
+    if (!err && dd) err = det_sum(dd, 0, a.det_dd, 0, (int64_t)N * C, 1, grid.x, (int64_t)N * C, arena, s);
+    if (err) { set_error("sg2_layer_bwd: det_sum"); return err; }
+    return 0;
 }
 
 extern "C" int sg2_dot_hw(float* out, const void* a, const void* b, int dtype, int N, int HW, int C, void* stream) {
@@ -338,8 +397,16 @@ extern "C" int sg2_dot_hw(float* out, const void* a, const void* b, int dtype, i
     const int PPP = std::max(1, 256 / (C / 8));
     const int ppb = std::min(HW, PPP * 32);
     dim3 grid((unsigned)cdiv(HW, ppb), (unsigned)N);
-    const size_t lds = C * sizeof(float);
-    if (dtype == SG2_F16) dot_hw_kernel<f16_t><<<grid, 256, lds, s>>>(out, (const f16_t*)a, (const f16_t*)b, HW, C, ppb);
-    else dot_hw_kernel<bf16_t><<<grid, 256, lds, s>>>(out, (const bf16_t*)a, (const bf16_t*)b, HW, C, ppb);
-    return launch_status("sg2_dot_hw");
+    DetArena arena;
+    float* det_ws = nullptr;
+    if (det_on()) SG2_DET_GET(det_ws, arena, (int64_t)grid.x * N * C, "sg2_dot_hw");
+    const size_t lds = (det_ws ? (size_t)PPP * C : (size_t)C) * sizeof(float);
+    if (dtype == SG2_F16)
+        dot_hw_kernel<f16_t><<<grid, 256, lds, s>>>(out, (const f16_t*)a, (const f16_t*)b, HW, C, ppb, det_ws);
+    else dot_hw_kernel<bf16_t><<<grid, 256, lds, s>>>(out, (const bf16_t*)a, (const bf16_t*)b, HW, C, ppb, det_ws);
+    int rc = launch_status("sg2_dot_hw");
+    if (rc || !det_ws) return rc;
+    e = det_sum(out, 0, det_ws, 0, (int64_t)N * C, 1, grid.x, (int64_t)N * C, arena, s);
+    if (e) { set_error("sg2_dot_hw: det_sum"); return e; }
+    return 0;
 }

@@ -44,6 +44,48 @@ inline hipError_t zero_acc(void* p, size_t bytes, hipStream_t s) {
     return accumulators_prezeroed() ? hipSuccess : zero_fill(p, bytes, s);
 }
 
+// Deterministic mode (sg2_set_deterministic, process-wide).  Every float accumulation that the fast path
+// makes with atomics (split-K partial sums, weight-gradient pixel splits, per-channel dot / bias / demod
+// reductions, the grid-sample scatter) is made instead by writing each contribution to a slot of the registered
+// scratch and summing the slots in a fixed order (det_sum): results are bitwise reproducible run to run.
+// Within a workgroup, LDS float atomics are replaced by per-thread partials summed in thread order.
+bool det_on();
+// A per-call bump allocator over the registered scratch (floats).  get() returns nullptr (and sets the error)
+// when the scratch is exhausted; entry points then return -1.
+class DetArena {
+ public:
+    DetArena();
+    float* get(int64_t n_floats);
+ private:
+    float* base_;
+    int64_t cap_, off_;
+};
+// out[g * go + i] += sum_{s < S} ws[g * gw + s * ss + i] for g < G, i < n: a fixed-order sum (runs of 64
+// consecutive s first, then runs of those, ...), temporaries from `arena`.
+hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t ss, int G, int64_t S, int64_t n,
+                   DetArena& arena, hipStream_t st);
+#define SG2_DET_GET(ptr, arena, n, what)                                                        \
+    do {                                                                                       \
+        (ptr) = (arena).get(n);                                                                \
+        if (!(ptr)) {                                                                          \
+            ::sg2::set_error(std::string(what) + ": deterministic scratch too small");        \
+            return -1;                                                                         \
+        }                                                                                      \
+    } while (0)
+
+// Deterministic replacement of a workgroup's LDS float atomics `red[c0 + j] += v[j]` by threads laid out as
+// (row, c0): each thread stores its 8 partials in its row of part[rows][C]; after a barrier, det_rows_sum(i)
+// adds channel i over the rows in row order.
+__device__ __forceinline__ void det_rows_store(float* part, int C, int row, int c0, const float* v) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[row * C + c0 + j] = v[j];
+}
+__device__ __forceinline__ float det_rows_sum(const float* part, int C, int rows, int i) {
+    float s = 0.f;
+    for (int r = 0; r < rows; ++r) s += part[r * C + i];
+    return s;
+}
+
 inline int launch_status(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -57,7 +57,15 @@ struct W3Args {
     int tiles_per_block;
     float alpha;          // dw += alpha * partial sums (a layer's weight gain)
     PTap taps[9];
+    float* det;           // deterministic mode: [gridDim.z][A][KK][B] workgroup partials (det_sum adds them)
+    int det_slots;
 };
+
+// dw[i] += v, or (deterministic mode) the workgroup's slot of i
+__device__ __forceinline__ void w3_add(const W3Args& a, int64_t i, float v) {
+    if (a.det) a.det[(int64_t)blockIdx.z * a.A * a.KK * a.B + i] = v;
+    else atomicAdd(a.dw + i, v);
+}
 
 template <typename T>
 using v8w = typename std::conditional<std::is_same<T, bf16_t>::value, bf16x8, f16x8>::type;
@@ -209,7 +217,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(W3Args a) {
             if (ar >= a.A) continue;
 #pragma unroll
             for (int t = 0; t < NT; ++t)
-                atomicAdd(a.dw + ((int64_t)ar * a.KK + a.taps[t].out) * a.B + b, acc[t][j] * a.alpha);
+                w3_add(a, ((int64_t)ar * a.KK + a.taps[t].out) * a.B + b, acc[t][j] * a.alpha);
         }
     }
 }
@@ -376,7 +384,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_dma_kernel(W3Args a) {
             const float f = a.alpha * sx * ((SC && a.gscale) ? a.gscale[n0 * A + ar] : 1.f);
 #pragma unroll
             for (int t = 0; t < NT; ++t)
-                atomicAdd(a.dw + ((int64_t)ar * a.KK + (NT == 9 ? t : 0)) * B + b, acc[t][j] * f);
+                w3_add(a, ((int64_t)ar * a.KK + (NT == 9 ? t : 0)) * B + b, acc[t][j] * f);
         }
     }
 }
@@ -507,7 +515,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_s2_kernel(W3Args a) {
             const int ar = a0 + wa * 32 + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
             if (ar >= a.A) continue;
 #pragma unroll
-            for (int t = 0; t < 9; ++t) atomicAdd(a.dw + ((int64_t)ar * 9 + t) * a.B + b, acc[t][j] * a.alpha);
+            for (int t = 0; t < 9; ++t) w3_add(a, ((int64_t)ar * 9 + t) * a.B + b, acc[t][j] * a.alpha);
         }
     }
 }
@@ -566,11 +574,44 @@ bool wgrad_halo_ok(int dtype, int KH, int KW, int stride, int pad_y, int pad_x, 
     return true;
 }
 
-// dw already zeroed.  One launch per output phase that has taps.
+namespace {
+int wgrad3x3_run(W3Args& a, DetArena& arena, float* dw, const void* g, const void* x, const float* gscale,
+                 const float* xscale, int dtype, int N, int A, int OH, int OW, int B, int H, int W, int KH, int KW,
+                 int stride, int pad_y, int pad_x, float alpha, hipStream_t s);
+}
+
+// dw already zeroed.  One launch per output phase that has taps.  Deterministic mode: every launch writes its
+// workgroups' partial sums to slots (blockIdx.z) of one zeroed [splits][A][KK][B] array, added in slot order
+// into dw at the end.
 int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale, const float* xscale, int dtype,
                     int N, int A, int OH, int OW, int B, int H, int W, int KH, int KW, int stride, int pad_y,
                     int pad_x, float alpha, hipStream_t s) {
     W3Args a{};
+    DetArena arena;
+    int rc = wgrad3x3_run(a, arena, dw, g, x, gscale, xscale, dtype, N, A, OH, OW, B, H, W, KH, KW, stride, pad_y,
+                          pad_x, alpha, s);
+    if (rc || !a.det) return rc;
+    const int64_t nel = (int64_t)A * KH * KW * B;
+    hipError_t e = det_sum(dw, 0, a.det, 0, nel, 1, a.det_slots, nel, arena, s);
+    if (e) { set_error("sg2_conv2d_wgrad: det_sum"); return (int)e; }
+    return 0;
+}
+
+namespace {
+// det mode: allocate and zero the slot array for `slots` workgroup splits
+int w3_det_slots(W3Args& a, DetArena& arena, int slots, hipStream_t s) {
+    if (!det_on()) return 0;
+    const int64_t n = (int64_t)slots * a.A * a.KK * a.B;
+    SG2_DET_GET(a.det, arena, n, "sg2_conv2d_wgrad (halo)");
+    a.det_slots = slots;
+    hipError_t e = zero_fill(a.det, n * sizeof(float), s);
+    if (e) { set_error("sg2_conv2d_wgrad: zero"); return (int)e; }
+    return 0;
+}
+
+int wgrad3x3_run(W3Args& a, DetArena& arena, float* dw, const void* g, const void* x, const float* gscale,
+                 const float* xscale, int dtype, int N, int A, int OH, int OW, int B, int H, int W, int KH, int KW,
+                 int stride, int pad_y, int pad_x, float alpha, hipStream_t s) {
     a.g = g; a.x = x; a.gscale = gscale; a.xscale = xscale; a.dw = dw; a.alpha = alpha;
     a.N = N; a.GH = OH; a.GW = OW; a.XH = H; a.XW = W; a.A = A; a.B = B; a.KK = KH * KW; a.S = stride;
     static const bool s2_on = [] { const char* e = getenv("SG2_WGRAD_S2"); return !e || atoi(e) != 0; }();
@@ -584,6 +625,7 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
         a.tiles_per_block = (int)cdiv(a.tiles, splits);
         splits = (int)cdiv(a.tiles, a.tiles_per_block);
         dim3 grid((unsigned)cdiv(A, BC), (unsigned)cdiv(B, BC), (unsigned)splits);
+        if (int rc = w3_det_slots(a, arena, (int)grid.z, s)) return rc;
         static const bool swz = [] { const char* e = getenv("SG2_WGRAD_SWZ"); return e != nullptr && e[0] == '1'; }();
         if (dtype == SG2_F16) {
             if (swz) wgrad3x3_s2_kernel<f16_t, true><<<grid, 256, 0, s>>>(a);
@@ -625,6 +667,7 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
             for (int kx = 0; kx < KW; ++kx)
                 a.taps[ky * KW + kx] = PTap{(int8_t)(ky - pad_y), (int8_t)(kx - pad_x), (int8_t)(ky * KW + kx), 0};
         a.PY = 0; a.PX = 0;
+        if (int rc = w3_det_slots(a, arena, (int)grid.z, s)) return rc;
         const int sel = ((gscale || xscale) ? 1 : 0) | (KH == 3 ? 2 : 0) | (TW == 32 ? 4 : 0) | (dtype == SG2_F16 ? 8 : 0);
         switch (sel) {
 #define SG2_WDMA_2(B_, T_, TW_, NT_)                                   \
@@ -642,6 +685,7 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
         }
         return launch_status("sg2_conv2d_wgrad (halo, LDS-DMA)");
     }
+    if (int rc = w3_det_slots(a, arena, (int)grid.z, s)) return rc;
     for (int py = 0; py < stride; ++py)
         for (int px = 0; px < stride; ++px) {
             int nt = 0;
@@ -666,5 +710,6 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
         }
     return 0;
 }
+}  // namespace
 
 }  // namespace sg2

@@ -45,6 +45,7 @@ SIGNATURES = {
                     _vp],
     'sg2_set_zeroed_accumulators': [_i],
     'sg2_set_clean_workspace': [_i],
+    'sg2_set_deterministic': [_vp, _i64],
     'sg2_conv3x3_s2': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _f, _f, _f, _vp, _i,
                        _vp, _vp, _vp],
     'sg2_conv3x3_up2': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp],
@@ -69,7 +70,7 @@ SIGNATURES = {
     'sg2_infnorm_bwd': [_vp, _vp, _vp, _vp, _i, _i, _f, _i, _vp],
     'sg2_pack_weight': [_vp, _i, _vp, _i, _i, _i, _i, _i64, _i64, _i64, _i, _f, _vp],
 }
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib = None
 
@@ -90,6 +91,7 @@ def lib():
         L.sg2_last_error.restype = ctypes.c_char_p
         L.sg2_set_zeroed_accumulators.restype = None
         L.sg2_set_clean_workspace.restype = None
+        L.sg2_set_deterministic.restype = None
         if L.sg2_abi_version() != ABI_VERSION:
             raise RuntimeError(f'sg2hip: ABI version mismatch ({L.sg2_abi_version()} != {ABI_VERSION})')
         _lib = L
@@ -108,6 +110,30 @@ def clean_workspace(on=True):
         yield
     finally:
         L.sg2_set_clean_workspace(0)
+
+
+_det_scratch = {}
+
+
+@contextlib.contextmanager
+def deterministic(on=True, scratch_mb=2048, device=None):
+    """Bitwise-reproducible mode (sg2_set_deterministic): inside, every float accumulation the kernels would make
+    with atomics is made through slots of a device scratch buffer summed in a fixed order.  The scratch
+    (`scratch_mb` MiB, allocated once per device and kept) must not be used by two streams at once: run the calls
+    inside on one stream."""
+    if not on:
+        yield
+        return
+    L = lib()
+    dev = torch.device('cuda', torch.cuda.current_device()) if device is None else torch.device(device)
+    buf = _det_scratch.get(dev)
+    if buf is None or buf.numel() * 4 < scratch_mb << 20:
+        buf = _det_scratch[dev] = torch.empty([scratch_mb << 18], dtype=torch.float32, device=dev)
+    L.sg2_set_deterministic(ctypes.c_void_p(buf.data_ptr()), ctypes.c_int64(buf.numel() * 4))
+    try:
+        yield
+    finally:
+        L.sg2_set_deterministic(ctypes.c_void_p(0), ctypes.c_int64(0))
 
 
 @contextlib.contextmanager

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define SG2_ABI_VERSION 3
+#define SG2_ABI_VERSION 4
 
 enum sg2_dtype { SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2 };
 
@@ -155,6 +155,17 @@ void sg2_set_zeroed_accumulators(int on);
  * entry and is left zero on return (the finalize pass clears what it read), so a split-K call issues no
  * memset.  The caller keeps one persistent zeroed workspace per stream.  Default off. */
 void sg2_set_clean_workspace(int on);
+
+/* Deterministic mode (process-wide, so that autograd's backward threads see it; scratch NULL = off, the
+ * default).  While a device scratch buffer is
+ * registered, every float accumulation the entry points otherwise make with atomics -- split-K partial sums,
+ * weight-gradient pixel splits, dot_out / db / dd reductions, the grid-sample input-gradient scatter -- is made
+ * by writing each contribution to a slot of the scratch and summing the slots in a fixed order, so results
+ * are bitwise reproducible.  Calls made while it is on must be stream-ordered (they share the scratch); a call
+ * whose partial sums do not fit returns -1 ("deterministic scratch too small").  The explicit-grid
+ * sg2_grid_sample_bwd keeps its atomics (only the affine form has the gather used here).  Test / audit mode:
+ * slower (extra passes over the partial sums). */
+void sg2_set_deterministic(void* scratch, int64_t bytes);
 
 /* Stride-2 / pad-0 form of sg2_conv3x3 (conv2d_resample.py:139-142 with down = 2: the discriminator's
  * down-2 3x3 layers after their FIR pre-filter, and the input gradient of the up-2 synthesis layers):

@@ -1017,11 +1017,27 @@ def make_phases(G, D, G_reg_interval=4, D_reg_interval=16, glr=0.0025, dlr=0.002
     return phases
 
 
+def D_of(phases):
+    return next(ph['module'] for ph in phases if ph['name'].startswith('D'))
+
+
 def train_iteration(loss, phases, G, G_ema, real_img, real_c, all_gen_z, all_gen_c, batch_idx, cur_nimg,
-                    batch_size, ema_kimg=10, ema_rampup=0.05, on_grads=None):
+                    batch_size, ema_kimg=10, ema_rampup=0.05, on_grads=None, isolated=False):
+    """isolated: every phase starts from the state the iteration started from (parameters and buffers restored,
+    no optimiser step, no EMA) -- the phase-isolated form of the parity fixtures (tests/golden/make_golden.py
+    gen_config_isolated): each phase's gradients are then a function of one fixed state, not of the earlier
+    phases' Adam steps (whose first step, beta1 = 0, is ~lr * sign(g) for every gradient entry)."""
+    start = None
+    if isolated:
+        start = [{k: v.detach().clone() for k, v in m.state_dict().items()} for m in (G, D_of(phases))]
     for pi, ph in enumerate(phases):
         if batch_idx % ph['interval'] != 0:
             continue
+        if isolated:
+            with torch.no_grad():
+                for m, sd in zip((G, D_of(phases)), start):
+                    for k, v in m.state_dict().items():
+                        v.copy_(sd[k])
         ph['opt'].zero_grad(set_to_none=True)
         ph['module'].requires_grad_(True)
         loss.accumulate_gradients(ph['name'], real_img, real_c, all_gen_z[pi], all_gen_c[pi], ph['interval'], cur_nimg)
@@ -1034,7 +1050,10 @@ def train_iteration(loss, phases, G, G_ema, real_img, real_c, all_gen_z, all_gen
                 p.grad = g.reshape(p.shape)
             if on_grads is not None:
                 on_grads(ph['name'], ph['module'])
-        ph['opt'].step()
+        if not isolated:
+            ph['opt'].step()
+    if isolated:
+        return None
     ema_nimg = ema_kimg * 1000
     if ema_rampup is not None:
         ema_nimg = min(ema_nimg, cur_nimg * ema_rampup)

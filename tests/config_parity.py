@@ -65,11 +65,11 @@ def _perturb(t, rel, gen):
     return t * (1 + rel * u)
 
 
-def run_oracle(cfg, inp, tape, aug_p=0.3, perturb=0.0):
+def run_oracle(cfg, inp, tape, aug_p=0.3, perturb=0.0, isolated=False):
     """The CPU oracle's iteration; `tape` records (mode 'record') or replays its draws.  perturb > 0: every
     parameter, real image and latent is multiplied by (1 +- perturb) first (a fixed random sign per entry) --
     evaluated in float64 with perturb = 2^-24 this measures how far an f32-sized change of the state moves
-    each result, i.e. the conditioning every f32 implementation inherits (config_parity.judge_cond)."""
+    each result, i.e. the conditioning every f32 implementation inherits."""
     from oracle import sg2_oracle as O
     torch.manual_seed(0)
     G, D = _nets(O, cfg, 4)
@@ -97,15 +97,18 @@ def run_oracle(cfg, inp, tape, aug_p=0.3, perturb=0.0):
     ctx = tape.record() if not tape.entries else tape.replay()
     with ctx:
         O.train_iteration(loss, O.make_phases(G, D), G, G_ema, T(inp['real']), T(inp['c']), T(inp['gen_z']),
-                          T(inp['gen_c']), batch_idx=0, cur_nimg=1000, batch_size=cfg['batch'], on_grads=on_grads)
+                          T(inp['gen_c']), batch_idx=0, cur_nimg=1000, batch_size=cfg['batch'], on_grads=on_grads,
+                          isolated=isolated)
     out['pl_mean'] = loss.pl_mean.detach().numpy()
+    if isolated:
+        return out, [(n, v.numpy()) for n, v in stats]
     out.update(summarize(dict(G.named_parameters()), 'G1'))
     out.update(summarize(dict(D.named_parameters()), 'D1'))
     out.update(summarize(dict(G_ema.named_parameters()), 'Gema1'))
     return out, [(n, v.numpy()) for n, v in stats]
 
 
-def run_oracle_f64(cfg, inp, tape, aug_p=0.3, perturb=0.0):
+def run_oracle_f64(cfg, inp, tape, aug_p=0.3, perturb=0.0, isolated=False):
     """The oracle evaluated in float64 on the same draws: the rounding-free answer that f32 results (the
     reference's and the product's alike) are judged against."""
     from oracle import sg2_oracle as O
@@ -113,15 +116,45 @@ def run_oracle_f64(cfg, inp, tape, aug_p=0.3, perturb=0.0):
     O.REAL = torch.float64
     torch.set_default_dtype(torch.float64)
     try:
-        return run_oracle(cfg, inp, tape, aug_p, perturb)
+        return run_oracle(cfg, inp, tape, aug_p, perturb, isolated)
     finally:
         O.REAL = prev[0]
         torch.set_default_dtype(prev[1])
 
 
-def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False):
+def _isolated_phases(tr, G, D, real, c, gz, gc):
+    """Each of the trainer's phases from the starting state (the phase-isolated fixtures): parameters and buffers
+    restored before every phase, the phase's forward / backward and gradient exchange as Trainer.step runs them
+    (eager), then the exchange's /N and nan_to_num, and no optimiser step."""
+    from torch_utils import misc
+    start = [{k: v.detach().clone() for k, v in m.state_dict().items()} for m in (G, D)]
+    for pi, ph in enumerate(tr.phases):
+        with torch.no_grad():
+            for m, sd in zip((G, D), start):
+                for k, v in m.state_dict().items():
+                    v.copy_(sd[k])
+        ph.opt.zero_grad(set_to_none=True)
+        ph.module.requires_grad_(True)
+        tr._accumulate(ph, [real], [c], [gz[pi]], [gc[pi]])
+        ph.module.requires_grad_(False)
+        ph.exchange.finish(ph.name, None)
+        misc.nan_to_num(ph.exchange.flat, nan=0, posinf=1e5, neginf=-1e5, out=ph.exchange.flat)
+        tr.on_grads(ph.name, ph.module)
+        ph.exchange._reset()
+
+
+def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False, isolated=False, deterministic=True):
     """The product's iteration on `dev`.  fp16_dtype None: all-f32 (num_fp16_res=0, the reference's CPU
-    arithmetic); else the reference's GPU default num_fp16_res=4 in that 16-bit type."""
+    arithmetic); else the reference's GPU default num_fp16_res=4 in that 16-bit type.  isolated: every phase
+    from the starting state, no optimiser step (the *_iso fixtures); returns the gradients, pl_mean and stats.
+    deterministic: the library's fixed-order reductions (sg2hip.deterministic) -- the result is a function of
+    the inputs, so a bound is met or missed by the code, not by a run's atomic order."""
+    import sg2hip
+    with sg2hip.deterministic(deterministic, device=dev):
+        return _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated)
+
+
+def _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated):
     from training import networks_stylegan2 as net, augment_mi, loss as loss_mod, trainer as trainer_mod
     torch.manual_seed(0)
     G, D = _nets(net, cfg, 0 if fp16_dtype is None else 4, fp16_dtype)
@@ -148,12 +181,17 @@ def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False):
     try:
         with tape.replay():
             gz, gc = T(inp['gen_z']), T(inp['gen_c'])
-            tr.step([T(inp['real'])], [T(inp['c'])], [[gz[i]] for i in range(4)], [[gc[i]] for i in range(4)])
+            if isolated:
+                _isolated_phases(tr, G, D, T(inp['real']), T(inp['c']), gz, gc)
+            else:
+                tr.step([T(inp['real'])], [T(inp['c'])], [[gz[i]] for i in range(4)], [[gc[i]] for i in range(4)])
         torch.cuda.synchronize(dev)
     finally:
         loss_mod.training_stats.report = orig
     assert tape.pos == len(tape.entries), 'product consumed a different number of random draws'
     out['pl_mean'] = loss.pl_mean.detach().cpu().numpy()
+    if isolated:
+        return out, stats
     out.update(summarize(dict(G.named_parameters()), 'G1'))
     out.update(summarize(dict(D.named_parameters()), 'D1'))
     out.update(summarize(dict(G_ema.named_parameters()), 'Gema1'))
@@ -248,67 +286,10 @@ def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
     return worst, sorted(ratios)
 
 
-def judge_cond(got, fix, floors=F32_FLOORS, factor=4.0, groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True,
-               rerun=None, max_out=0.02, hard=60.0):
-    """f32 results against the float64 answer, each tensor k held to its OWN conditioning (no phase-wide term):
-
-        err(got_k, f64) <= max(floor, factor * max(err(ref_k, f64), err(f64p_k, f64), err(got_k, rerun_k)))
-
-    f64p is the float64 evaluation with the state and inputs nudged by half an f32 ulp (make_golden.py
-    gen_conditioning): how far a rounding-sized change of the inputs moves tensor k, whatever evaluates it.
-    The reference's own f32 result is a second sample of that spread.  rerun: the product's second run of the
-    same iteration (or a list of them) -- its float-atomic reductions sum in a different order each run, a rounding-sized change
-    INSIDE the evaluation, which the downstream conditioning amplifies as it does the input nudge (the reference
-    run on a GPU has the same: cuDNN's weight gradients accumulate with atomics too).  Returns ({group: (worst
-    norm err, worst sample err, worst bound, worst ratio to the bound, its tensor)}, [(ratio, tensor, bound n,
-    bound s)]) and raises after computing everything when `check` and more than `max_out` of the tensors are out
-    of bounds or any tensor is beyond `hard` x its bound.
-    Why a share and not every tensor: the errors are heavy-tailed, and a few tensors are unstable in a way none of
-    the three spreads sees.  Measured at C4 / p = 0 (profiles/r03_c4p0_spread.txt): the product's f32 forward is
-    not bitwise reproducible (split-K float atomics, ~3e-7 relative at the first synthesis layer), and the
-    minibatch-std layer's sqrt(var + 1e-8) over a group of two turns that into a bimodal Dmain b4.conv.bias
-    gradient -- 0.15 off the float64 answer in 9 of 11 runs and 2e-4 in the other 2, in every process -- where
-    three runs in one process can all land in the same mode.  A broken kernel moves many tensors (and its
-    phase's flat vector, checked separately) or one tensor far beyond its bound; both still fail."""
-    truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
-    cond = {k[5:]: v for k, v in fix.items() if k.startswith('f64p/')}
-    assert cond, 'fixture has no f64p/ (conditioning) summaries'
-    kw, kg = _keys(truth, groups), _keys(got, groups)
-    _one_sided_zero(got, truth, kg, kw)
-    keys = sorted(set(kw) & set(kg))
-    worst, rows, fails = {}, [], []
-    for k in keys:
-        gn, gs = _tensor_errs(got, truth, k)
-        rn, rs_ = _tensor_errs(fix, truth, k)
-        cn, cs = _tensor_errs(cond, truth, k) if k + '/norm' in cond else (0.0, 0.0)
-        for rr in (rerun if isinstance(rerun, (list, tuple)) else [rerun] if rerun is not None else []):
-            pn, ps = _tensor_errs(rr, got, k)
-            cn, cs = max(cn, pn), max(cs, ps)
-        floor = floors['grad' if k.startswith('grad/') else 'param']
-        bn, bs = max(floor[0], factor * max(rn, cn)), max(floor[1], factor * max(rs_, cs))
-        ratio = max(gn / bn, gs / bs)
-        g = _group(k)
-        w = worst.get(g, (0.0, 0.0, 0.0, 0.0, ''))
-        worst[g] = (max(w[0], gn), max(w[1], gs), max(w[2], bn), max(w[3], ratio), k if ratio > w[3] else w[4])
-        rows.append((ratio, k, bn, bs))
-        if gn > bn:
-            fails.append(f'{k}: norm err vs f64 {gn:.3g} > bound {bn:.3g} (reference f32 {rn:.3g}, conditioning / '
-                         f'rerun {cn:.3g})')
-        if gs > bs:
-            fails.append(f'{k}: sampled-entry err vs f64 {gs:.3g} > bound {bs:.3g} (reference {rs_:.3g}, conditioning {cs:.3g})')
-    if check:
-        n_out = sum(1 for r in rows if r[0] > 1.0)
-        assert n_out <= max_out * len(rows), f'{n_out} of {len(rows)} tensors out of bounds; first: {fails[0]}'
-        far = [r for r in rows if r[0] > hard]
-        assert not far, f'{far[0][1]}: {far[0][0]:.3g} x its bound'
-    return worst, sorted(rows, reverse=True)
-
-
-def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/',), check=True, rerun=None):
+def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/',), check=True):
     """Direct product-vs-reference-f32 check on every tensor the reference's f32 result gets right (both its
     norm and its sampled entries within `well` of the float64 answer): the product must then agree with the
-    reference itself to `tol` (or 4x the product's own run-to-run difference on that tensor, when `rerun` is
-    given) on both measures.  Gradients only: a parameter after Adam's first step (beta1 = 0) moves each entry by
+    reference itself to `tol` on both measures.  Gradients only: a parameter after Adam's first step (beta1 = 0) moves each entry by
     about lr * sign(g), so an entry whose gradient is zero up to rounding lands 2 lr apart in two correct
     evaluations (measured: D1/b512.conv1.bias at C4 / p = 0); the parameters are held by the flat check.
     Returns (number of tensors checked, worst error, its key)."""
@@ -323,9 +304,7 @@ def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/',), check=T
         en, es = _tensor_errs(got, fix, k)
         if max(en, es) > worst:
             worst, wk = max(en, es), k
-        reruns = rerun if isinstance(rerun, (list, tuple)) else [rerun] if rerun is not None else []
-        t = max([tol] + [4.0 * max(_tensor_errs(rr, got, k)) for rr in reruns])
-        if en > t or es > t:
+        if en > tol or es > tol:
             fails.append(f'{k}: vs reference f32 norm {en:.3g} samples {es:.3g} > {tol}')
     if check:
         assert not fails, f'{len(fails)} of {n} well-conditioned tensors differ from the reference: {fails[0]}'
@@ -348,11 +327,9 @@ def judge_flat(got_flat, ref_flat, floor, factor=3.0):
 REG_STATS = ('Loss/pl_penalty', 'Loss/G/reg', 'Loss/r1_penalty', 'Loss/D/reg')
 
 
-def judge_stats_f32(got, fix, floor=1e-4, reg_floor=3e-3, factor=4.0, group_factor=3.0, check=True,
-                    rerun_stats=()):
+def judge_stats_f32(got, fix, floor=1e-4, reg_floor=3e-3, factor=4.0, group_factor=3.0, check=True):
     """Reported loss statistics against f64: each within max(floor, factor x the reference f32's error on it,
-    group_factor x the reference's worst statistic error, factor x the product's own run-to-run difference on it
-    when reruns are given) -- the same chance argument as judge_f32 / judge_cond."""
+    group_factor x the reference's worst statistic error) -- the same chance argument as judge_f32."""
     names, ref_vals = fixture_stats(fix)
     assert [n for n, _ in got] == names, 'reported statistics differ in name or order'
     rows = []
@@ -361,16 +338,15 @@ def judge_stats_f32(got, fix, floor=1e-4, reg_floor=3e-3, factor=4.0, group_fact
             continue
         t = np.asarray(fix[f'f64/stats/{j}'], np.float64)
         den = max(np.linalg.norm(t), 1e-30)
-        spread = max([0.0] + [float(np.linalg.norm(np.asarray(rs[j][1], np.float64) - np.asarray(v, np.float64)))
-                              / den for rs in rerun_stats])
         rows.append((n, np.linalg.norm(np.asarray(v, np.float64) - t) / den,
-                     np.linalg.norm(np.asarray(r, np.float64) - t) / den, spread))
-    gmax = max(er for _, _, er, _ in rows)
-    for n, e, er, sp in rows:
+                     np.linalg.norm(np.asarray(r, np.float64) - t) / den))
+    gmax = max(er for _, _, er in rows)
+    for n, e, er in rows:
         fl = reg_floor if n in REG_STATS else floor
-        assert not check or e <= max(fl, factor * er, group_factor * gmax, factor * sp), \
-            f'stat {n}: rel err vs f64 {e:.3g} (reference f32 {er:.3g}, worst reference stat {gmax:.3g}, rerun {sp:.3g})'
-    return max(e for _, e, _, _ in rows)
+        t = max(fl, factor * er, group_factor * gmax)
+        assert not check or e <= t, \
+            f'stat {n}: rel err vs f64 {e:.3g} > bound {t:.3g} (reference f32 {er:.3g}, worst reference stat {gmax:.3g})'
+    return max(e for _, e, _ in rows)
 
 
 def judge_pl_mean(got, fix, floor=3e-3, factor=4.0, check=True):

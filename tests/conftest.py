@@ -17,7 +17,19 @@ def pytest_configure(config):
     config.addinivalue_line('markers', 'slow: long-running')
 
 
+# Unit-level files first, whole-iteration files last: a failure under -x then stops the run after the kernel
+# tests have reported, not before them.
+_ORDER = ['test_capi', 'test_oracle_golden', 'test_loss_host', 'test_trainer_shell', 'test_dist_gloo', 'test_ops_gpu',
+          'test_deterministic_gpu', 'test_train_gpu', 'test_trainer_gpu', 'test_training_loop_gpu', 'test_config_gpu']
+
+
+def _rank(item):
+    mod = os.path.splitext(os.path.basename(str(item.fspath)))[0]
+    return _ORDER.index(mod) if mod in _ORDER else len(_ORDER)
+
+
 def pytest_collection_modifyitems(config, items):
+    items.sort(key=_rank)     # stable: the order inside a file is kept
     try:
         import torch
         has_gpu = torch.cuda.is_available()

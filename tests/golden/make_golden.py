@@ -389,7 +389,9 @@ CONFIGS = {
 }
 
 
-def gen_config_iteration(tag, cfg, input_seed=31, tape_seed=13, aug_p=0.3):
+def gen_config_iteration(tag, cfg, input_seed=31, tape_seed=13, aug_p=0.3, isolated=False):
+    """isolated: the phase-isolated fixture train_<tag>_iso.npz -- every phase from the initial state (parameters
+    and buffers restored, no optimiser step), see oracle.sg2_oracle.train_iteration."""
     import config_parity as cp
     d = {}
     torch.manual_seed(0)
@@ -433,8 +435,14 @@ def gen_config_iteration(tag, cfg, input_seed=31, tape_seed=13, aug_p=0.3):
     gen_z, gen_c = inp['gen_z'], inp['gen_c']
     cur_nimg = 1000
     tape = Tape(seed=tape_seed)
+    start = [{k: v.detach().clone() for k, v in m.state_dict().items()} for m in (G, D)]
     with tape.record():
         for pi, ph in enumerate(phases):
+            if isolated:
+                with torch.no_grad():
+                    for m, sd in zip((G, D), start):
+                        for k, v in m.state_dict().items():
+                            v.copy_(sd[k])
             ph['opt'].zero_grad(set_to_none=True)
             ph['module'].requires_grad_(True)
             n0 = len(stats)
@@ -447,31 +455,33 @@ def gen_config_iteration(tag, cfg, input_seed=31, tape_seed=13, aug_p=0.3):
             for (_, p), g in zip(named, flat.split([p.numel() for _, p in named])):
                 p.grad = g.reshape(p.shape)
             d.update(summarize({n_: p.grad for n_, p in named}, f'grad/{ph["name"]}'))
-            ph['opt'].step()
+            if not isolated:
+                ph['opt'].step()
             d[f'stats_names/{ph["name"]}'] = np.array([s_[0] for s_ in stats[n0:]])
             for j, s_ in enumerate(stats[n0:]):
                 d[f'stats/{ph["name"]}/{j}'] = s_[1]
             if ph['name'] == 'Greg':
                 d['pl_mean'] = npy(loss.pl_mean)
     loss_mod.training_stats.report = orig_report
-    ema_beta = 0.5 ** (B / max(min(10 * 1000, cur_nimg * 0.05), 1e-8))
-    with torch.no_grad():
-        for p_ema, p in zip(G_ema.parameters(), G.parameters()):
-            p_ema.copy_(p.lerp(p_ema, ema_beta))
-    d.update(summarize(dict(G.named_parameters()), 'G1'))
-    d.update(summarize(dict(D.named_parameters()), 'D1'))
-    d.update(summarize(dict(G_ema.named_parameters()), 'Gema1'))
+    if not isolated:
+        ema_beta = 0.5 ** (B / max(min(10 * 1000, cur_nimg * 0.05), 1e-8))
+        with torch.no_grad():
+            for p_ema, p in zip(G_ema.parameters(), G.parameters()):
+                p_ema.copy_(p.lerp(p_ema, ema_beta))
+        d.update(summarize(dict(G.named_parameters()), 'G1'))
+        d.update(summarize(dict(D.named_parameters()), 'D1'))
+        d.update(summarize(dict(G_ema.named_parameters()), 'Gema1'))
     d.update(tape.to_compact_npz_dict('tape'))
     # the float64 oracle on the same state, inputs and draws
     replay = Tape.from_npz(tape.to_compact_npz_dict('t'), 't')
-    f64, f64_stats = cp.run_oracle_f64(cfg, inp, replay, aug_p)
+    f64, f64_stats = cp.run_oracle_f64(cfg, inp, replay, aug_p, isolated=isolated)
     assert replay.pos == len(replay.entries)
     for k, v in f64.items():
         d[f'f64/{k}'] = v
     for j, (n_, v) in enumerate(f64_stats):
         d[f'f64/stats/{j}'] = np.asarray(v, np.float64)
-    d['cfg'] = np.array(repr(dict(cfg, aug_p=aug_p, init_seeds=(1, 2), input_seed=input_seed)))
-    np.savez_compressed(os.path.join(OUT, f'train_{tag}.npz'), **pack(d))
+    d['cfg'] = np.array(repr(dict(cfg, aug_p=aug_p, init_seeds=(1, 2), input_seed=input_seed, isolated=isolated)))
+    np.savez_compressed(os.path.join(OUT, f'train_{tag}{"_iso" if isolated else ""}.npz'), **pack(d))
     print(tag, 'written', flush=True)
 
 
@@ -517,6 +527,11 @@ if __name__ == '__main__':
         if tag in which:
             gen_config_iteration(tag, CONFIGS[base], aug_p=0.0)
     for w in which:
+        if w.startswith('iso:'):           # iso:<tag>[:<batch>]  phase-isolated fixture train_<tag>_iso.npz
+            parts = w.split(':')
+            base = parts[1][:-2] if parts[1].endswith('p0') else parts[1]
+            cfg_i = dict(CONFIGS[base], **({'batch': int(parts[2])} if len(parts) > 2 else {}))
+            gen_config_iteration(parts[1], cfg_i, aug_p=0.0 if parts[1].endswith('p0') else 0.3, isolated=True)
         if w.startswith('cond:'):          # cond:<tag>[:<cache dir>]
             parts = w.split(':')
             gen_conditioning(parts[1], parts[2] if len(parts) > 2 else None)

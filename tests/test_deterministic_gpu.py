@@ -1,0 +1,184 @@
+"""Deterministic mode (sg2hip.deterministic / sg2_set_deterministic): every kernel that reduces with float atomics
+on the fast path -- split-K partial sums, weight-gradient pixel splits, per-(n, c) dot / bias / demodulation
+reductions, the grid-sample input-gradient scatter -- is run twice in deterministic mode and must give bitwise
+equal results, and must agree with the fast (atomic) path to the rounding of a different summation order.
+Then one whole phase-isolated iteration at configuration width (C2) in f32 and fp16: every gradient summary and
+statistic bitwise equal between two runs."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import sg2hip
+from golden_util import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda', 0)
+CL = torch.channels_last
+
+
+def _nhwc(t, dtype):
+    return t.to(DEV).to(dtype).contiguous(memory_format=CL)
+
+
+def _check(fn, tol):
+    """fn() -> list of tensors.  Deterministic twice: bitwise equal; vs the atomic path: within tol."""
+    with sg2hip.deterministic():
+        a = [t.detach().clone() for t in fn()]
+        b = [t.detach().clone() for t in fn()]
+    ref = [t.detach().clone() for t in fn()]
+    torch.cuda.synchronize()
+    for i, (x, y, r) in enumerate(zip(a, b, ref)):
+        assert torch.equal(x, y), f'output {i}: deterministic runs differ (max {float((x.float() - y.float()).abs().max()):.3g})'
+        assert rel_err(x.float(), r.double().cpu()) < tol, f'output {i}: deterministic vs atomic path {rel_err(x.float(), r.double().cpu()):.3g}'
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('shape', [(2, 16, 24, 8), (3, 64, 7, 512), (4, 64, 64, 64)])
+def test_det_layer_bwd(dtype, shape):
+    from torch_utils.ops import conv2d_gradfix as cg
+    N, H, W, C = shape
+    g = torch.Generator().manual_seed(3)
+    y, c, dy = (_nhwc(torch.randn(N, C, H, W, generator=g) * 2, dtype) for _ in range(3))
+    d = (torch.rand(N, C, generator=g) + 0.5).to(DEV)
+    _check(lambda: cg.layer_bwd(dy, y, c, d, act=1, alpha=0.2, gain=1.5, clamp=2.5), 1e-5)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(2, 64, 20, 33, 96), (9, 64, 128, 256, 64), (2, 512, 16, 16, 512)])
+def test_det_conv3x3_dot_and_wgrad(dtype, shape):
+    """16-bit 3x3: the dot epilogue (generic halo kernel; the persistent C = 64 shape, whose wave atomics the
+    deterministic mode routes to the halo kernel) and the LDS-DMA weight gradient, plain and scaled."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    N, Cin, H, W, Cout = shape
+    g = torch.Generator().manual_seed(4)
+    x = _nhwc(torch.randn(N, Cin, H, W, generator=g), dtype)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / np.sqrt(Cin * 9)).to(DEV).to(dtype)
+    src = _nhwc(torch.randn(N, Cout, H, W, generator=g), dtype)
+    s = (torch.rand(N, Cout, generator=g) + 0.5).to(DEV)
+    gr = _nhwc(torch.randn(N, Cout, H, W, generator=g), dtype)
+    xs = (torch.rand(N, Cin, generator=g) + 0.5).to(DEV)
+
+    def fn():
+        y, raw, dot = cg.conv3x3_fused(x, cg._pack_conv(w), Cout, out_scale=s, dot_src=src)
+        return [y, dot, cg._wgrad_raw(gr, x, 3, 3, 1, (1, 1)), cg._wgrad_raw(gr, x, 3, 3, 1, (1, 1), x_scale=xs)]
+    _check(fn, 1e-5)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float16])
+@pytest.mark.parametrize('geom', [(3, 1, 1, False, 2, 512, 8, 8, 512), (3, 1, 1, False, 2, 512, 4, 4, 512),
+                                  (3, 2, 0, True, 2, 128, 9, 9, 64), (3, 2, 0, False, 3, 32, 12, 10, 48),
+                                  (1, 1, 0, True, 3, 128, 9, 7, 3)])
+def test_det_conv_fused_split_k_and_dot(dtype, geom):
+    """Implicit-GEMM conv: split-K (the f32 low-resolution 512-channel layers), strided / transposed phases,
+    the per-element dot epilogue, the 1x1 small-depth dot kernel; and the generic weight gradient (f32 split
+    form, pixel-split slots)."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    k, stride, pad, transpose, N, Cin, H, W, Cout = geom
+    g = torch.Generator().manual_seed(29)
+    x = _nhwc(torch.randn(N, Cin, H, W, generator=g), dtype)
+    if transpose:
+        w = (torch.randn(Cin, Cout, k, k, generator=g) / (Cin * k * k) ** 0.5).to(DEV).to(dtype)
+        oh, ow = (H - 1) * stride - 2 * pad + k, (W - 1) * stride - 2 * pad + k
+        wp = cg._pack_convT(w)
+    else:
+        w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).to(DEV).to(dtype)
+        oh, ow = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+        wp = cg._pack_conv(w)
+    s = (torch.rand(N, Cout, generator=g) + 0.5).to(DEV)
+    src = _nhwc(torch.randn(N, Cout, oh, ow, generator=g), dtype)
+    gr = _nhwc(torch.randn(N, Cout, oh, ow, generator=g), dtype)
+
+    def fn():
+        y, _, dot = cg.conv_fused(x, wp, Cout, oh, ow, k, k, stride, (pad, pad), transpose=transpose, out_scale=s,
+                                  dot_src=src)
+        out = [y, dot]
+        if not transpose:
+            out.append(cg._wgrad_raw(gr, x, k, k, stride, (pad, pad)))
+        return out
+    _check(fn, 1e-5)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('cin,cout', [(1, 64), (3, 16), (64, 1), (128, 3)])
+def test_det_wgrad_1x1_small_depth(dtype, cin, cout):
+    from torch_utils.ops import conv2d_gradfix as cg
+    g = torch.Generator().manual_seed(11)
+    n, h, w = 2, 33, 47
+    x = _nhwc(torch.randn(n, cin, h, w, generator=g), dtype)
+    gr = _nhwc(torch.randn(n, cout, h, w, generator=g), dtype)
+    gs, xs = (torch.rand(n, cout, generator=g) + 0.5).to(DEV), (torch.rand(n, cin, generator=g) + 0.5).to(DEV)
+    _check(lambda: [cg._wgrad_raw(gr, x, 1, 1, 1, (0, 0), x_scale=xs, g_scale=gs)], 1e-5)
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('case', ['s2', 's2_scaled', 'reg16_scaled'])
+def test_det_wgrad_halo_phases(dtype, case):
+    """Halo weight gradients: the stride-2 one-launch kernel, and the register-staged per-phase kernel (a scaled
+    16^2 layer whose workgroups span several samples): slots summed in order."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    g = torch.Generator().manual_seed(31)
+    if case.startswith('s2'):
+        N, Ci, Co = 3, 64, 72
+        x = _nhwc(torch.randn(N, Ci, 67, 65, generator=g), dtype)
+        gr = _nhwc(torch.randn(N, Co, 33, 32, generator=g), dtype)
+        xs = (torch.rand(N, Ci, generator=g) + 0.5).to(DEV) if case == 's2_scaled' else None
+        _check(lambda: [cg._wgrad_raw(gr, x, 3, 3, 2, (0, 0), x_scale=xs)], 1e-5)
+    else:
+        N, Ci, Co = 8, 128, 128
+        x = _nhwc(torch.randn(N, Ci, 16, 16, generator=g), dtype)
+        gr = _nhwc(torch.randn(N, Co, 16, 16, generator=g), dtype)
+        xs = (torch.rand(N, Ci, generator=g) + 0.5).to(DEV)
+        gs = (torch.rand(N, Co, generator=g) + 0.5).to(DEV)
+        _check(lambda: [cg._wgrad_raw(gr, x, 3, 3, 1, (1, 1), x_scale=xs, g_scale=gs)], 1e-5)
+
+
+def test_det_affine_grid_sample_bwd():
+    """The ADA warp's input gradient: a fixed-order gather per input pixel in deterministic mode vs the
+    atomic scatter, with a static buffer and a dynamic logical extent as the augment pipe uses it."""
+    from torch_utils.ops import grid_sample_gradfix as gs
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(3, 3, 140, 136, generator=g).to(DEV).requires_grad_(True)
+    theta = torch.tensor([[[1.05, 0.1, 0.03], [-0.08, 0.95, -0.02]], [[0.9, -0.2, 0.1], [0.15, 1.1, 0.05]],
+                          [[0.7, 0.0, -0.2], [0.0, 1.3, 0.1]]], device=DEV)
+    size = [3, 3, 150, 146]
+    dyn = torch.tensor([130, 128], dtype=torch.int32, device=DEV)
+    dy = torch.randn(size, generator=g).to(DEV)
+
+    def fn():
+        out = []
+        for d in (None, dyn):
+            y = gs.affine_grid_sample(x, theta, size, dyn_hw=d)
+            gx, = torch.autograd.grad(y, [x], dy)
+            out.append(gx)
+        return out
+    _check(fn, 1e-6)
+
+
+def test_det_dot_hw_and_vjp_axpy():
+    from torch_utils.ops import conv2d_gradfix as cg
+    g = torch.Generator().manual_seed(5)
+    a = _nhwc(torch.randn(3, 64, 37, 41, generator=g), torch.float16)
+    b = _nhwc(torch.randn(3, 64, 37, 41, generator=g), torch.float16)
+    _check(lambda: [cg.dot_hw(a, b)], 1e-5)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('dt', [None, 'fp16'])
+def test_det_isolated_iteration_c2(dt):
+    """A whole phase-isolated iteration at the C2 configuration's width (256^2, cbase 16384, batch 4), twice in
+    deterministic mode: every gradient summary (norm and sampled entries), pl_mean and every reported statistic
+    bitwise equal."""
+    import config_parity as cp
+    from golden_util import load
+    fdt = None if dt is None else torch.float16
+    runs = []
+    for _ in range(2):
+        cfg, inp, tape, fix = cp.load_fixture(load('train_c2_iso.npz'))
+        runs.append(cp.run_product(cfg, inp, tape, DEV, fp16_dtype=fdt, isolated=True, deterministic=True))
+    (g1, s1), (g2, s2) = runs
+    assert sorted(g1) == sorted(g2)
+    diff = [k for k in g1 if not np.array_equal(np.asarray(g1[k]), np.asarray(g2[k]))]
+    assert not diff, f'{len(diff)} summaries differ between deterministic runs, e.g. {diff[:3]}'
+    for (n1, v1), (n2, v2) in zip(s1, s2):
+        assert n1 == n2 and np.array_equal(v1, v2), n1

@@ -459,7 +459,7 @@ def test_fused_synthesis_layer_matches_composed(dtype):
 
 @pytest.mark.parametrize('dtype,res', [(torch.float16, 16), (torch.bfloat16, 16), (torch.float32, 16),
                                        (torch.float16, 4), (torch.float32, 8)])
-def test_fused_synthesis_layer_pl_pass(dtype, res):
+def test_fused_synthesis_layer_pl_pass(dtype, res, monkeypatch):
     """The path-length pass as loss.py runs it: the create_graph gradient w.r.t. ws under
     conv2d_gradfix.no_weight_gradients() (where the dgrad goes through _ScaledConvT, the demodulation scale
     on the operand staging), then the penalty's backward with weight gradients enabled (_ScaledConvT's
@@ -480,7 +480,8 @@ def test_fused_synthesis_layer_pl_pass(dtype, res):
     params = [layer.weight, layer.bias, layer.noise_strength, layer.affine.weight, layer.affine.bias]
     out = []
     for fused, vjp in [(True, True), (False, False), (True, False)]:
-        modconv.enabled, modconv.fused_vjp = fused, vjp
+        monkeypatch.setattr(modconv, 'enabled', fused)
+        monkeypatch.setattr(modconv, 'fused_vjp', vjp)
         x = x0.clone().requires_grad_(True)
         wv = w0.clone().requires_grad_(True)
         orig = torch.randn
@@ -493,7 +494,6 @@ def test_fused_synthesis_layer_pl_pass(dtype, res):
             g_w, = torch.autograd.grad((y.float() * pl).sum(), [wv], create_graph=True)
         g2 = torch.autograd.grad(g_w.square().sum(), params + [x, wv], allow_unused=True)
         out.append((g_w.float(), [g if g is None else g.float() for g in g2]))
-    modconv.enabled, modconv.fused_vjp = True, True
     tol = {torch.float16: 2e-2, torch.bfloat16: 5e-2, torch.float32: 1e-4}[dtype]
     # the fused VJP node (_LayerVJP) against the unfused layer, and against the fused layer's composed VJP
     for (gw1, g21), (gw2, g22) in [(out[0], out[1]), (out[0], out[2])]:
@@ -1379,7 +1379,7 @@ def test_vjp_axpy(dtype, C, form):
 @pytest.mark.parametrize('up,cin,cout,res,n', [(1, 512, 512, 64, 1), (2, 512, 512, 64, 1), (1, 128, 64, 32, 3),
                                                 (2, 64, 64, 64, 2), (1, 64, 64, 256, 2)])
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float16])
-def test_layer_vjp_matches_composed(up, cin, cout, res, n, dtype):
+def test_layer_vjp_matches_composed(up, cin, cout, res, n, dtype, monkeypatch):
     """The fused create_graph VJP nodes (modconv._LayerVJP, _UpLayerVJP) against the fused layer's composed VJP on
     the path-length pass (reference loss.py:85-100: the ws gradient under no_weight_gradients, then the penalty's
     backward with weight gradients on) at network widths: the f32 split-K shapes of the 64^2 / 512-channel
@@ -1400,7 +1400,7 @@ def test_layer_vjp_matches_composed(up, cin, cout, res, n, dtype):
     params = [layer.weight, layer.bias, layer.noise_strength, layer.affine.weight, layer.affine.bias]
     out = []
     for vjp in [True, False]:
-        modconv.fused_vjp = vjp
+        monkeypatch.setattr(modconv, 'fused_vjp', vjp)   # restored even if the pass raises
         x = x0.clone().requires_grad_(True)
         wv = w0.clone().requires_grad_(True)
         orig = torch.randn
@@ -1414,7 +1414,6 @@ def test_layer_vjp_matches_composed(up, cin, cout, res, n, dtype):
         loss = g_w.square().sum() + g_x.float().square().sum()
         g2 = torch.autograd.grad(loss, params + [x, wv], allow_unused=True)
         out.append([g_w.float(), g_x.float()] + [g if g is None else g.float() for g in g2])
-    modconv.fused_vjp = True
     tol = 1e-4 if dtype == torch.float32 else 2e-2
     names = ['g_w', 'g_x', 'weight', 'bias', 'noise_strength', 'affine.weight', 'affine.bias', 'x', 'wv']
     for name, a_, b_ in zip(names, *out):
