@@ -134,25 +134,41 @@ def test_det_wgrad_halo_phases(dtype, case):
 
 
 def test_det_affine_grid_sample_bwd():
-    """The ADA warp's input gradient: a fixed-order gather per input pixel in deterministic mode vs the
-    atomic scatter, with a static buffer and a dynamic logical extent as the augment pipe uses it."""
+    """The ADA warp's input gradient: a fixed-order gather per input pixel in deterministic mode (bitwise equal
+    twice), against affine_grid + grid_sample's input gradient in float64 as the atomic scatter is held
+    (test_ops_gpu.py::test_affine_grid_sample), with a static buffer and a dynamic logical extent as the augment
+    pipe uses it."""
     from torch_utils.ops import grid_sample_gradfix as gs
     g = torch.Generator().manual_seed(4)
-    x = torch.randn(3, 3, 140, 136, generator=g).to(DEV).requires_grad_(True)
+    x = torch.randn(3, 3, 140, 136, generator=g)
     theta = torch.tensor([[[1.05, 0.1, 0.03], [-0.08, 0.95, -0.02]], [[0.9, -0.2, 0.1], [0.15, 1.1, 0.05]],
-                          [[0.7, 0.0, -0.2], [0.0, 1.3, 0.1]]], device=DEV)
+                          [[0.7, 0.0, -0.2], [0.0, 1.3, 0.1]]])
     size = [3, 3, 150, 146]
-    dyn = torch.tensor([130, 128], dtype=torch.int32, device=DEV)
-    dy = torch.randn(size, generator=g).to(DEV)
+    dy = torch.randn(size, generator=g)
+    grid = F.affine_grid(theta.double(), size, align_corners=False)
+    xd = x.to(DEV).requires_grad_(True)
+    refs = []
+    for hw in (None, (130, 128)):
+        xr = (x if hw is None else x[:, :, :hw[0], :hw[1]]).double().requires_grad_(True)
+        gr, = torch.autograd.grad(F.grid_sample(xr, grid, align_corners=False), [xr], dy.double())
+        refs.append(gr if hw is None else F.pad(gr, [0, 136 - hw[1], 0, 140 - hw[0]]))
 
     def fn():
         out = []
-        for d in (None, dyn):
-            y = gs.affine_grid_sample(x, theta, size, dyn_hw=d)
-            gx, = torch.autograd.grad(y, [x], dy)
-            out.append(gx)
+        for hw in (None, (130, 128)):
+            dyn = None if hw is None else torch.tensor(hw, dtype=torch.int32, device=DEV)
+            y = gs.affine_grid_sample(xd, theta.to(DEV), size, dyn_hw=dyn)
+            gx, = torch.autograd.grad(y, [xd], dy.to(DEV))
+            out.append(gx if hw is None else gx[:, :, :hw[0], :hw[1]])
         return out
-    _check(fn, 1e-6)
+    with sg2hip.deterministic():
+        a = [t.clone() for t in fn()]
+        b = [t.clone() for t in fn()]
+    fast = fn()
+    for i, (u, v, w, r) in enumerate(zip(a, b, fast, refs)):
+        r = r if i == 0 else r[:, :, :130, :128]
+        assert torch.equal(u, v), f'extent {i}: deterministic runs differ'
+        assert rel_err(u, r) < 1e-5 and rel_err(w, r) < 1e-5, (rel_err(u, r), rel_err(w, r))
 
 
 def test_det_dot_hw_and_vjp_axpy():
