@@ -77,6 +77,7 @@ struct ConvArgs {
     int nck;                 // ceil(Cin / BK)
     int splits, kper;        // K split: kper chunks per split
     int64_t det_stride;      // deterministic mode: split s stores its partial sums at acc + s * det_stride
+    int64_t xpl, wpl;        // SG2_F32S3 operands: elements between the h / m / l bf16 planes of x and w
     Phase ph[kMaxPhases];
     Tap taps[kMaxTaps];
 };
@@ -130,6 +131,33 @@ __device__ __forceinline__ void split3x4(float x0, float x1, float x2, float x3,
     h = __builtin_bit_cast(bf16x4_s3, u32x2_t{hu[0], hu[1]});
     m = __builtin_bit_cast(bf16x4_s3, u32x2_t{mu[0], mu[1]});
     l = __builtin_bit_cast(bf16x4_s3, u32x2_t{lu[0], lu[1]});
+}
+
+// sg2_split3: planes[p * n + i] = piece p of x[i] * scale[n_of(i), i % C]; 8 elements a lane (one 32-byte load, three
+// 16-byte stores), the same arithmetic as the kernels' in-loop split (split3x4: round-to-nearest-even residuals)
+__global__ __launch_bounds__(256) void split3_kernel(bf16_t* planes, const float* x, int64_t n, int C, int64_t pix_per_n,
+                                                     const float* scale) {
+    const int64_t groups = n / 8;
+    for (int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gi < groups; gi += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = gi * 8;
+        const float4 v0 = *(const float4*)(x + i), v1 = *(const float4*)(x + i + 4);
+        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        if (scale) {
+            const int64_t pix = i / C;
+            const int c = (int)(i - pix * C);
+            const float* sp = scale + (pix / pix_per_n) * C + c;
+            const float4 s0 = *(const float4*)sp, s1 = *(const float4*)(sp + 4);
+            const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = __fmul_rn(v[j], sv[j]);   // the rounded product, as the kernels' staging
+        }
+        bf16x4_s3 h0, m0, l0, h1, m1, l1;
+        split3x4(v[0], v[1], v[2], v[3], h0, m0, l0);
+        split3x4(v[4], v[5], v[6], v[7], h1, m1, l1);
+        *(bf16x8*)(planes + i) = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        *(bf16x8*)(planes + n + i) = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
+        *(bf16x8*)(planes + 2 * n + i) = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
 }
 
 // acc += a * b over the six significant products of the split operands (small terms first)
@@ -408,10 +436,14 @@ __global__ __launch_bounds__(256) void conv1x1_smallo_kernel(ConvArgs a) {
     }
 }
 
-template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI, bool S3>
+// P3 (with S3): the operands arrive pre-split (SG2_F32S3, sg2_split3): three bf16 planes in HBM, loaded as whole
+// 16-byte pieces (8 elements a lane) straight into the LDS planes -- no split VALU in the K loop, and each element
+// is split once per call instead of once per workgroup that stages it.
+template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI, bool S3, bool P3 = false>
 __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
     static_assert(!S3 || std::is_same<T, float>::value, "the split form is for f32 operands");
-    constexpr int BK = KStage<T, S3>::BK, V = Traits<T>::V;
+    static_assert(!P3 || (S3 && VEC && !SI), "pre-split operands: the split form, vector loads, scale folded in");
+    constexpr int BK = KStage<T, S3>::BK, V = P3 ? 8 : Traits<T>::V;
     constexpr int LPR = BK / V;          // lanes per tile row
     constexpr int RPP = 256 / LPR;       // rows per load pass
     constexpr int PA = BM / RPP, PB = BN / RPP;
@@ -466,8 +498,10 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
     const int k_begin = split * a.kper;
     const int k_end = min(nk, k_begin + a.kper);
 
-    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, (int64_t)a.N * a.H * a.W * a.Cin * (int64_t)sizeof(T));
-    const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, (int64_t)a.Cout * wrow * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, P3 ? 6 * a.xpl : (int64_t)a.N * a.H * a.W * a.Cin * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(w, P3 ? 6 * a.wpl : (int64_t)a.Cout * wrow * (int64_t)sizeof(T));
+    const int xplb = (int)(2 * a.xpl), wplb = (int)(2 * a.wpl);   // plane strides in bytes (P3)
+    bf16x8 r3a[P3 ? PA : 1][3], r3b[P3 ? PB : 1][3];
     vecT ra[PA], rb[PB];
     bool ra_ok[PA], rb_ok[PB];
     float rsc[SI ? PA : 1][V];
@@ -479,6 +513,25 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
         const Tap tp = a.taps[tap0 + t];
         const int dy = tp.dy, dx = tp.dx, wt = tp.w;
         const int tapoff = (dy * a.W + dx) * a.Cin;
+        if constexpr (P3) {
+#pragma unroll
+            for (int i = 0; i < PA; ++i) {
+                const int iy = a_qy[i] + dy, ix = a_qx[i] + dx;
+                const bool ok = a_ok[i] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W && c < a.Cin;
+                const int off = ok ? (a_base[i] + tapoff + c) * 2 : -1;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) r3a[i][p] = buf_load16<bf16x8>(rx, ok ? off + p * xplb : -1);
+            }
+            const int woff = wt * a.Cin;
+#pragma unroll
+            for (int i = 0; i < PB; ++i) {
+                const bool ok = b_ok[i] && c < a.Cin;
+                const int off = ok ? (b_base[i] + woff + c) * 2 : -1;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) r3b[i][p] = buf_load16<bf16x8>(rw, ok ? off + p * wplb : -1);
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             const int iy = a_qy[i] + dy, ix = a_qx[i] + dx;
@@ -524,6 +577,19 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
         *(bf16x4_t*)(p + 2 * PLANE) = l;
     };
     auto sstore = [&](int buf) {
+        if constexpr (P3) {   // whole 16-byte pieces of each plane, the same swizzled rows as store3
+            char* P = (char*)(lds3 + buf * BUF3);
+#pragma unroll
+            for (int i = 0; i < PA; ++i)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) *(bf16x8*)(P + p * PLANE * 2 + swz64(lrow + i * RPP, lcol >> 3)) = r3a[i][p];
+#pragma unroll
+            for (int i = 0; i < PB; ++i)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    *(bf16x8*)(P + p * PLANE * 2 + swz64(BM + lrow + i * RPP, lcol >> 3)) = r3b[i][p];
+            return;
+        }
         T* As = lds + buf * BUF;
         T* Bs = As + BM * LDK;
 #pragma unroll
@@ -531,7 +597,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
             vecT v = VEC ? ra[i] : Loader<T, VEC>::mask(ra[i], cur_c, a.Cin, ra_ok[i]);
             if (SI) {
 #pragma unroll
-                for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * rsc[i][j]);
+                for (int j = 0; j < V; ++j) v[j] = (T)__fmul_rn((float)v[j], rsc[i][j]);   // rounded product (no fma contraction)
             }
             if constexpr (S3) store3(buf, lrow + i * RPP, v);
             else if constexpr (sizeof(T) == 2) *(vecT*)((char*)As + swz64(lrow + i * RPP, lcol >> 3)) = v;
@@ -814,9 +880,9 @@ size_t fwd_lds_bytes() {
     return std::max(main, epi);
 }
 
-template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI, bool S3>
+template <typename T, int BM, int BN, bool VEC, bool SPLIT, bool SI, bool S3, bool P3 = false>
 int launch_fwd_k(ConvArgs& a, dim3 grid, hipStream_t s) {
-    auto kern = conv_fwd_kernel<T, BM, BN, VEC, SPLIT, SI, S3>;
+    auto kern = conv_fwd_kernel<T, BM, BN, VEC, SPLIT, SI, S3, P3>;
     const size_t lds = fwd_lds_bytes<T, BM, BN, S3>();
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
@@ -835,6 +901,10 @@ int launch_fwd(ConvArgs& a, bool vec, hipStream_t s) {
         if (a.ph[i].M > 0) { maxM = std::max(maxM, a.ph[i].M); nph = i + 1; }
     dim3 grid((unsigned)cdiv(maxM, BM), (unsigned)cdiv(a.Cout, BN), (unsigned)(nph * a.splits));
     constexpr bool F32 = std::is_same<T, float>::value;
+    if (F32 && a.xpl) {      // pre-split operands (SG2_F32S3)
+        if (a.splits > 1) return launch_fwd_k<T, BM, BN, true, true, false, F32, F32>(a, grid, s);
+        return launch_fwd_k<T, BM, BN, true, false, false, F32, F32>(a, grid, s);
+    }
     if (F32 && !f32_exact()) {
 #define LF(V_, S_) return a.in_scale ? launch_fwd_k<T, BM, BN, V_, S_, true, F32>(a, grid, s) \
                                      : launch_fwd_k<T, BM, BN, V_, S_, false, F32>(a, grid, s)
@@ -863,6 +933,7 @@ struct WgradArgs {
     int splits;
     float alpha;     // dw += alpha * (partial sums): a layer's weight gain folded in
     float* det;      // deterministic mode: partial sums by slot (split / lane row), summed by det_sum
+    int64_t gpl, xpl;   // SG2_F32S3 operands: elements between the h / m / l bf16 planes of g and x
 };
 
 template <typename T>
@@ -993,10 +1064,11 @@ __global__ __launch_bounds__(256) void wgrad1x1_smalla_kernel(WgradArgs a) {
     for (int i = threadIdx.x; i < a.A * a.B; i += 256) atomicAdd(a.dw + i, red[i] * a.alpha);
 }
 
-template <typename T, int BM, int BN, bool VEC, bool S3>
+template <typename T, int BM, int BN, bool VEC, bool S3, bool P3 = false>
 __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a) {
     static_assert(!S3 || std::is_same<T, float>::value, "the split form is for f32 operands");
-    constexpr int BK = KStage<T, S3>::BK, V = Traits<T>::V;
+    static_assert(!P3 || (S3 && VEC), "pre-split operands: the split form with vector loads");
+    constexpr int BK = KStage<T, S3>::BK, V = P3 ? 8 : Traits<T>::V;
     constexpr int LDA = BM + V, LDB = BN + V;   // padded pixel-major rows
     constexpr int LPA = BM / V, LPB = BN / V;   // lanes per row
     constexpr int RPA = 256 / LPA, RPB = 256 / LPB;
@@ -1029,8 +1101,10 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
     const int ky = tap / a.KW, kx = tap % a.KW;
     const T* __restrict__ g = (const T*)a.g;
     const T* __restrict__ x = (const T*)a.x;
-    const __amdgpu_buffer_rsrc_t rgw = make_rsrc(g, (int64_t)a.M * a.A * (int64_t)sizeof(T));
-    const __amdgpu_buffer_rsrc_t rxw = make_rsrc(x, (int64_t)a.N * a.H * a.W * a.B * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rgw = make_rsrc(g, P3 ? 6 * a.gpl : (int64_t)a.M * a.A * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rxw = make_rsrc(x, P3 ? 6 * a.xpl : (int64_t)a.N * a.H * a.W * a.B * (int64_t)sizeof(T));
+    const int gplb = (int)(2 * a.gpl), xplb = (int)(2 * a.xpl);
+    bf16x8 r3a[P3 ? PA : 1][3], r3b[P3 ? PB : 1][3];
 
     const int ga_row = tid / LPA, ga_col = (tid % LPA) * V;
     const int xb_row = tid / LPB, xb_col = (tid % LPB) * V;
@@ -1041,6 +1115,33 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
     bool ra_ok[PA], rb_ok[PB];
     float rsc[PB][V], asc[PA][V];
     auto gload = [&](int p0) {
+        if constexpr (P3) {   // scales folded into the planes by sg2_split3
+#pragma unroll
+            for (int i = 0; i < PA; ++i) {
+                const int r = ga_row + i * RPA;
+                const int m = p0 + r;
+                const bool ok = r < BK && m < p_end && a0 + ga_col < a.A;
+                const int off = ok ? (m * a.A + a0 + ga_col) * 2 : -1;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) r3a[i][q] = buf_load16<bf16x8>(rgw, ok ? off + q * gplb : -1);
+            }
+#pragma unroll
+            for (int i = 0; i < PB; ++i) {
+                const int r = xb_row + i * RPB;
+                const int m = p0 + r;
+                bool ok = r < BK && m < p_end;
+                const int mm = ok ? m : 0;
+                const int per = a.OH * a.OW;
+                const int n = mm / per;
+                const int rr = mm - n * per;
+                const int iy = (rr / a.OW) * a.stride + ky - a.pady, ix = (rr % a.OW) * a.stride + kx - a.padx;
+                ok = ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W && b0 + xb_col < a.B;
+                const int off = ok ? (((n * a.H + iy) * a.W + ix) * a.B + b0 + xb_col) * 2 : -1;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) r3b[i][q] = buf_load16<bf16x8>(rxw, ok ? off + q * xplb : -1);
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
             const int r = ga_row + i * RPA;
@@ -1115,6 +1216,26 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
         }
     };
     auto sstore = [&](int buf) {
+        if constexpr (P3) {
+#pragma unroll
+            for (int i = 0; i < PA; ++i) {
+                const int r = ga_row + i * RPA;
+                if (r < BK) {
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) *(bf16x8*)(lds3 + buf * 3 * PL3 + q * PL3 + r * LDA3 + ga_col) = r3a[i][q];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < PB; ++i) {
+                const int r = xb_row + i * RPB;
+                if (r < BK) {
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        *(bf16x8*)(lds3 + buf * 3 * PL3 + q * PL3 + BK * LDA3 + r * LDB3 + xb_col) = r3b[i][q];
+                }
+            }
+            return;
+        }
         T* As = lds[buf];
         T* Bs = lds[buf] + BK * LDA;
 #pragma unroll
@@ -1123,7 +1244,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
             vecT v = VEC ? ra[i] : Loader<T, VEC>::mask(ra[i], a0 + ga_col, a.A, ra_ok[i]);
             if (a.a_scale) {
 #pragma unroll
-                for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * asc[i][j]);
+                for (int j = 0; j < V; ++j) v[j] = (T)__fmul_rn((float)v[j], asc[i][j]);
             }
             if constexpr (S3) {
                 if (r < BK) store3(buf, r * LDA3 + ga_col, v);
@@ -1137,7 +1258,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
             vecT v = VEC ? rb[i] : Loader<T, VEC>::mask(rb[i], b0 + xb_col, a.B, rb_ok[i]);
             if (a.b_scale) {
 #pragma unroll
-                for (int j = 0; j < V; ++j) v[j] = (T)((float)v[j] * rsc[i][j]);
+                for (int j = 0; j < V; ++j) v[j] = (T)__fmul_rn((float)v[j], rsc[i][j]);   // rounded product (no fma contraction)
             }
             if constexpr (S3) {
                 if (r < BK) store3(buf, BK * LDA3 + r * LDB3 + xb_col, v);
@@ -1245,7 +1366,7 @@ __global__ __launch_bounds__(256, S3 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a
 template <typename T, int BM, int BN>
 int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
     constexpr bool F32 = std::is_same<T, float>::value;
-    const bool s3 = F32 && !f32_exact();
+    const bool s3 = F32 && (a.gpl || !f32_exact());
     const int BK = s3 ? KStage<float, true>::BK : Traits<T>::BK;
     const int mt = (int)cdiv(a.A, BM), nt = (int)cdiv(a.B, BN);
     const int KK = a.KH * a.KW;
@@ -1260,7 +1381,9 @@ int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
     const int64_t nel = (int64_t)a.A * KK * a.B;
     if (det_on()) SG2_DET_GET(a.det, arena, a.splits * nel, "sg2_conv2d_wgrad");
     dim3 grid(mt, nt, KK * a.splits);
-    if (s3) {
+    if (F32 && a.gpl) {      // pre-split operands (SG2_F32S3)
+        conv_wgrad_kernel<T, BM, BN, true, F32, F32><<<grid, 256, 0, s>>>(a);
+    } else if (s3) {
         if (vec) conv_wgrad_kernel<T, BM, BN, true, F32><<<grid, 256, 0, s>>>(a);
         else conv_wgrad_kernel<T, BM, BN, false, F32><<<grid, 256, 0, s>>>(a);
     } else {
@@ -1304,9 +1427,20 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
                   "sg2_conv2d: bad epilogue aux output");
     }
     hipStream_t s = as_stream(stream);
+    // SG2_F32S3: x and w are sg2_split3 planes (h, m, l), everything else f32
+    const bool p3 = dtype == SG2_F32S3;
+    if (p3) {
+        SG2_CHECK(in_scale == nullptr, "sg2_conv2d: SG2_F32S3 operands carry their modulation (sg2_split3 scale)");
+        SG2_CHECK(Cin % 8 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)w % 16 == 0,
+                  "sg2_conv2d: SG2_F32S3 needs Cin % 8 == 0 and 16-byte aligned planes");
+        SG2_CHECK((int64_t)N * H * W * Cin * 6 < INT32_MAX && (int64_t)Cout * KH * KW * Cin * 6 < INT32_MAX,
+                  "sg2_conv2d: SG2_F32S3 planes too large (32-bit byte offsets)");
+        dtype = SG2_F32;
+    }
 
     ConvArgs base{};
     base.x = x; base.w = w; base.y = y; base.acc = nullptr; base.in_scale = in_scale;
+    if (p3) { base.xpl = (int64_t)N * H * W * Cin; base.wpl = (int64_t)Cout * KH * KW * Cin; }
     base.N = N; base.H = H; base.W = W; base.Cin = Cin; base.Cout = Cout; base.OH = OH; base.OW = OW;
     base.wtaps = KH * KW;
     if (epi) {
@@ -1363,7 +1497,7 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
     }
 
     int rc = 0;
-    if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W && Cout <= 4 &&
+    if (!p3 && KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W && Cout <= 4 &&
         Cin % 8 == 0 && Cin >= 8 && !base.e.dot_out && (uintptr_t)x % 16 == 0 && (uintptr_t)w % 16 == 0 &&
         (uintptr_t)in_scale % 16 == 0 && dtype != SG2_F32) {
         const int64_t groups = (int64_t)N * H * W;
@@ -1372,7 +1506,7 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
         return launch_status("sg2_conv2d (1x1, small Cout)");
     }
     // (a 1x1 stride-1 transposed conv is the same product with the caller's transposed pack: dgrad of toRGB)
-    if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W &&
+    if (!p3 && KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W &&
         Cin <= 4 && Cout % 8 == 0 && 256 % (Cout / 8) == 0 && (uintptr_t)y % 32 == 0 &&
         (!base.e.aux || (uintptr_t)base.e.aux % 32 == 0) && (!base.e.residual || (uintptr_t)base.e.residual % 32 == 0) &&
         (!base.e.dot_out || (uintptr_t)base.e.dot_src % 16 == 0)) {
@@ -1396,9 +1530,9 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
     }
     SG2_DISPATCH(dtype, T, {
         constexpr int V = Traits<T>::V;
-        const int BK = (std::is_same<T, float>::value && !f32_exact()) ? KStage<float, true>::BK : Traits<T>::BK;
-        const bool vec = (Cin % V == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)w % 16 == 0) &&
-                         ((uintptr_t)in_scale % 16 == 0);
+        const int BK = (std::is_same<T, float>::value && (p3 || !f32_exact())) ? KStage<float, true>::BK : Traits<T>::BK;
+        const bool vec = p3 || ((Cin % V == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)w % 16 == 0) &&
+                                ((uintptr_t)in_scale % 16 == 0));
         const bool wide = Cout > 64;
         const int BN_ = wide ? 128 : 64;
         base.nck = (Cin + BK - 1) / BK;
@@ -1492,6 +1626,14 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     SG2_CHECK((int64_t)N * OH * OW * A * 4 < INT32_MAX && (int64_t)N * H * W * B * 4 < INT32_MAX,
               "sg2_conv2d_wgrad: tensor too large (32-bit byte offsets of the buffer loads)");
     hipStream_t s = as_stream(stream);
+    const bool p3 = dtype == SG2_F32S3;
+    if (p3) {
+        SG2_CHECK(!g_scale && !x_scale, "sg2_conv2d_wgrad: SG2_F32S3 operands carry their scales (sg2_split3)");
+        SG2_CHECK(A % 8 == 0 && B % 8 == 0 && (uintptr_t)g % 16 == 0 && (uintptr_t)x % 16 == 0,
+                  "sg2_conv2d_wgrad: SG2_F32S3 needs A, B % 8 == 0 and 16-byte aligned planes");
+        SG2_CHECK((int64_t)N * OH * OW * A * 6 < INT32_MAX && (int64_t)N * H * W * B * 6 < INT32_MAX,
+                  "sg2_conv2d_wgrad: SG2_F32S3 planes too large (32-bit byte offsets)");
+    }
     hipError_t e = zero_acc(dw, (int64_t)A * KH * KW * B * sizeof(float), s);
     if (e != hipSuccess) { set_error("sg2_conv2d_wgrad: memset failed"); return (int)e; }
     WgradArgs a{};
@@ -1499,6 +1641,16 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     a.N = N; a.A = A; a.OH = OH; a.OW = OW; a.B = B; a.H = H; a.W = W; a.KH = KH; a.KW = KW;
     a.stride = stride; a.pady = pad_y; a.padx = pad_x; a.alpha = alpha;
     a.M = N * OH * OW;
+    if (p3) {
+        a.gpl = (int64_t)N * OH * OW * A;
+        a.xpl = (int64_t)N * H * W * B;
+        int rc = 0;
+        if (A > 64 && B > 64) rc = launch_wgrad<float, 128, 128>(a, true, s);
+        else if (A > 64) rc = launch_wgrad<float, 128, 64>(a, true, s);
+        else if (B > 64) rc = launch_wgrad<float, 64, 128>(a, true, s);
+        else rc = launch_wgrad<float, 64, 64>(a, true, s);
+        return rc;
+    }
     if (KH == 1 && KW == 1 && stride == 1 && pad_y == 0 && pad_x == 0 && OH == H && OW == W && B <= 4 &&
         A % 8 == 0 && 256 % (A / 8) == 0 && A * B <= 2048 && (uintptr_t)g % 16 == 0) {
         const int g_ = (int)std::min<int64_t>(cdiv((int64_t)a.M * (A / 8), 256), 1024);
@@ -1540,4 +1692,17 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
         else rc = launch_wgrad<T, 64, 64>(a, vec, s);
     });
     return rc;
+}
+
+extern "C" int sg2_split3(void* planes, const float* x, int64_t n, int C, int64_t pix_per_n, const float* scale,
+                          void* stream) {
+    using namespace sg2;
+    SG2_CHECK(planes && x, "sg2_split3: null pointer");
+    SG2_CHECK(C > 0 && C % 8 == 0 && n % C == 0 && pix_per_n > 0, "sg2_split3: C % 8 == 0 and n a multiple of C");
+    SG2_CHECK((uintptr_t)planes % 16 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)scale % 16 == 0,
+              "sg2_split3: 16-byte alignment required");
+    if (n == 0) return 0;
+    const int g = (int)std::min<int64_t>(cdiv(n / 8, 256), 256 * 64);
+    split3_kernel<<<g, 256, 0, as_stream(stream)>>>((bf16_t*)planes, x, n, C, pix_per_n, scale);
+    return launch_status("sg2_split3");
 }

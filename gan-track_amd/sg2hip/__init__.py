@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SG2HIP_LIB', os.path.join(_HERE, 'libsg2hip.so'))
 
-F32, F16, BF16 = 0, 1, 2
+F32, F16, BF16, F32S3 = 0, 1, 2, 3
 _DTYPES = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16}
 
 _c_i64p = ctypes.POINTER(ctypes.c_int64)
@@ -46,6 +46,7 @@ SIGNATURES = {
     'sg2_set_zeroed_accumulators': [_i],
     'sg2_set_clean_workspace': [_i],
     'sg2_set_deterministic': [_vp, _i64],
+    'sg2_split3': [_vp, _vp, _i64, _i, _i64, _vp, _vp],
     'sg2_conv3x3_s2': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _i, _f, _f, _f, _vp, _i,
                        _vp, _vp, _vp],
     'sg2_conv3x3_up2': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp],
@@ -70,7 +71,7 @@ SIGNATURES = {
     'sg2_infnorm_bwd': [_vp, _vp, _vp, _vp, _i, _i, _f, _i, _vp],
     'sg2_pack_weight': [_vp, _i, _vp, _i, _i, _i, _i, _i64, _i64, _i64, _i, _f, _vp],
 }
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lib = None
 

@@ -53,6 +53,46 @@ def _nhwc(t):
     return t
 
 
+# f32 convolutions (the 4^2..16^2 blocks) on pre-split operands: each f32 operand is split ONCE per call into its
+# three bf16 planes (sg2_split3, with the layer's modulation folded in) and the kernels stage the planes directly
+# (SG2_F32S3) instead of every workgroup re-splitting its tiles inside the K loop; bitwise the same arithmetic
+# (tests/test_ops_gpu.py::test_presplit_f32_bitwise).  SG2_P3=0 keeps the in-loop split (A/B switch).
+presplit = os.environ.get('SG2_P3', '1') != '0' and os.environ.get('SG2_F32_EXACT', '0') != '1'
+# the forward / input-gradient convolutions measured no faster on pre-split operands (tools/f32_ab.py: 16^2 bs64
+# 0.484 -> 0.430 ms with the split included, 8^2 and 4^2 0.082 -> 0.085 / 0.044 -> 0.055): the weight gradients
+# alone take them (0.611 -> 0.488, 0.312 -> 0.257, 0.124 -> 0.111 ms)
+presplit_fwd = os.environ.get('SG2_P3_FWD', '0') != '0'
+
+
+def split3(x, scale=None, packed=False):
+    """f32 activation [N, C, H, W] (NHWC memory), or (packed) a packed weight [.., C] in its memory order ->
+    [3, numel] bf16 planes of x * scale[n, c]."""
+    C = x.shape[-1] if packed else x.shape[1]
+    per = 1 if packed else x.shape[2] * x.shape[3]
+    planes = torch.empty([3, x.numel()], dtype=torch.bfloat16, device=x.device)
+    sc = scale.float().contiguous() if scale is not None else None
+    _hip.check(_hip.lib().sg2_split3(_hip.ptr(planes), _hip.ptr(x), x.numel(), C, per, _hip.ptr(sc),
+                                     _hip.stream_ptr(x.device)), 'sg2_split3')
+    return planes
+
+
+def _split_w(wp):
+    """The planes of a packed f32 weight, cached with the pack inside a pack_cache() scope."""
+    key = ('s3', wp.data_ptr(), wp._version, tuple(wp.shape))
+    if _pack_cache is not None:
+        hit = _pack_cache.get(key)
+        if hit is not None:
+            return hit[0]
+    out = split3(wp.contiguous(), packed=True)
+    if _pack_cache is not None:
+        _pack_cache[key] = (out, wp)
+    return out
+
+
+def _p3(x, cin):
+    return presplit and x.dtype == torch.float32 and cin % 8 == 0 and x.is_cuda
+
+
 _WS_LIMIT = 1 << 23  # split-K f32 workspace only for small outputs (low-resolution layers)
 _CLEAN_WS = {}       # device -> persistent zeroed split-K workspace (every call leaves it zeroed)
 
@@ -118,9 +158,12 @@ def _conv_raw(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose):
     y = torch.empty([n, cout, oh, ow], dtype=x.dtype, device=x.device, memory_format=_CL)
     total = n * cout * oh * ow
     ws, clean = _workspace(x, total)
+    xa, wa, dt = x, wp, _hip.dtype_code(x)
+    if presplit_fwd and _p3(x, cin):
+        xa, wa, dt = split3(_nhwc(x)), _split_w(wp), _hip.F32S3
     with _split_k(x, clean):
         _hip.check(_hip.lib().sg2_conv2d(
-            _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
+            _hip.ptr(y), _hip.ptr(xa), _hip.ptr(wa), dt, n, cin, h, w, cout, oh, ow, kh, kw,
             stride, pad[0], pad[1], int(transpose), _hip.ptr(ws), ws.numel() if ws is not None else 0,
             _hip.stream_ptr(x.device)), 'sg2_conv2d')
     return y
@@ -155,10 +198,13 @@ def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_sca
                             _hip.ptr(dot_src), _hip.ptr(dot))
     total = n * cout * oh * ow
     ws, clean = _workspace(x, total)
+    xa, wa, dt, isc = x, wp, _hip.dtype_code(x), in_scale
+    if presplit_fwd and _p3(x, cin):
+        xa, wa, dt, isc = split3(_nhwc(x), in_scale), _split_w(wp), _hip.F32S3, None
     with _hip.zeroed_accumulators(dot_out is not None and dot is not None), _split_k(x, clean):
         _hip.check(_hip.lib().sg2_conv2d_fused(
-            _hip.ptr(y), _hip.ptr(x), _hip.ptr(wp), _hip.dtype_code(x), n, cin, h, w, cout, oh, ow, kh, kw,
-            stride, pad[0], pad[1], int(transpose), _hip.ptr(in_scale), ctypes.byref(epi) if epi is not None else None,
+            _hip.ptr(y), _hip.ptr(xa), _hip.ptr(wa), dt, n, cin, h, w, cout, oh, ow, kh, kw,
+            stride, pad[0], pad[1], int(transpose), _hip.ptr(isc), ctypes.byref(epi) if epi is not None else None,
             _hip.ptr(ws), ws.numel() if ws is not None else 0, _hip.stream_ptr(x.device)), 'sg2_conv2d_fused')
     return (y, aux, dot) if dot_src is not None else (y, aux)
 
@@ -170,10 +216,13 @@ def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None, alpha=1.0,
     n, a, oh, ow = g.shape
     _, b, h, w = x.shape
     dw = out.view(a, kh, kw, b) if out is not None else torch.empty([a, kh, kw, b], dtype=torch.float32, device=g.device)
+    ga, xa, dt, gs, xs = g, x, _hip.dtype_code(g), g_scale, x_scale
+    if _p3(g, 8) and a % 8 == 0 and b % 8 == 0 and not (kh == 1 and kw == 1 and min(a, b) <= 4):
+        ga, xa, dt, gs, xs = split3(_nhwc(g), g_scale), split3(_nhwc(x), x_scale), _hip.F32S3, None, None
     with _hip.zeroed_accumulators(out is not None):
         _hip.check(_hip.lib().sg2_conv2d_wgrad(
-            _hip.ptr(dw), _hip.ptr(g), _hip.ptr(x), _hip.dtype_code(g), n, a, oh, ow, b, h, w, kh, kw, stride,
-            pad[0], pad[1], _hip.ptr(g_scale), _hip.ptr(x_scale), float(alpha), _hip.stream_ptr(g.device)),
+            _hip.ptr(dw), _hip.ptr(ga), _hip.ptr(xa), dt, n, a, oh, ow, b, h, w, kh, kw, stride,
+            pad[0], pad[1], _hip.ptr(gs), _hip.ptr(xs), float(alpha), _hip.stream_ptr(g.device)),
             'sg2_conv2d_wgrad')
     return dw.permute(0, 3, 1, 2)
 

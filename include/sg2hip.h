@@ -39,9 +39,20 @@
 extern "C" {
 #endif
 
-#define SG2_ABI_VERSION 4
+#define SG2_ABI_VERSION 5
 
-enum sg2_dtype { SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2 };
+enum sg2_dtype { SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2, SG2_F32S3 = 3 };
+
+/* SG2_F32S3 (ABI 5): float32 operands handed over PRE-SPLIT as three bf16 planes h, m, l (x = h + m + l, exact
+ * for normal floats; sg2_split3), each plane the tensor's element order, the planes back to back.  Accepted as
+ * the operand dtype of sg2_conv2d / sg2_conv2d_fused (x and w; the output, epilogue and workspace are float32;
+ * Cin % 8 == 0; in_scale must be folded into x's planes) and of sg2_conv2d_wgrad (g and x; A, B % 8 == 0;
+ * scales folded in).  The f32 convolutions then run the split form's six bf16 MFMA products on operands split
+ * once per call instead of once per workgroup that stages them.
+ *
+ * planes[p * n + i] = piece p of x[i] * scale[(i / C) / pix_per_n, i % C]   (scale NULL = 1; x f32, n elements,
+ * C % 8 == 0, 16-byte aligned) */
+int sg2_split3(void* planes, const float* x, int64_t n, int C, int64_t pix_per_n, const float* scale, void* stream);
 
 /* ABI version of the loaded library (SG2_ABI_VERSION). */
 int sg2_abi_version(void);

@@ -24,6 +24,36 @@ import torch.nn.functional as F
 # float64 to evaluate the exact (rounding-free) answer the fp32 results are judged against.
 REAL = torch.float32
 
+# 16-bit emulation (None, torch.float16 or torch.bfloat16).  The reference on a GPU runs its top num_fp16_res
+# blocks in float16 (networks_stylegan2.py:419-420, :607-608): every op of such a block produces a 16-bit tensor
+# -- computed in f32 by the kernel (cuDNN / the plugins / torch's opmath) and rounded once -- and autograd
+# produces each of those tensors' gradients in 16 bits too.  With EMU16 set, the blocks flagged use_fp16 round
+# every such tensor to EMU16 (forward value and incoming gradient, _Round16) at exactly those points, while the
+# arithmetic in between stays REAL: the oracle then evaluates the reference's 16-bit GPU iteration (to its
+# f32-versus-REAL accumulation difference), the yardstick the product's 16-bit results are held to.
+EMU16 = None
+
+
+class _Round16(torch.autograd.Function):
+    """y = round_to_16bit(x); dL/dx = round_to_16bit(dL/dy) (the gradient of a 16-bit tensor is a 16-bit tensor);
+    differentiable again for the double backward."""
+
+    @staticmethod
+    def forward(ctx, x, dt):
+        ctx.dt = dt
+        return x.to(dt).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _Round16.apply(g, ctx.dt), None
+
+
+def _q(x, on):
+    """Round to the emulated 16-bit type inside a use_fp16 block (identity otherwise)."""
+    if not on or EMU16 is None or x is None:
+        return x
+    return _Round16.apply(x, EMU16)
+
 # =============================================================================================
 # upfirdn2d  (SG3/torch_utils/ops/upfirdn2d.py)
 # =============================================================================================
@@ -69,6 +99,10 @@ def setup_filter(f, normalize=True, flip_filter=False, gain=1, separable=None):
 
 def upfirdn2d(x, f, up=1, down=1, padding=0, flip_filter=False, gain=1):
     """Zero-insert upsample, pad/crop, FIR, decimate.  SG3 upfirdn2d.py:166-211."""
+    return _upfirdn2d_(x, f, up, down, padding, flip_filter, gain)
+
+
+def _upfirdn2d_(x, f, up=1, down=1, padding=0, flip_filter=False, gain=1):
     if f is None:
         f = torch.ones([1, 1], dtype=REAL)
     n, c, h, w = x.shape
@@ -194,7 +228,7 @@ def grid_sample(inp, grid):
 # =============================================================================================
 
 
-def _conv(x, w, stride=1, padding=0, groups=1, transpose=False, flip_weight=True):
+def _conv_(x, w, stride=1, padding=0, groups=1, transpose=False, flip_weight=True):
     if not flip_weight and (w.shape[2] > 1 or w.shape[3] > 1):
         w = w.flip([2, 3])
     if transpose:
@@ -202,7 +236,16 @@ def _conv(x, w, stride=1, padding=0, groups=1, transpose=False, flip_weight=True
     return F.conv2d(x, w, stride=stride, padding=padding, groups=groups)
 
 
-def conv2d_resample(x, w, f=None, up=1, down=1, padding=0, groups=1, flip_weight=True, flip_filter=False):
+def conv2d_resample(x, w, f=None, up=1, down=1, padding=0, groups=1, flip_weight=True, flip_filter=False, q16=False):
+    """q16: every intermediate is a 16-bit tensor (EMU16), as the reference's fp16 blocks run it."""
+    if q16 and EMU16 is not None:
+        def _conv(*a, **k):
+            return _q(_conv_(*a, **k), True)
+
+        def upfirdn2d(*a, **k):
+            return _q(_upfirdn2d_(*a, **k), True)
+    else:
+        _conv, upfirdn2d = _conv_, _upfirdn2d_
     oc, icg, kh, kw = w.shape
     fw, fh = filter_size(f)
     px0, px1, py0, py1 = _pad4(padding)
@@ -261,10 +304,14 @@ def normalize_2nd_moment(x, dim=1, eps=1e-8):
 
 
 def modulated_conv2d(x, weight, styles, noise=None, up=1, down=1, padding=0, resample_filter=None,
-                     demodulate=True, flip_weight=True, fused_modconv=True):
-    """:32-89 (fp32 path; the fp16 pre-normalisation :52-54 applies only to fp16 inputs)."""
+                     demodulate=True, flip_weight=True, fused_modconv=True, q16=False):
+    """:32-89 (the fp16 pre-normalisation :52-54 applies only to fp16 inputs: EMU16 float16 in a q16 block)."""
     n = x.shape[0]
     oc, ic, kh, kw = weight.shape
+    q = q16 and EMU16 is not None
+    if q and EMU16 == torch.float16 and demodulate:                     # :52-54
+        weight = weight * (1 / np.sqrt(ic * kh * kw) / weight.norm(float('inf'), dim=[1, 2, 3], keepdim=True))
+        styles = styles / styles.norm(float('inf'), dim=1, keepdim=True)
     w = dcoefs = None
     if demodulate or fused_modconv:
         w = weight.unsqueeze(0) * styles.reshape(n, 1, -1, 1, 1)
@@ -273,14 +320,15 @@ def modulated_conv2d(x, weight, styles, noise=None, up=1, down=1, padding=0, res
     if demodulate and fused_modconv:
         w = w * dcoefs.reshape(n, -1, 1, 1, 1)
     if not fused_modconv:
-        x = x * styles.reshape(n, -1, 1, 1)
-        x = conv2d_resample(x, weight, f=resample_filter, up=up, down=down, padding=padding, flip_weight=flip_weight)
-        if demodulate and noise is not None:
-            return torch.addcmul(noise, x, dcoefs.reshape(n, -1, 1, 1))
+        x = _q(x * _q(styles, q).reshape(n, -1, 1, 1), q)                  # :69-70, weight.to(x.dtype)
+        x = conv2d_resample(x, _q(weight, q), f=resample_filter, up=up, down=down, padding=padding,
+                            flip_weight=flip_weight, q16=q)
+        if demodulate and noise is not None:                                # fma.fma: one rounding
+            return _q(torch.addcmul(_q(noise, q), x, _q(dcoefs, q).reshape(n, -1, 1, 1)), q)
         if demodulate:
-            return x * dcoefs.reshape(n, -1, 1, 1)
+            return _q(x * _q(dcoefs, q).reshape(n, -1, 1, 1), q)
         if noise is not None:
-            return x + noise
+            return _q(x + _q(noise, q), q)
         return x
     x = x.reshape(1, -1, *x.shape[2:])
     w = w.reshape(-1, ic, kh, kw)
@@ -337,12 +385,12 @@ class Conv2dLayer(torch.nn.Module):
             else:
                 self.bias = None
 
-    def forward(self, x, gain=1):
+    def forward(self, x, gain=1, q16=False):
         w = self.weight * self.weight_gain
-        x = conv2d_resample(x, w, f=self.resample_filter, up=self.up, down=self.down, padding=self.padding,
-                            flip_weight=(self.up == 1))
+        x = conv2d_resample(x, _q(w, q16), f=self.resample_filter, up=self.up, down=self.down, padding=self.padding,
+                            flip_weight=(self.up == 1), q16=q16)
         clamp = self.conv_clamp * gain if self.conv_clamp is not None else None
-        return bias_act(x, self.bias, act=self.activation, gain=self.act_gain * gain, clamp=clamp)
+        return _q(bias_act(x, _q(self.bias, q16), act=self.activation, gain=self.act_gain * gain, clamp=clamp), q16)
 
 
 class MappingNetwork(torch.nn.Module):
@@ -405,7 +453,7 @@ class SynthesisLayer(torch.nn.Module):
             self.noise_strength = torch.nn.Parameter(torch.zeros([]))
         self.bias = torch.nn.Parameter(torch.zeros([out_channels]))
 
-    def forward(self, x, w, noise_mode='random', fused_modconv=True, gain=1):
+    def forward(self, x, w, noise_mode='random', fused_modconv=True, gain=1, q16=False):
         styles = self.affine(w)
         noise = None
         if self.use_noise and noise_mode == 'random':
@@ -414,9 +462,9 @@ class SynthesisLayer(torch.nn.Module):
             noise = self.noise_const * self.noise_strength
         x = modulated_conv2d(x, self.weight, styles, noise=noise, up=self.up, padding=self.padding,
                              resample_filter=self.resample_filter, flip_weight=(self.up == 1),
-                             fused_modconv=fused_modconv)
+                             fused_modconv=fused_modconv, q16=q16)
         clamp = self.conv_clamp * gain if self.conv_clamp is not None else None
-        return bias_act(x, self.bias, act=self.activation, gain=self.act_gain * gain, clamp=clamp)
+        return _q(bias_act(x, _q(self.bias, q16), act=self.activation, gain=self.act_gain * gain, clamp=clamp), q16)
 
 
 class ToRGBLayer(torch.nn.Module):
@@ -430,10 +478,10 @@ class ToRGBLayer(torch.nn.Module):
         self.bias = torch.nn.Parameter(torch.zeros([out_channels]))
         self.weight_gain = 1 / np.sqrt(in_channels * kernel_size ** 2)
 
-    def forward(self, x, w, fused_modconv=True):
+    def forward(self, x, w, fused_modconv=True, q16=False):
         styles = self.affine(w) * self.weight_gain
-        x = modulated_conv2d(x, self.weight, styles, demodulate=False, fused_modconv=fused_modconv)
-        return bias_act(x, self.bias, clamp=self.conv_clamp)
+        x = modulated_conv2d(x, self.weight, styles, demodulate=False, fused_modconv=fused_modconv, q16=q16)
+        return _q(bias_act(x, _q(self.bias, q16), clamp=self.conv_clamp), q16)
 
 
 class SynthesisBlock(torch.nn.Module):
@@ -470,21 +518,24 @@ class SynthesisBlock(torch.nn.Module):
             fused_modconv = self.fused_modconv_default
         if fused_modconv == 'inference_only':
             fused_modconv = not self.training
+        q = self.use_fp16 and EMU16 is not None and not force_fp32          # :419-420 (x.to(dtype) below)
         if self.in_channels == 0:
-            x = self.const.unsqueeze(0).repeat([ws.shape[0], 1, 1, 1])
-            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, **layer_kwargs)
+            x = _q(self.const, q).unsqueeze(0).repeat([ws.shape[0], 1, 1, 1])
+            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, q16=q, **layer_kwargs)
         elif self.architecture == 'resnet':
-            y = self.skip(x, gain=np.sqrt(0.5))
-            x = self.conv0(x, next(w_iter), fused_modconv=fused_modconv, **layer_kwargs)
-            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, gain=np.sqrt(0.5), **layer_kwargs)
-            x = y + x
+            x = _q(x, q)
+            y = self.skip(x, gain=np.sqrt(0.5), q16=q)
+            x = self.conv0(x, next(w_iter), fused_modconv=fused_modconv, q16=q, **layer_kwargs)
+            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, gain=np.sqrt(0.5), q16=q, **layer_kwargs)
+            x = _q(y + x, q)
         else:
-            x = self.conv0(x, next(w_iter), fused_modconv=fused_modconv, **layer_kwargs)
-            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, **layer_kwargs)
+            x = _q(x, q)
+            x = self.conv0(x, next(w_iter), fused_modconv=fused_modconv, q16=q, **layer_kwargs)
+            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, q16=q, **layer_kwargs)
         if img is not None:
             img = upsample2d(img, self.resample_filter)
         if self.is_last or self.architecture == 'skip':
-            y = self.torgb(x, next(w_iter), fused_modconv=fused_modconv).to(REAL)
+            y = self.torgb(x, next(w_iter), fused_modconv=fused_modconv, q16=q).to(REAL)
             img = img + y if img is not None else y
         return x, img
 
@@ -548,6 +599,7 @@ class DiscriminatorBlock(torch.nn.Module):
                  use_fp16=False, fp16_channels_last=False, freeze_layers=0):
         super().__init__()
         self.in_channels, self.resolution, self.architecture = in_channels, resolution, architecture
+        self.use_fp16 = use_fp16
         self.register_buffer('resample_filter', setup_filter(list(resample_filter)))
         self.num_layers = 0
 
@@ -568,17 +620,19 @@ class DiscriminatorBlock(torch.nn.Module):
                                     trainable=trainable(), resample_filter=resample_filter)
 
     def forward(self, x, img, force_fp32=False):
+        q = self.use_fp16 and EMU16 is not None and not force_fp32           # :607-608
+        x = _q(x, q)
         if self.in_channels == 0 or self.architecture == 'skip':
-            y = self.fromrgb(img)
-            x = x + y if x is not None else y
+            y = self.fromrgb(_q(img, q), q16=q)
+            x = _q(x + y, q) if x is not None else y
             img = downsample2d(img, self.resample_filter) if self.architecture == 'skip' else None
         if self.architecture == 'resnet':
-            y = self.skip(x, gain=np.sqrt(0.5))
-            x = self.conv0(x)
-            x = self.conv1(x, gain=np.sqrt(0.5))
-            x = y + x
+            y = self.skip(x, gain=np.sqrt(0.5), q16=q)
+            x = self.conv0(x, q16=q)
+            x = self.conv1(x, gain=np.sqrt(0.5), q16=q)
+            x = _q(y + x, q)
         else:
-            x = self.conv1(self.conv0(x))
+            x = self.conv1(self.conv0(x, q16=q), q16=q)
         return x, img
 
 

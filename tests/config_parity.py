@@ -108,17 +108,20 @@ def run_oracle(cfg, inp, tape, aug_p=0.3, perturb=0.0, isolated=False):
     return out, [(n, v.numpy()) for n, v in stats]
 
 
-def run_oracle_f64(cfg, inp, tape, aug_p=0.3, perturb=0.0, isolated=False):
+def run_oracle_f64(cfg, inp, tape, aug_p=0.3, perturb=0.0, isolated=False, emu16=None):
     """The oracle evaluated in float64 on the same draws: the rounding-free answer that f32 results (the
-    reference's and the product's alike) are judged against."""
+    reference's and the product's alike) are judged against.  emu16 (torch.float16 / bfloat16): the reference's
+    16-bit GPU iteration instead -- its num_fp16_res blocks with every tensor rounded where the reference's is
+    (oracle.sg2_oracle.EMU16), float64 in between."""
     from oracle import sg2_oracle as O
-    prev = (O.REAL, torch.get_default_dtype())
+    prev = (O.REAL, torch.get_default_dtype(), O.EMU16)
     O.REAL = torch.float64
+    O.EMU16 = emu16
     torch.set_default_dtype(torch.float64)
     try:
         return run_oracle(cfg, inp, tape, aug_p, perturb, isolated)
     finally:
-        O.REAL = prev[0]
+        O.REAL, O.EMU16 = prev[0], prev[2]
         torch.set_default_dtype(prev[1])
 
 
@@ -258,10 +261,19 @@ def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
     err, worst ratio to the bound, its tensor)}, sorted ratios); raises after computing everything when
     `check` and any tensor is out of bounds."""
     truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
+    cond = {k[5:]: v for k, v in fix.items() if k.startswith('f64p/')}
     kw, kg = _keys(truth, groups), _keys(got, groups)
     _one_sided_zero(got, truth, kg, kw)
     keys = sorted(set(kw) & set(kg))
     errs = {k: (_tensor_errs(got, truth, k), _tensor_errs(fix, truth, k)) for k in keys}
+    # with conditioning summaries (f64p/: float64 at a nudged state) a tensor's reference error term is the larger
+    # of the reference's f32 error and the conditioning shift -- both are samples of the spread any f32
+    # evaluation of that tensor has
+    for k in keys:
+        if k + '/norm' in cond:
+            (gn, gs), (rn, rs_) = errs[k]
+            cn, cs = _tensor_errs(cond, truth, k)
+            errs[k] = ((gn, gs), (max(rn, cn), max(rs_, cs)))
     gmax = {}
     for k, (_, (rn, rs_)) in errs.items():
         m = gmax.get(_group(k), (0.0, 0.0))
@@ -294,11 +306,13 @@ def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/',), check=T
     evaluations (measured: D1/b512.conv1.bias at C4 / p = 0); the parameters are held by the flat check.
     Returns (number of tensors checked, worst error, its key)."""
     truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
+    cond = {k[5:]: v for k, v in fix.items() if k.startswith('f64p/')}
     keys = sorted(set(_keys(truth, groups)) & set(_keys(got, groups)))
     n, worst, wk, fails = 0, 0.0, '', []
     for k in keys:
         rn, rs_ = _tensor_errs(fix, truth, k)
-        if max(rn, rs_) >= well or float(fix[k + '/norm']) == 0.0:
+        cn, cs = _tensor_errs(cond, truth, k) if k + '/norm' in cond else (0.0, 0.0)
+        if max(rn, rs_, cn, cs) >= well or float(fix[k + '/norm']) == 0.0:
             continue
         n += 1
         en, es = _tensor_errs(got, fix, k)

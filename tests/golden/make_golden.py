@@ -492,7 +492,7 @@ def gen_config_iteration(tag, cfg, input_seed=31, tape_seed=13, aug_p=0.3, isola
 P0_CONFIGS = {f'{k}p0': k for k in ('c2', 'c4', 'c5')}
 
 
-def gen_conditioning(tag, cache_dir=None):
+def gen_conditioning(tag, cache_dir=None, perturb=2.0 ** -24):
     """Add 'f64p/...' to train_<tag>.npz: the float64 oracle on the fixture's state, inputs and draws with
     every parameter, real image and latent nudged by a factor (1 +- 2^-24) -- half an f32 ulp, a fixed random
     sign per entry (config_parity.run_oracle).  How far that moves each result from the float64 answer is the
@@ -513,10 +513,33 @@ def gen_conditioning(tag, cache_dir=None):
         with np.load(cached, allow_pickle=False) as f:
             out = unpack(f)
     else:
-        out, _ = cp.run_oracle_f64(cfg, inp, tape, cfg.get('aug_p', 0.3), perturb=2.0 ** -24)
+        out, _ = cp.run_oracle_f64(cfg, inp, tape, cfg.get('aug_p', 0.3), perturb=perturb,
+                                   isolated=cfg.get('isolated', False))
     z.update({f'f64p/{k}': v for k, v in out.items()})
+    z['f64p_perturb'] = np.array(perturb, np.float64)
     np.savez_compressed(path, **pack(z))
     print(tag, 'conditioning written', flush=True)
+
+def gen_emulated16(tag, dt):
+    """Add 'q16/...' (dt fp16) or 'qbf/...' (bf16) to train_<tag>.npz: the oracle's emulation of the reference's
+    16-bit GPU evaluation of the fixture (oracle.sg2_oracle.EMU16: the num_fp16_res = 4 blocks round every tensor
+    and gradient where the reference's fp16 blocks do), float64 otherwise.  Its distance from the float64 answer
+    is the reference's own 16-bit error, the yardstick of the product's 16-bit tests."""
+    import config_parity as cp
+    from golden_init import unpack
+    path = os.path.join(OUT, f'train_{tag}.npz')
+    with np.load(path, allow_pickle=False) as f:
+        z = unpack(f)
+    with np.load(path, allow_pickle=False) as f:
+        cfg, inp, tape, _ = cp.load_fixture(f)
+    pre = {'fp16': 'q16', 'bf16': 'qbf'}[dt]
+    z = {k: v for k, v in z.items() if not k.startswith(pre + '/')}
+    out, _ = cp.run_oracle_f64(cfg, inp, tape, cfg.get('aug_p', 0.3), isolated=cfg.get('isolated', False),
+                               emu16={'fp16': torch.float16, 'bf16': torch.bfloat16}[dt])
+    z.update({f'{pre}/{k}': v for k, v in out.items()})
+    np.savez_compressed(path, **pack(z))
+    print(tag, dt, 'emulation written', flush=True)
+
 
 if __name__ == '__main__':
     which = sys.argv[1:] or ['ops', 'nets'] + list(CONFIGS)
@@ -532,9 +555,12 @@ if __name__ == '__main__':
             base = parts[1][:-2] if parts[1].endswith('p0') else parts[1]
             cfg_i = dict(CONFIGS[base], **({'batch': int(parts[2])} if len(parts) > 2 else {}))
             gen_config_iteration(parts[1], cfg_i, aug_p=0.0 if parts[1].endswith('p0') else 0.3, isolated=True)
-        if w.startswith('cond:'):          # cond:<tag>[:<cache dir>]
+        if w.startswith('emu:'):           # emu:<tag>:<fp16|bf16>
             parts = w.split(':')
-            gen_conditioning(parts[1], parts[2] if len(parts) > 2 else None)
+            gen_emulated16(parts[1], parts[2])
+        if w.startswith('cond:'):          # cond:<tag>[:<log2 of the nudge, default -24>]
+            parts = w.split(':')
+            gen_conditioning(parts[1], perturb=2.0 ** float(parts[2]) if len(parts) > 2 else 2.0 ** -24)
     if 'aug' in which:
         gen_augment()
     if 'ops' not in which:

@@ -22,7 +22,9 @@ def _nhwc(t, dtype):
 
 
 def _check(fn, tol):
-    """fn() -> list of tensors.  Deterministic twice: bitwise equal; vs the atomic path: within tol."""
+    """fn() -> list of tensors.  Deterministic twice: bitwise equal; vs the atomic path: within tol (f32
+    outputs), or within 1e-3 for 16-bit outputs: a sum that lands next to a rounding boundary of the 16-bit
+    result rounds to the neighbouring value (one ulp, 2^-11 / 2^-8 relative) when its order changes."""
     with sg2hip.deterministic():
         a = [t.detach().clone() for t in fn()]
         b = [t.detach().clone() for t in fn()]
@@ -30,7 +32,9 @@ def _check(fn, tol):
     torch.cuda.synchronize()
     for i, (x, y, r) in enumerate(zip(a, b, ref)):
         assert torch.equal(x, y), f'output {i}: deterministic runs differ (max {float((x.float() - y.float()).abs().max()):.3g})'
-        assert rel_err(x.float(), r.double().cpu()) < tol, f'output {i}: deterministic vs atomic path {rel_err(x.float(), r.double().cpu()):.3g}'
+        t = tol if x.dtype == torch.float32 else max(tol, 1e-3)
+        e = rel_err(x.float(), r.double().cpu())
+        assert e < t, f'output {i}: deterministic vs atomic path {e:.3g} (tol {t:g})'
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])

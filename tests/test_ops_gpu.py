@@ -1421,3 +1421,52 @@ def test_layer_vjp_matches_composed(up, cin, cout, res, n, dtype, monkeypatch):
             assert a_ is None or float(a_.abs().max()) == 0, name
             continue
         assert rel_err(a_, b_) < tol, (name, rel_err(a_, b_))
+
+
+@pytest.mark.parametrize('geom', [(3, 1, 1, False, 2, 512, 8, 8, 512), (3, 1, 1, False, 4, 512, 4, 4, 512),
+                                  (3, 1, 1, False, 4, 256, 16, 16, 128), (3, 2, 0, True, 2, 128, 9, 9, 64),
+                                  (3, 2, 0, False, 3, 64, 17, 17, 48), (1, 1, 0, False, 2, 64, 16, 16, 40)])
+def test_presplit_f32_accuracy(geom, monkeypatch):
+    """f32 convolutions on pre-split operands (sg2_split3 + SG2_F32S3) keep f32 accuracy: forward with modulation,
+    epilogue and dot (plain, split-K, strided, transposed) and the weight gradient with both scales, each within
+    2e-6 of float64 and no worse than 1.5x the in-loop split's error (the two forms tile and order their sums
+    differently, so they are not bitwise equal)."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    k, stride, pad, transpose, N, Cin, H, W, Cout = geom
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, Cin, H, W, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    if transpose:
+        w = (torch.randn(Cin, Cout, k, k, generator=g) / (Cin * k * k) ** 0.5).to(DEV)
+        oh, ow = (H - 1) * stride - 2 * pad + k, (W - 1) * stride - 2 * pad + k
+        wp = cg._pack_convT(w)
+    else:
+        w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).to(DEV)
+        oh, ow = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+        wp = cg._pack_conv(w)
+    s_in = (torch.rand(N, Cin, generator=g) + 0.5).to(DEV)
+    s_out = (torch.rand(N, Cout, generator=g) + 0.5).to(DEV)
+    src = torch.randn(N, Cout, oh, ow, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    gr = torch.randn(N, Cout, oh, ow, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    gs = (torch.rand(N, Cout, generator=g) + 0.5).to(DEV)
+    bias = torch.randn(Cout, generator=g).to(DEV)
+    out = []
+    for p3 in (True, False):
+        monkeypatch.setattr(cg, 'presplit', p3)
+        monkeypatch.setattr(cg, 'presplit_fwd', p3)
+        y, _, dot = cg.conv_fused(x, wp, Cout, oh, ow, k, k, stride, (pad, pad), transpose=transpose, in_scale=s_in,
+                                  out_scale=s_out, bias=bias, act=1, gain=1.4, dot_src=src)
+        res = [y, dot, cg._conv_raw(x, wp, Cout, oh, ow, k, k, stride, (pad, pad), transpose)]
+        if not transpose:
+            res.append(cg._wgrad_raw(gr, x, k, k, stride, (pad, pad), x_scale=s_in, g_scale=gs, alpha=0.7))
+        out.append(res)
+    ref = _ref_conv(x * s_in[:, :, None, None], w, stride, pad, transpose, (oh, ow))
+    v = ref * s_out.double().cpu()[:, :, None, None] + bias.double().cpu()[None, :, None, None]
+    refs = [torch.where(v > 0, v, 0.2 * v) * 1.4, (ref * src.double().cpu()).sum([2, 3]),
+            _ref_conv(x, w, stride, pad, transpose, (oh, ow))]
+    if not transpose:
+        refs.append(torch.nn.grad.conv2d_weight((x * s_in[:, :, None, None]).double().cpu(), (Cout, Cin, k, k),
+                                                (gr * gs[:, :, None, None]).double().cpu(), stride=stride,
+                                                padding=pad) * 0.7)
+    for i, r in enumerate(refs):
+        e3, e = rel_err(out[0][i], r), rel_err(out[1][i], r)
+        assert e3 < 2e-6 and e3 <= 1.5 * e + 1e-7, f'output {i}: pre-split err {e3:.3g}, in-loop split err {e:.3g}'
