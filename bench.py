@@ -59,10 +59,45 @@ def parse():
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--phase-timing', action='store_true')
     ap.add_argument('--graphs', default='auto', choices=['auto', 'on', 'off'],
-                    help='HIP-graph replay of each phase (auto: on for one GPU; with several GPUs the eager path, '
-                         'whose bucketed all_reduces overlap the backward from post-accumulate hooks)')
+                    help='HIP-graph replay of each phase, the bucket all_reduces captured into the phase graphs with '
+                         'several GPUs (auto: on, after a capture probe of an RCCL all_reduce agrees on every rank; '
+                         'otherwise the eager path, whose bucketed all_reduces overlap the backward from hooks)')
     ap.add_argument('--no-graphs', action='store_true', help='same as --graphs off')
     return ap.parse_args()
+
+
+def rccl_graph_ok(device, world):
+    """Can this stack capture the trainer's exchange pattern (an async RCCL all_reduce joined with wait())
+    into a HIP graph and replay it correctly?  Every rank captures; the replay runs only if all ranks captured
+    (an eager MIN over the ranks' flags, so no rank replays a collective the others will not join); the
+    replayed value is checked and agreed on the same way.  False -> the bench stays on the eager path."""
+    dist = torch.distributed
+
+    def agree(flag):
+        t = torch.tensor([1.0 if flag else 0.0], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return float(t) == 1.0
+
+    src = torch.ones(4096, device=device)
+    dist.all_reduce(src.clone())                      # communicator warm-up, eager
+    torch.cuda.synchronize(device)
+    g, ok = torch.cuda.CUDAGraph(), True
+    try:
+        with torch.cuda.graph(g):
+            y = src * 2
+            work = dist.all_reduce(y, async_op=True)
+            work.wait()
+            z = y + 1
+    except Exception as e:                            # noqa: BLE001 (any capture failure -> eager path)
+        print(f'[bench] RCCL graph capture failed: {e!r}', flush=True)
+        ok = False
+    if not agree(ok):
+        return False
+    src.fill_(3.0)
+    g.replay()
+    torch.cuda.synchronize(device)
+    ok = bool((z == 6.0 * world + 1).all())
+    return agree(ok)
 
 
 def build(args, device, rank, num_gpus):
@@ -273,7 +308,12 @@ def main():
     real, real_c = make_inputs(args, device, rank)
     for _ in range(args.warmup):
         one_step(tr, args, device, real, real_c)
-    graphs = (args.graphs == 'on' or (args.graphs == 'auto' and num_gpus == 1)) and not args.no_graphs
+    graphs = args.graphs != 'off' and not args.no_graphs
+    if graphs and args.graphs == 'auto' and num_gpus > 1:
+        graphs = backend == 'nccl' and rccl_graph_ok(device, world)   # gloo cannot be captured
+        if rank == 0:
+            print(f'[bench] phase graphs at {world} ranks: {"on (RCCL capture probe passed)" if graphs else "off"}',
+                  file=sys.stderr, flush=True)
     if graphs:
         # capture: one untimed step at batch_idx 0 runs (and captures) all four phases; afterwards every
         # phase is a single HIP-graph replay (trainer.py Trainer.graphs; with several GPUs the bucket

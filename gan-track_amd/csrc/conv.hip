@@ -170,13 +170,11 @@ __device__ __forceinline__ f32x4 mfma_s3(const bf16x8* a, const bf16x8* b, f32x4
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
 }
 
-// f32 exact mode (SG2_F32_EXACT=1): the f32-input MFMA kernels instead of the bf16 split
+// f32 exact mode (SG2_F32_EXACT=1): the f32-input MFMA kernels instead of the bf16 split.  Read per launch
+// (an A/B switch that diagnostics flip between calls; one getenv beside a kernel launch)
 inline bool f32_exact() {
-    static const bool v = [] {
-        const char* e = getenv("SG2_F32_EXACT");
-        return e != nullptr && e[0] == '1';
-    }();
-    return v;
+    const char* e = getenv("SG2_F32_EXACT");
+    return e != nullptr && e[0] == '1';
 }
 template <> struct Traits<f16_t> {
     static constexpr int BK = 32, V = 8;

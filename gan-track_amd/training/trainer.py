@@ -265,18 +265,19 @@ class Trainer:
                 if phase.opt.exp_avg is None:
                     phase.opt.exp_avg = torch.zeros_like(flat)
                     phase.opt.exp_avg_sq = torch.zeros_like(flat)
-            torch.cuda.synchronize(self.device)
-            st.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(st.graph):
+            want_opt = st.opt_in_graph
+
+            def body():
                 phase.module.requires_grad_(True)
                 self._accumulate(phase, *st.inputs)
                 st.part = [i for i, p in enumerate(ex.params) if p.grad is not None]
                 st.overlapped = ex.close_capture()
                 phase.module.requires_grad_(False)
-                st.opt_in_graph = st.opt_in_graph and st.part == part0
+                st.opt_in_graph = want_opt and st.part == part0
                 if st.opt_in_graph:
                     phase.opt.launch(flat, st.part, grad_scale=1.0 / self.num_gpus,
                                      write_grad=self.on_grads is not None, tag=phase.name)
+            st.graph = self._capture(body, phase)
             self._graphs[phase.name] = st
             training_stats.mark_captured()
             st.views = False
@@ -293,6 +294,20 @@ class Trainer:
             ex.finish(phase.name, st.part)
             st.views = True
         return st.part, st.opt_in_graph
+
+    graph_impl = None    # tests: a host stand-in for the capture, graph_impl(body, phase) -> object with replay()
+
+    def _capture(self, body, phase):
+        """Capture body() -- the phase's forward / backward, bucket fills, all_reduces (several ranks) and
+        optimiser launch -- into a HIP graph and return it.  `graph_impl` replaces the capture on hosts without
+        a GPU (tests/test_dist_gloo.py drives the phase-graph bookkeeping at world size 2 with it)."""
+        if self.graph_impl is not None:
+            return self.graph_impl(body, phase)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            body()
+        return g
 
     def _stage(self, st, phase, real, gen):
         """Copy a phase's inputs into its graph's static buffers (the shared real batch only once a step)."""

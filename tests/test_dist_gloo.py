@@ -110,3 +110,106 @@ def test_dp_gradient_exchange_gloo():
         assert n > 20
         assert nb > 3, 'test should exercise several buckets'
         assert worst < 1e-6, (rank, worst)
+
+
+class _HostGraph:
+    """CPU stand-in for a captured phase graph (Trainer.graph_impl).  A capture records without executing: the
+    stand-in runs the phase body once with the random state forked (a capture consumes no draws of the step), then
+    restores the state the body updates in place (the path-length mean) and drops the gradients it made.  A replay clears the module's gradients -- a real replay rewrites the gradient
+    buffers its capture allocated, instead of accumulating into the flat views finish() installed -- and runs
+    the body again, with its bucket fills and gloo all_reduces, as the replayed graph re-issues the captured
+    fills and collectives."""
+    captures = 0
+    replays = 0
+
+    def __init__(self, body, phase, loss):
+        self.body, self.phase = body, phase
+        _HostGraph.captures += 1
+        pl_mean = loss.pl_mean.clone()
+        with torch.random.fork_rng(devices=[]):
+            body()
+        loss.pl_mean.copy_(pl_mean)
+        phase.opt.zero_grad(set_to_none=True)
+
+    def replay(self):
+        _HostGraph.replays += 1
+        self.phase.opt.zero_grad(set_to_none=True)
+        self.body()
+
+
+def _graph_worker(rank, world, port, paths, result_q):
+    """Eager steps vs the phase-graph path (Trainer._graph_phase: static input staging, participation sets,
+    capture-time exchange close, per-replay .grad views, /N) at world size 2: same parameters after every step."""
+    import sys
+    sys.path[:0] = paths
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    try:
+        from oracle import sg2_oracle as O
+        from training.trainer import Trainer
+        from torch_utils import misc
+        torch.manual_seed(0)
+        G = O.Generator(z_dim=16, c_dim=0, w_dim=16, img_resolution=16, img_channels=1, channel_base=64,
+                        channel_max=8, mapping_kwargs=dict(num_layers=2),
+                        fused_modconv_default='inference_only').train().requires_grad_(False)
+        D = O.Discriminator(c_dim=0, img_resolution=16, img_channels=1, channel_base=64, channel_max=8,
+                            epilogue_kwargs=dict(mbstd_group_size=2)).train().requires_grad_(False)
+        init = (copy.deepcopy(G.state_dict()), copy.deepcopy(D.state_dict()))
+        opt = dict(class_name='torch.optim.Adam', lr=0.0025, betas=[0, 0.99], eps=1e-8)
+        B, steps = 4, 5
+        g = torch.Generator().manual_seed(20 + rank)
+        reals = torch.rand([steps, B, 1, 16, 16], generator=g) * 2 - 1
+        zs = torch.randn([steps, 4, B, 16], generator=g)
+        c = torch.zeros([4, B, 0])
+        chunks = lambda t: list(t.split(B // 2))  # noqa: E731
+
+        def run(graphs):
+            G.load_state_dict(init[0])
+            D.load_state_dict(init[1])
+            G_ema = copy.deepcopy(G).eval()
+            loss = O.StyleGAN2Loss(None, G, D, r1_gamma=0.5, style_mixing_prob=0.5, pl_weight=2)
+            tr = Trainer(G, D, G_ema, loss, opt, dict(opt), G_reg_interval=2, D_reg_interval=2, batch_size=B * world,
+                         batch_gpu=B // 2, num_gpus=world, rank=rank, device=torch.device('cpu'), bucket_mb=0.0005)
+            tr.graph_impl = lambda body, phase: _HostGraph(body, phase, loss)
+            snaps = []
+            for s in range(steps):
+                tr.graphs = graphs and s >= 1    # one eager step first, as bench.py warms up
+                torch.manual_seed(777 + 13 * s + rank)
+                tr.step(chunks(reals[s]), chunks(torch.zeros([B, 0])), [chunks(zs[s, i]) for i in range(4)],
+                        [chunks(c[i]) for i in range(4)])
+                snaps.append([p.detach().clone() for m in (G, D, G_ema) for p in m.parameters()])
+            return snaps, tr
+
+        eager, _ = run(False)
+        graph, tr = run(True)
+        worst = 0.0
+        for a, b in zip(eager, graph):
+            for x, y in zip(a, b):
+                worst = max(worst, float((x - y).abs().max() / (x.abs().max() + 1e-12)))
+        misc.check_ddp_consistency(G, ignore_regex=r'.*\.[^.]+_(avg|ema)')
+        misc.check_ddp_consistency(D)
+        result_q.put((rank, worst, sorted(tr._graphs), _HostGraph.captures, _HostGraph.replays))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_graph_phase_exchange_gloo():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = [os.path.join(root, 'gan-track_amd'), root]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_graph_worker, args=(r, 2, port, paths, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    for rank, worst, captured, ncap, nrep in res:
+        assert captured == ['Dmain', 'Dreg', 'Gmain', 'Greg'], captured
+        assert ncap == 4 and nrep >= 8, (ncap, nrep)
+        assert worst == 0.0, (rank, worst)

@@ -71,8 +71,14 @@ def cmp(a, b):
     for k in sorted(A):
         if A[k] is None or k not in B or B[k] is None:
             continue
-        d = (A[k].double() - B[k].double()).norm() / max(B[k].double().norm(), 1e-300)
-        print(f'{k:12s} {tuple(A[k].shape)} rel diff {float(d):.3g}  max abs {float((A[k] - B[k]).abs().max()):.3g}')
+        diff = A[k].double() - B[k].double()
+        d = diff.norm() / max(B[k].double().norm(), 1e-300)
+        # where the difference lives: share of its energy in the 16 / 256 largest pixels (summed over channels)
+        e = (diff ** 2).sum(1).flatten() if diff.ndim == 4 else (diff ** 2).flatten()
+        top = torch.sort(e, descending=True).values
+        tot = max(float(e.sum()), 1e-300)
+        print(f'{k:12s} {tuple(A[k].shape)} rel diff {float(d):.3g}  max abs {float(diff.abs().max()):.3g}  '
+              f'energy in top 16 px {float(top[:16].sum()) / tot:.2f}, top 256 {float(top[:256].sum()) / tot:.2f}')
 
 
 if __name__ == '__main__':
