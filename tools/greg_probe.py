@@ -79,6 +79,16 @@ def cmp(a, b):
         tot = max(float(e.sum()), 1e-300)
         print(f'{k:12s} {tuple(A[k].shape)} rel diff {float(d):.3g}  max abs {float(diff.abs().max()):.3g}  '
               f'energy in top 16 px {float(top[:16].sum()) / tot:.2f}, top 256 {float(top[:256].sum()) / tot:.2f}')
+        if diff.ndim == 4 and k.endswith('_dy') and float(d) > 1e-5:
+            yk = k[:-3] + '_y'
+            for flat in torch.argsort(e, descending=True)[:3].tolist():
+                n_, rem = divmod(flat, diff.shape[2] * diff.shape[3])
+                yy, xx = divmod(rem, diff.shape[3])
+                ya, yb = A[yk][n_, :, yy, xx].double(), B[yk][n_, :, yy, xx].double()
+                c = int(torch.argmax(diff[n_, :, yy, xx].abs()))
+                print(f'    px (n{n_}, {yy}, {xx}) ch {c}: dy {float(A[k][n_, c, yy, xx]):.4g} / {float(B[k][n_, c, yy, xx]):.4g}'
+                      f'  y {float(ya[c]):.4g} / {float(yb[c]):.4g}; min |y| over ch {float(ya.abs().min()):.3g} / '
+                      f'{float(yb.abs().min()):.3g}; sign flips {int(((ya > 0) != (yb > 0)).sum())}')
 
 
 if __name__ == '__main__':
