@@ -27,6 +27,15 @@ class Epilogue(ctypes.Structure):
                 ('act', ctypes.c_int), ('aux_mode', ctypes.c_int), ('dot_src', ctypes.c_void_p),
                 ('dot_out', ctypes.c_void_p)]
 
+class AugGeomArgs(ctypes.Structure):
+    """sg2_aug_geom_args (include/sg2hip.h)."""
+    _fields_ = [('draw', ctypes.c_void_p * 16), ('p', ctypes.c_void_p)] + \
+        [(k, ctypes.c_float) for k in ('xflip', 'rotate90', 'xint', 'xint_max', 'scale', 'rotate', 'aniso', 'xfrac',
+                                       'scale_std', 'rotate_max', 'aniso_std', 'xfrac_std', 'pad_x', 'pad_y',
+                                       'inv_sx', 'inv_sy')] + \
+        [(k, ctypes.c_int) for k in ('n', 'h', 'w')]
+
+
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _i64 = ctypes.c_int64
@@ -63,6 +72,7 @@ SIGNATURES = {
     'sg2_affine_grid_sample_fwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
     'sg2_affine_grid_sample_bwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
     'sg2_reflect_pad_dyn': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp],
+    'sg2_aug_geom': [_vp, _vp, _vp, _vp, ctypes.POINTER(AugGeomArgs), _vp],
     'sg2_demod_fwd': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp],
     'sg2_demod_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
     'sg2_adam_multi': [_vp, _vp, _vp, _i, _vp, _vp, _vp, _f, _f, _f, _f, _i, _vp],
@@ -71,7 +81,7 @@ SIGNATURES = {
     'sg2_infnorm_bwd': [_vp, _vp, _vp, _vp, _i, _i, _f, _i, _vp],
     'sg2_pack_weight': [_vp, _i, _vp, _i, _i, _i, _i, _i64, _i64, _i64, _i, _f, _vp],
 }
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lib = None
 

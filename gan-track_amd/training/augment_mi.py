@@ -10,15 +10,22 @@ reference's order (so an RNG tape reproduces the reference exactly).
 
 Deviation: `allow_aug_debug_print` (matplotlib PNG dump, :449-491) is accepted and ignored.
 """
+import ctypes
+
 import numpy as np
 import torch
 
+import sg2hip as _hip
 from torch_utils import misc
 from torch_utils import persistence
 from torch_utils.ops import conv2d_gradfix
 from torch_utils.ops import grid_sample_gradfix
 from torch_utils.ops import reflect_pad
 from torch_utils.ops import upfirdn2d
+
+# the transform algebra of the geometric stage in one launch (sg2_aug_geom); False: the per-op torch algebra
+# (debug-percentile mode always takes it)
+fused_geometric = True
 
 wavelets = {
     'haar': [0.7071067811865476, 0.7071067811865476],
@@ -125,9 +132,62 @@ class AugmentPipe(torch.nn.Module):
         self.register_buffer('Hz_fbank', torch.as_tensor(_filter_bank(), dtype=torch.float32))
 
     # ------------------------------------------------------------------ geometric
+    def _geometric_enabled(self):
+        return any(v > 0 for v in (self.xflip, self.rotate90, self.xint, self.scale, self.rotate, self.aniso,
+                                   self.xfrac))
+
+    def _geometric_fused(self, images):
+        """The geometric stage with the transform algebra in one launch (sg2_aug_geom): the same draws, in the
+        same order, as _geometric below; the kernel composes each sample's matrix, the batch margins and the
+        pad / up-sampling conjugations (reference :214-318) that _geometric builds with ~100 small torch ops."""
+        n, c, h, w = images.shape
+        dev = images.device
+        rand = lambda *s: torch.rand(list(s), device=dev)    # noqa: E731
+        randn = lambda *s: torch.randn(list(s), device=dev)  # noqa: E731
+        draws = [None] * 16
+        if self.xflip > 0:
+            draws[0], draws[1] = rand(n), rand(n)
+        if self.rotate90 > 0:
+            draws[2], draws[3] = rand(n), rand(n)
+        if self.xint > 0:
+            draws[4], draws[5] = rand(n, 2), rand(n, 1)
+        if self.scale > 0:
+            draws[6], draws[7] = randn(n), rand(n)
+        if self.rotate > 0:
+            draws[8], draws[9] = rand(n), rand(n)
+        if self.aniso > 0:
+            draws[10], draws[11] = randn(n), rand(n)
+        if self.rotate > 0:
+            draws[12], draws[13] = rand(n), rand(n)
+        if self.xfrac > 0:
+            draws[14], draws[15] = randn(n, 2), rand(n, 1)
+        hz_pad = self.Hz_geom.shape[0] // 4
+        hup, wup = (h + hz_pad * 2) * 2, (w + hz_pad * 2) * 2
+        theta = torch.empty([n, 2, 3], dtype=torch.float32, device=dev)
+        ints = torch.empty([14], dtype=torch.int32, device=dev)          # margins [4], lims [8], dyn_hw [2]
+        mi, lims, dyn_hw = ints[:4], ints[4:12], ints[12:]
+        a = _hip.AugGeomArgs()
+        for k, t in enumerate(draws):
+            a.draw[k] = _hip.ptr(t)
+        a.p = _hip.ptr(self.p)
+        for k in ('xflip', 'rotate90', 'xint', 'xint_max', 'scale', 'rotate', 'aniso', 'xfrac', 'scale_std',
+                  'rotate_max', 'aniso_std', 'xfrac_std'):
+            setattr(a, k, getattr(self, k))
+        a.pad_x, a.pad_y = hz_pad * 2 - (w - 1) / 2, hz_pad * 2 - (h - 1) / 2
+        a.inv_sx, a.inv_sy = 1 / (2 / wup), 1 / (2 / hup)
+        a.n, a.h, a.w = n, h, w
+        _hip.check(_hip.lib().sg2_aug_geom(_hip.ptr(theta), _hip.ptr(mi), _hip.ptr(lims), _hip.ptr(dyn_hw),
+                                           ctypes.byref(a), _hip.stream_ptr(dev)), 'sg2_aug_geom')
+        images = reflect_pad.reflect_pad_dyn(images, mi)
+        images = upfirdn2d.upsample2d_limited(images, self.Hz_geom, lims.view(4, 2).unbind(0), up=2)
+        images = grid_sample_gradfix.affine_grid_sample(images, theta, [n, c, hup, wup], dyn_hw=dyn_hw)
+        return upfirdn2d.downsample2d(x=images, f=self.Hz_geom, down=2, padding=-hz_pad * 2, flip_filter=True)
+
     def _geometric(self, images, dp):
         n, c, h, w = images.shape
         dev = images.device
+        if dp is None and images.is_cuda and fused_geometric and self._geometric_enabled():
+            return self._geometric_fused(images)
         I_3 = torch.eye(3, device=dev)
         G = I_3
 

@@ -236,6 +236,61 @@ class FullyConnectedLayer(torch.nn.Module):
         return f'in_features={self.in_features:d}, out_features={self.out_features:d}, activation={self.activation:s}'
 
 
+# The synthesis network's affine layers (one FullyConnectedLayer per conv / toRGB layer, 20 at 256^2) as ONE
+# GEMM: every layer's weight rows side by side, every w row against all of them (S = ws @ W_cat^T, N * num_ws x
+# sum C -- the off-diagonal blocks are wasted but cost microseconds), then one gather picks each layer's block
+# (its w row, its columns) into a layer-major buffer whose per-layer slices are contiguous [N, C], with the
+# layer's weight / bias gains.  The bias rows enter through a rank-1 GEMM (ones[N] x b * gain) gathered with
+# unique indices, so the backward has no duplicate-index scatter (whose atomics would make the bias gradients
+# run-to-run different; sg2hip.deterministic).  Autograd of these few torch ops (mm, take, addcmul, cat) replaces ~3 launches per
+# layer forward and ~4 backward (GEMMs, GEMVs, the ws unbind / narrow adds), and is differentiable twice (the
+# path-length pass).  Reference per layer: networks_stylegan2.py:111-125 (styles = affine(w)), :352 (toRGB's
+# styles * weight_gain).
+grouped_affine = True
+_PLAN_CACHE = {}
+
+
+def _style_plan(layers, n, num_ws, device):
+    """Index / gain tensors of grouped_styles for one batch size: (elem index into S, elem index into the
+    [N, sum C] bias matrix, elem alpha, column beta, ones [N, 1], per-layer (offset, C))."""
+    key = (tuple((id(a), k, float(g)) for a, k, g in layers), n, num_ws, device)
+    plan = _PLAN_CACHE.get(key)
+    if plan is not None:
+        return plan
+    tot = sum(a.out_features for a, _, _ in layers)
+    idx, bidx, alpha, beta, spans = [], [], [], [], []
+    col, off = 0, 0
+    for a, k, g in layers:
+        c = a.out_features
+        rows = np.arange(n)[:, None] * num_ws + k                      # [N, 1]
+        cols = col + np.arange(c)[None, :]                             # [1, C]
+        idx.append((rows * tot + cols).reshape(-1))
+        bidx.append((np.arange(n)[:, None] * tot + cols).reshape(-1))
+        alpha.append(np.full(n * c, np.float32(a.weight_gain * g), np.float32))
+        beta.append(np.full(c, np.float32(a.bias_gain * g), np.float32))
+        spans.append((off, c))
+        col += c
+        off += n * c
+    T = lambda v, dt: torch.as_tensor(np.concatenate(v), dtype=dt, device=device)  # noqa: E731
+    plan = (T(idx, torch.int64), T(bidx, torch.int64), T(alpha, torch.float32), T(beta, torch.float32),
+            torch.ones([n, 1], dtype=torch.float32, device=device), spans)
+    _PLAN_CACHE[key] = plan
+    return plan
+
+
+def grouped_styles(ws, layers):
+    """ws [N, num_ws, w_dim] f32; layers: [(FullyConnectedLayer (linear, with bias), w index, out gain)] ->
+    per-layer styles [N, C] (contiguous) = ws[:, k] @ (W * weight_gain)^T * g + b * bias_gain * g."""
+    n, num_ws, d = ws.shape
+    W = torch.cat([a.weight for a, _, _ in layers])
+    b = torch.cat([a.bias for a, _, _ in layers])
+    S = torch.mm(ws.reshape(n * num_ws, d), W.t())
+    idx, bidx, alpha, beta, ones, spans = _style_plan(layers, n, num_ws, ws.device)
+    B = torch.mm(ones, (b * beta).view(1, -1))                         # [N, sum C]: row n = b * gain
+    out = torch.addcmul(B.take(bidx), S.take(idx), alpha)
+    return [out.narrow(0, o, n * c).view(n, c) for o, c in spans]
+
+
 @persistence.persistent_class
 class Conv2dLayer(torch.nn.Module):
     """:133-181"""
@@ -369,10 +424,12 @@ class SynthesisLayer(torch.nn.Module):
             self.noise_strength = torch.nn.Parameter(torch.zeros([]))
         self.bias = torch.nn.Parameter(torch.zeros([out_channels]))
 
-    def forward(self, x, w, noise_mode='random', fused_modconv=True, gain=1):
+    def forward(self, x, w, noise_mode='random', fused_modconv=True, gain=1, styles=None):
+        """styles: this layer's affine(w), when the network computed it (grouped_styles)."""
         assert noise_mode in ['random', 'const', 'none']
         misc.assert_shape(x, [None, self.in_channels, self.resolution // self.up, self.resolution // self.up])
-        styles = self.affine(w)
+        if styles is None:
+            styles = self.affine(w)
         noise = None
         if self.use_noise and noise_mode == 'random':
             noise = torch.randn([x.shape[0], 1, self.resolution, self.resolution], device=x.device) * self.noise_strength
@@ -419,8 +476,9 @@ class ToRGBLayer(torch.nn.Module):
         self.bias = torch.nn.Parameter(torch.zeros([out_channels]))
         self.weight_gain = 1 / np.sqrt(in_channels * (kernel_size ** 2))
 
-    def forward(self, x, w, fused_modconv=True):
-        styles = self.affine(w, out_gain=self.weight_gain)
+    def forward(self, x, w, fused_modconv=True, styles=None):
+        if styles is None:
+            styles = self.affine(w, out_gain=self.weight_gain)
         if modconv.supported_generic(x, self.weight):
             # modulation folded into the conv's operand staging, bias + clamp into its epilogue
             return modconv.fused_conv(x, self.weight, styles=styles, bias=self.bias,
@@ -465,9 +523,28 @@ class SynthesisBlock(torch.nn.Module):
             self.skip = Conv2dLayer(in_channels, out_channels, kernel_size=1, bias=False, up=2,
                                     resample_filter=resample_filter)
 
-    def forward(self, x, img, ws, force_fp32=False, fused_modconv=None, update_emas=False, **layer_kwargs):
+    def style_layers(self):
+        """(affine, w index within the block's ws, out gain) of the block's layers in w order."""
+        out, k = [], 0
+        if self.in_channels != 0:
+            out.append((self.conv0.affine, k, 1.0))
+            k += 1
+        out.append((self.conv1.affine, k, 1.0))
+        k += 1
+        if self.is_last or self.architecture == 'skip':
+            out.append((self.torgb.affine, k, float(self.torgb.weight_gain)))
+        return out
+
+    def forward(self, x, img, ws, force_fp32=False, fused_modconv=None, update_emas=False, styles=None,
+                **layer_kwargs):
+        """styles: the layers' styles in w order (SynthesisNetwork's grouped_styles), or None (per-layer affine)."""
         misc.assert_shape(ws, [None, self.num_conv + self.num_torgb, self.w_dim])
-        w_iter = iter(ws.unbind(dim=1))
+        if styles is not None:
+            s_iter = iter(styles)
+            w_iter = iter([None] * len(styles))
+        else:
+            s_iter = iter([None] * (self.num_conv + self.num_torgb))
+            w_iter = iter(ws.unbind(dim=1))
         dtype = self.fp16_dtype if self.use_fp16 and not force_fp32 else torch.float32
         if fused_modconv is None:
             fused_modconv = self.fused_modconv_default
@@ -480,20 +557,21 @@ class SynthesisBlock(torch.nn.Module):
             misc.assert_shape(x, [None, self.in_channels, self.resolution // 2, self.resolution // 2])
             x = x.to(dtype=dtype, memory_format=_CL)
         if self.in_channels == 0:
-            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, **layer_kwargs)
+            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, styles=next(s_iter), **layer_kwargs)
         elif self.architecture == 'resnet':
             y = self.skip(x, gain=np.sqrt(0.5))
-            x = self.conv0(x, next(w_iter), fused_modconv=fused_modconv, **layer_kwargs)
-            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, gain=np.sqrt(0.5), **layer_kwargs)
+            x = self.conv0(x, next(w_iter), fused_modconv=fused_modconv, styles=next(s_iter), **layer_kwargs)
+            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, gain=np.sqrt(0.5), styles=next(s_iter),
+                           **layer_kwargs)
             x = y.add_(x)
         else:
-            x = self.conv0(x, next(w_iter), fused_modconv=fused_modconv, **layer_kwargs)
-            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, **layer_kwargs)
+            x = self.conv0(x, next(w_iter), fused_modconv=fused_modconv, styles=next(s_iter), **layer_kwargs)
+            x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, styles=next(s_iter), **layer_kwargs)
         if img is not None:
             misc.assert_shape(img, [None, self.img_channels, self.resolution // 2, self.resolution // 2])
             img = upfirdn2d.upsample2d(img, self.resample_filter)
         if self.is_last or self.architecture == 'skip':
-            y = self.torgb(x, next(w_iter), fused_modconv=fused_modconv)
+            y = self.torgb(x, next(w_iter), fused_modconv=fused_modconv, styles=next(s_iter))
             y = y.to(dtype=torch.float32, memory_format=torch.contiguous_format)
             img = img.add_(y) if img is not None else y
         assert x.dtype == dtype
@@ -532,12 +610,21 @@ class SynthesisNetwork(torch.nn.Module):
         misc.assert_shape(ws, [None, self.num_ws, self.w_dim])
         ws = ws.to(torch.float32)
         x = img = None
+        styles = None
+        if grouped_affine and ws.is_cuda:
+            plan, w_idx = [], 0
+            for r in self.block_resolutions:
+                block = getattr(self, f'b{r}')
+                plan += [(a, w_idx + k, g) for a, k, g in block.style_layers()]
+                w_idx += block.num_conv
+            styles = iter(grouped_styles(ws, plan))
         w_idx = 0
         for r in self.block_resolutions:
             block = getattr(self, f'b{r}')
             cur = ws.narrow(1, w_idx, block.num_conv + block.num_torgb)
             w_idx += block.num_conv
-            x, img = block(x, img, cur, **block_kwargs)
+            bs = [next(styles) for _ in block.style_layers()] if styles is not None else None
+            x, img = block(x, img, cur, styles=bs, **block_kwargs)
         return img
 
     def extra_repr(self):

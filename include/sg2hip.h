@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define SG2_ABI_VERSION 5
+#define SG2_ABI_VERSION 6
 
 enum sg2_dtype { SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2, SG2_F32S3 = 3 };
 
@@ -269,6 +269,26 @@ int sg2_affine_grid_sample_bwd(float* gin, const void* gout, const float* theta,
  * (gather of the reflected positions) of x [N,C,Hs,Ws]. */
 int sg2_reflect_pad_dyn(float* y, const float* x, const int* margins, int N, int C, int H, int W, int Hs, int Ws,
                         int adjoint, void* stream);
+
+/* ADA geometric transforms of a batch in one launch (ABI 6; replaces the per-op matrix algebra of
+ * SG3/training/augment_mi.py:214-318 -- stack / sin / cos / where / matmul per enabled op, the corner margins
+ * and the pad / up-sampling conjugations).  draw[2k], draw[2k+1]: the value draw and the choice draw of op k
+ * in the reference's order -- 0 xflip (rand[N], rand[N]), 1 rotate90 (rand[N], rand[N]), 2 xint (rand[N,2],
+ * rand[N,1]), 3 scale (randn[N], rand[N]), 4 rotate (rand[N], rand[N]), 5 aniso (randn[N], rand[N]), 6 the
+ * second rotate, 7 xfrac (randn[N,2], rand[N,1]); NULL for an op whose probability is 0.  p: device f32
+ * scalar, the augmentation probability.  pad_x / pad_y: f32(2 hz_pad - (W-1)/2) / (.. (H-1)/2); inv_sx /
+ * inv_sy: f32(1 / (2 / Wup)) / f32(1 / (2 / Hup)) of the up-sampled static buffer (the reference's Python
+ * floats).  Writes theta [N,2,3] (the grid-sample transform), margins int[4] (mx0, my0, mx1, my1: the
+ * reflect pad), lims int[8] (the up-sampling extents) and dyn_hw int[2] (the logical up-sampled size). */
+typedef struct sg2_aug_geom_args {
+    const float* draw[16];
+    const float* p;
+    float xflip, rotate90, xint, xint_max, scale, rotate, aniso, xfrac;
+    float scale_std, rotate_max, aniso_std, xfrac_std;
+    float pad_x, pad_y, inv_sx, inv_sy;
+    int n, h, w;
+} sg2_aug_geom_args;
+int sg2_aug_geom(float* theta, int* margins, int* lims, int* dyn_hw, const sg2_aug_geom_args* args, void* stream);
 
 /* Demodulation coefficients d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps), wsq[o,i] = sum_k w[o,i,k]^2
  * (SG3/training/networks_stylegan2.py:59-63, summation regrouped); s [N,I] f32, w [O,I*KK] f32.  Also

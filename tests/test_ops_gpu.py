@@ -381,6 +381,30 @@ def test_augment_golden(name):
     assert rel_err(dx, z[f'{name}_dx']) < 2e-5
 
 
+@pytest.mark.parametrize('p,n', [(0.0, 4), (0.2, 64), (1.0, 300)])
+def test_augment_geometric_fused_matches_torch_algebra(p, n, monkeypatch):
+    """sg2_aug_geom (one launch for the transform algebra) against the per-op torch algebra it replaces, on the
+    same draws: images and input gradients to 1e-5, every op of the pipe enabled (incl. rotate90), the batch
+    beyond one workgroup's 256 threads (n = 300)."""
+    from training import augment_mi
+    cfg = dict(xflip=1, rotate90=1, xint=1, scale=1, rotate=1, aniso=1, xfrac=1, xint_max=0.05, rotate_max=3 / 360,
+               xfrac_std=0.05, scale_std=0.05, aniso_std=0.05)
+    pipe = augment_mi.AugmentPipe(run_dir=None, batch_size=n, **cfg).to(DEV)
+    pipe.p.fill_(p)
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(n, 1, 32, 32, generator=g) * 2 - 1).to(DEV).requires_grad_(True)
+    dy = torch.randn(n, 1, 32, 32, generator=g).to(DEV)
+    out = []
+    for fused in (True, False):
+        monkeypatch.setattr(augment_mi, 'fused_geometric', fused)
+        torch.manual_seed(123)
+        y = pipe(x, False)
+        dx, = torch.autograd.grad((y * dy).sum(), [x])
+        out.append((y.detach(), dx))
+    assert rel_err(out[0][0], out[1][0].double().cpu()) < 1e-5
+    assert rel_err(out[0][1], out[1][1].double().cpu()) < 1e-5
+
+
 # ------------------------------------------------------------------ LDS-halo 3x3 conv with fused epilogue
 @pytest.mark.parametrize('shape', [(2, 64, 32, 32, 64), (2, 64, 20, 37, 96), (1, 512, 32, 32, 512), (2, 128, 16, 16, 128),
                                    (2, 40, 16, 24, 8),

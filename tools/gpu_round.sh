@@ -43,6 +43,22 @@ if step prof; then
     f=$(find "$O/prof" -name 'run_kernel_stats.csv' | head -1)
     python3 "$R/profiles/prof_summary.py" "$(dirname "$f")" 45 > "$O/prof_summary.txt" 2>&1
     head -50 "$O/prof_summary.txt"
+    ms=$(python3 -c "import json,sys; print(json.loads([l for l in open('$O/prof_bench.log') if l.startswith('{')][-1])['ms_per_step'])")
+    t=$(find "$O/prof" -name 'run_kernel_trace.csv' | head -1)
+    python3 "$R/profiles/step_breakdown.py" "$t" "$ms" > "$O/step_breakdown.txt" 2>&1; cat "$O/step_breakdown.txt"
+    rm -f "$t"     # (the full trace exceeds what gpurun_out carries back)
+fi
+if step c4; then
+    echo "== C4 bench (512^2 3-ch, cbase 32768, bs16, fp16)"
+    (cd "$R" && timeout -k 10 500 python -u bench.py --res 512 --batch-gpu 16 --img-channels 3 --cbase 32768 --c-dim 0 \
+        > "$O/c4_bench.log" 2>&1)
+    rc=$?; tail -1 "$O/c4_bench.log"; [ $rc -eq 0 ] || exit $rc
+fi
+if step c5; then
+    echo "== C5 bench (1024^2 3-ch, cbase 32768, bs8, bf16)"
+    (cd "$R" && timeout -k 10 500 python -u bench.py --res 1024 --batch-gpu 8 --img-channels 3 --cbase 32768 --c-dim 0 \
+        --fp16-dtype bf16 > "$O/c5_bench.log" 2>&1)
+    rc=$?; tail -1 "$O/c5_bench.log"; [ $rc -eq 0 ] || exit $rc
 fi
 if step pmc; then
     # HBM bytes of the roofline kernel: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots).
