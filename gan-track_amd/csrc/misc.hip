@@ -334,3 +334,48 @@ extern "C" int sg2_infnorm_bwd(float* dt, const float* dy, const float* t, const
     infnorm_bwd_kernel<<<rows, 256, 0, as_stream(stream)>>>(dt, dy, t, nrm, L, c, mode);
     return launch_status("sg2_infnorm_bwd");
 }
+
+// ------------------------------------------------------------------------------------ statistic moments
+// training_stats.report (SG3/torch_utils/training_stats.py:55-99: count, sum and sum of squares of a reported
+// value, added into its float64 row) in one launch instead of ~7 (flatten / square / two sums / stack / cast /
+// two adds).  One workgroup: strided double partials, then a fixed-order tree -- deterministic.  mode 1: the
+// moments of sign(v) (the ADA heuristic's Loss/signs/*, without the separate sign launch).
+namespace sg2 {
+namespace {
+__global__ __launch_bounds__(256) void moments_kernel(double* row, const float* v, int64_t n, int mode) {
+    __shared__ double s1[256], s2[256];
+    const int tid = threadIdx.x;
+    double a = 0.0, b = 0.0;
+    for (int64_t i = tid; i < n; i += 256) {
+        float x = v[i];
+        if (mode == 1) x = x > 0.f ? 1.f : (x < 0.f ? -1.f : x);   // torch.sign: 0 -> 0, NaN -> NaN
+        const double d = (double)x;
+        a += d;
+        b += d * d;
+    }
+    s1[tid] = a;
+    s2[tid] = b;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (tid < s) {
+            s1[tid] += s1[tid + s];
+            s2[tid] += s2[tid + s];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        row[0] += (double)n;
+        row[1] += s1[0];
+        row[2] += s2[0];
+    }
+}
+}  // namespace
+}  // namespace sg2
+
+extern "C" int sg2_moments(double* row, const float* v, int64_t n, int mode, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(row && v, "sg2_moments: null pointer");
+    SG2_CHECK(n > 0 && (mode == 0 || mode == 1), "sg2_moments: n > 0, mode 0 or 1");
+    moments_kernel<<<1, 256, 0, as_stream(stream)>>>(row, v, n, mode);
+    return launch_status("sg2_moments");
+}

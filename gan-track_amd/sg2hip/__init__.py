@@ -73,6 +73,7 @@ SIGNATURES = {
     'sg2_affine_grid_sample_bwd': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _vp, _vp],
     'sg2_reflect_pad_dyn': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp],
     'sg2_aug_geom': [_vp, _vp, _vp, _vp, ctypes.POINTER(AugGeomArgs), _vp],
+    'sg2_moments': [_vp, _vp, _i64, _i, _vp],
     'sg2_demod_fwd': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp],
     'sg2_demod_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
     'sg2_adam_multi': [_vp, _vp, _vp, _i, _vp, _vp, _vp, _f, _f, _f, _f, _i, _vp],

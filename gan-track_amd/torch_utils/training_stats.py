@@ -94,16 +94,43 @@ def init_multiprocessing(rank, sync_device):
 
 def report(name, value):
     """Accumulate the moments of `value` (any scalar set) under `name`; returns `value` unchanged."""
+    return _report(name, value, 0)
+
+
+def report_sign(name, value):
+    """report(name, value.sign()) -- on the device without materialising the sign.  When a caller has replaced
+    `report` (tests that record the reported stream), the sign goes through the replacement."""
+    if report is not _REPORT:
+        report(name, torch.as_tensor(value).sign())
+        return value
+    return _report(name, value, 1)
+
+
+def _report(name, value, mode):
     r = _board.row(name)
     v = torch.as_tensor(value)
     if v.numel() == 0:
         return value
+    if v.is_cuda:     # one launch (sg2_moments) instead of flatten / square / sums / stack / cast / adds
+        import sg2hip as _hip
+        vf = v.detach().reshape(-1)
+        if vf.dtype != torch.float32 or not vf.is_contiguous():
+            vf = vf.float().contiguous()
+        row = _board.table(v.device)[r]
+        _hip.check(_hip.lib().sg2_moments(_hip.ptr(row), _hip.ptr(vf), vf.numel(), mode, _hip.stream_ptr(v.device)),
+                   'sg2_moments')
+        return value
     v = v.detach().flatten().float()
+    if mode == 1:
+        v = v.sign()
     moments = torch.stack([v.sum(), v.square().sum()]).double()
     row = _board.table(v.device)[r]
     row[1:].add_(moments)
     row[:1].add_(float(v.numel()))
     return value
+
+
+_REPORT = report
 
 
 def report0(name, value):

@@ -163,7 +163,7 @@ class StyleGAN2Loss(Loss):
 
     def _report_logits(self, kind, logits):
         training_stats.report(f'Loss/scores/{kind}', logits)
-        training_stats.report(f'Loss/signs/{kind}', logits.sign())
+        training_stats.report_sign(f'Loss/signs/{kind}', logits)
 
     def _generator_term(self, z, c, gain, sigma):
         """-log sigmoid(D(G(z))) on a full batch (reference :73-82)."""

@@ -290,6 +290,11 @@ typedef struct sg2_aug_geom_args {
 } sg2_aug_geom_args;
 int sg2_aug_geom(float* theta, int* margins, int* lims, int* dyn_hw, const sg2_aug_geom_args* args, void* stream);
 
+/* training_stats.report in one launch (ABI 6; SG3/torch_utils/training_stats.py:55-99): row[0] += n,
+ * row[1] += sum v, row[2] += sum v^2 over the n f32 values v (mode 1: of sign(v)), accumulated in float64 in a
+ * fixed order.  row: device double[3], the statistic's row of the caller's moment table. */
+int sg2_moments(double* row, const float* v, int64_t n, int mode, void* stream);
+
 /* Demodulation coefficients d[n,o] = rsqrt(sum_i s[n,i]^2 * wsq[o,i] + eps), wsq[o,i] = sum_k w[o,i,k]^2
  * (SG3/training/networks_stylegan2.py:59-63, summation regrouped); s [N,I] f32, w [O,I*KK] f32.  Also
  * writes wsq [O, I] (may be NULL) for the backward. */

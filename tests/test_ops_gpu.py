@@ -1494,3 +1494,22 @@ def test_presplit_f32_accuracy(geom, monkeypatch):
     for i, r in enumerate(refs):
         e3, e = rel_err(out[0][i], r), rel_err(out[1][i], r)
         assert e3 < 2e-6 and e3 <= 1.5 * e + 1e-7, f'output {i}: pre-split err {e3:.3g}, in-loop split err {e:.3g}'
+
+
+@pytest.mark.parametrize('n', [1, 37, 5000])
+def test_training_stats_moments(n):
+    """training_stats.report / report_sign on the device (sg2_moments, one launch) against the reference's
+    moments (count, sum, sum of squares; training_stats.py:55-99) of the value and of its sign."""
+    from torch_utils import training_stats as ts
+    g = torch.Generator().manual_seed(n)
+    v = torch.randn(n, 1, generator=g)
+    v[0, 0] = 0.0
+    table = ts._board.table(DEV)
+    ra, rb = ts._board.row(f'test/moments/{n}'), ts._board.row(f'test/signs/{n}')
+    before = table[[ra, rb]].clone()
+    ts.report(f'test/moments/{n}', v.to(DEV))
+    ts.report_sign(f'test/signs/{n}', v.to(DEV))
+    got = (table[[ra, rb]] - before).cpu()
+    vd, sd = v.double().flatten(), v.sign().double().flatten()
+    want = torch.tensor([[n, vd.sum(), vd.square().sum()], [n, sd.sum(), sd.square().sum()]], dtype=torch.float64)
+    assert torch.allclose(got, want, rtol=1e-12, atol=1e-9), (got, want)
