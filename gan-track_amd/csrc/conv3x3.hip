@@ -754,7 +754,7 @@ __device__ __forceinline__ void wait_vm() {           // s_waitcnt vmcnt(N) (gfx
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <typename T, bool SI, bool EPI, bool RAW, int R_TH, int WR, bool PIPE, bool STG, bool PKE = false>
+template <typename T, bool SI, bool EPI, bool RAW, int R_TH, int WR, bool PIPE, bool STG>
 __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER_CU)) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
     typedef Ring<R_TH, WR> RG;
@@ -941,21 +941,6 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
             const int r = WR * wr + (i >> 1), px = (i & 1) * 16 + l16;
             const int pix = (n * a.H + ty + r) * a.W + tx + px;
             vec8 yv, rv;
-            if constexpr (PKE && EPI) {
-                // packed-f32 form (v_pk_add / v_pk_fma / v_pk_mul_f32 on channel pairs): the same operations and
-                // roundings as the scalar form below, 4 instead of ~5.75 VALU per element
-                typedef float f2 __attribute__((ext_vector_type(2)));
-                const f2 nz2 = f2{nz[i], nz[i]}, al2 = f2{lr_alpha, lr_alpha};
-#pragma unroll
-                for (int e = 0; e < 8; e += 2) {
-                    const f2 cv = f2{A[i][e >> 2][e & 3], A[i][e >> 2][(e & 3) + 1]};
-                    if (RAW) { rv[e] = (T)cv.x; rv[e + 1] = (T)cv.y; }
-                    f2 v = __builtin_elementwise_fma(cv, f2{dd[e], dd[e + 1]}, f2{bb[e], bb[e + 1]} + nz2);
-                    const f2 va = v * al2;
-                    yv[e] = (T)__builtin_amdgcn_fmed3f(fmaxf(v.x, va.x), -clampv, clampv);
-                    yv[e + 1] = (T)__builtin_amdgcn_fmed3f(fmaxf(v.y, va.y), -clampv, clampv);
-                }
-            } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const float cv = A[i][e >> 2][e & 3];
@@ -967,7 +952,6 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
                     v = __builtin_amdgcn_fmed3f(v, -clampv, clampv);
                 }
                 yv[e] = (T)v;
-            }
             }
             int dst = (pix * 64 + ch0) * (int)sizeof(T) | -(int)((SG2_RDIAG & 32) != 0);   // timing-only build: dropped
             if (SG2_RDIAG & 256)   // timing-only build: the same bytes as whole-line stores (8 px x 128 B an instruction)
@@ -1143,10 +1127,10 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
 }
 
-template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, bool STG, bool PKE = false>
+template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, bool STG>
 int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
     typedef Ring<TH, WR> RG;
-    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW, TH, WR, PIPE, STG, PKE>;
+    auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW, TH, WR, PIPE, STG>;
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RG::LDS);
@@ -1156,26 +1140,24 @@ int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band
     return launch_status("sg2_conv3x3 (c64 ring)");
 }
 
-template <typename T, bool SI, bool EPI, int TH, int WR, bool PIPE = false, bool STG = false, bool PKE = false>
+template <typename T, bool SI, bool EPI, int TH, int WR, bool PIPE = false, bool STG = false>
 int launch_c64r_raw(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
-    return a.y_raw ? launch_c64r<T, SI, EPI, true, TH, WR, PIPE, STG, PKE>(a, s, tiles, grid, band)
-                   : launch_c64r<T, SI, EPI, false, TH, WR, PIPE, STG, PKE>(a, s, tiles, grid, band);
+    return a.y_raw ? launch_c64r<T, SI, EPI, true, TH, WR, PIPE, STG>(a, s, tiles, grid, band)
+                   : launch_c64r<T, SI, EPI, false, TH, WR, PIPE, STG>(a, s, tiles, grid, band);
 }
 
-// form: 4 = 32 x 4 tiles, two workgroups of 4 waves per CU (45: the same with the packed-f32 epilogue);
-// 8 = 32 x 8 tiles, one workgroup of 8 waves;
+// form: 4 = 32 x 4 tiles, two workgroups of 4 waves per CU; 8 = 32 x 8 tiles, one workgroup of 8 waves;
 // 44 = form 4 with whole-line stores staged through the consumed slot; 84 = 32 x 8 tiles, one workgroup of 4
 // waves with 4 rows each (one wave per SIMD, 512 registers).  (The PIPE
 // template form -- tile k - 1's epilogue beside tile k's MFMAs -- spills at 512 registers with the weights in
 // VGPRs and is not instantiated.)
 template <typename T, bool SI, bool EPI>
 int launch_c64r_form(const Conv3Args& a, hipStream_t s, int form) {
-    const int th = (form == 4 || form == 44 || form == 45) ? 4 : 8;
+    const int th = (form == 4 || form == 44) ? 4 : 8;
     const int tiles = a.N * (a.H / th) * (a.W / R_TW);
     const int ty = a.H / th;
     const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
     if (form == 4) return launch_c64r_raw<T, SI, EPI, 4, 2>(a, s, tiles, 2 * num_cus(), band);
-    if (form == 45) return launch_c64r_raw<T, SI, EPI, 4, 2, false, false, true>(a, s, tiles, 2 * num_cus(), band);
     if (form == 44) return launch_c64r_raw<T, SI, EPI, 4, 2, false, true>(a, s, tiles, 2 * num_cus(), band);
     if (form == 84) return launch_c64r_raw<T, SI, EPI, 8, 4>(a, s, tiles, num_cus(), band);
     return launch_c64r_raw<T, SI, EPI, 8, 2>(a, s, tiles, num_cus(), band);
@@ -1200,7 +1182,7 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     // SG2_C64_RING: 0 off, else the ring form (launch_c64r_form: 4 default, 8, 84)
     const char* ring_env = getenv("SG2_C64_RING");   // read per launch: tests switch forms in one process
     const int ring = ring_env ? atoi(ring_env) : 4;
-    const int rth = (ring == 4 || ring == 44 || ring == 45) ? 4 : 8;
+    const int rth = (ring == 4 || ring == 44) ? 4 : 8;
     if (ring && !a.dot_out && a.Cin == P_C && a.Cout == P_C && a.H % rth == 0 && a.W % R_TW == 0 &&
         ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 && ((uintptr_t)a.noise % 16) == 0 &&
         ((uintptr_t)a.out_scale % 16) == 0 && ((uintptr_t)a.in_scale % 16) == 0 &&
@@ -1208,7 +1190,7 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         const int tiles = a.N * (a.H / rth) * (a.W / R_TW);
         const int grid = (rth == 4 ? 2 : 1) * num_cus();
         if (tiles >= 2 * grid && tiles <= 128 * grid && a.N < 4096 && a.H / rth < 1024 && a.W / R_TW < 1024) {
-            const int form = (ring == 84 || ring == 44 || ring == 45) ? ring : rth;
+            const int form = (ring == 84 || ring == 44) ? ring : rth;
             if (si) { if (epi) return launch_c64r_form<T, true, true>(a, s, form); return launch_c64r_form<T, true, false>(a, s, form); }
             if (epi) return launch_c64r_form<T, false, true>(a, s, form);
             return launch_c64r_form<T, false, false>(a, s, form);

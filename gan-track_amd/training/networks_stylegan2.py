@@ -288,7 +288,9 @@ def grouped_styles(ws, layers):
     idx, bidx, alpha, beta, ones, spans = _style_plan(layers, n, num_ws, ws.device)
     B = torch.mm(ones, (b * beta).view(1, -1))                         # [N, sum C]: row n = b * gain
     out = torch.addcmul(B.take(bidx), S.take(idx), alpha)
-    return [out.narrow(0, o, n * c).view(n, c) for o, c in spans]
+    # split (not narrow): its backward is ONE cat of the layers' gradients, a narrow's is a zero-filled full-size
+    # slice_backward per layer plus the adds that sum them
+    return [t.view(n, c) for t, (_, c) in zip(out.split([n * c for _, c in spans]), spans)]
 
 
 @persistence.persistent_class

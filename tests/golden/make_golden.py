@@ -541,6 +541,45 @@ def gen_emulated16(tag, dt):
     print(tag, dt, 'emulation written', flush=True)
 
 
+def gen_emulated32(tag, k, cache_dir):
+    """One sample of an emulated f32 evaluation of train_<tag>.npz (oracle.sg2_oracle.EMU16 = float32 with
+    EMU_JITTER seeded k: every block tensor and gradient rounded to f32 after a random sub-ulp nudge), saved to
+    <cache_dir>/e32_<tag>_<k>.npz; emu32merge folds the samples into the fixture as 'e32_<k>/...'.  How far these
+    land from the float64 answer is how far f32 rounding ALONE can move a result -- including the discrete
+    events (an lrelu mask at a few pixels) that a nudge of the state does not reproduce."""
+    import config_parity as cp
+    from oracle import sg2_oracle as O
+    path = os.path.join(OUT, f'train_{tag}.npz')
+    with np.load(path, allow_pickle=False) as f:
+        cfg, inp, tape, _ = cp.load_fixture(f)
+    O.EMU_JITTER = np.random.default_rng(1000 + int(k))
+    try:
+        out, _ = cp.run_oracle_f64(cfg, inp, tape, cfg.get('aug_p', 0.3), isolated=cfg.get('isolated', False),
+                                   emu16=torch.float32)
+    finally:
+        O.EMU_JITTER = None
+    os.makedirs(cache_dir, exist_ok=True)
+    np.savez_compressed(os.path.join(cache_dir, f'e32_{tag}_{k}.npz'), **pack(out))
+    print(tag, k, 'f32 emulation sample written', flush=True)
+
+
+def merge_emulated32(tag, cache_dir):
+    from golden_init import unpack
+    import glob
+    path = os.path.join(OUT, f'train_{tag}.npz')
+    with np.load(path, allow_pickle=False) as f:
+        z = unpack(f)
+    z = {k: v for k, v in z.items() if not k.startswith('e32_')}
+    n = 0
+    for fn in sorted(glob.glob(os.path.join(cache_dir, f'e32_{tag}_*.npz'))):
+        k = fn.rsplit('_', 1)[1][:-4]
+        with np.load(fn, allow_pickle=False) as f:
+            z.update({f'e32_{k}/{kk}': v for kk, v in unpack(f).items()})
+        n += 1
+    np.savez_compressed(path, **pack(z))
+    print(tag, n, 'f32 emulation samples merged', flush=True)
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['ops', 'nets'] + list(CONFIGS)
     for tag in CONFIGS:
@@ -558,6 +597,11 @@ if __name__ == '__main__':
         if w.startswith('emu:'):           # emu:<tag>:<fp16|bf16>
             parts = w.split(':')
             gen_emulated16(parts[1], parts[2])
+        if w.startswith('emu32:'):         # emu32:<tag>:<sample k>   (to $GOLD_CACHE, default /tmp/gold)
+            parts = w.split(':')
+            gen_emulated32(parts[1], parts[2], os.environ.get('GOLD_CACHE', '/tmp/gold'))
+        if w.startswith('emu32merge:'):    # emu32merge:<tag>
+            merge_emulated32(w.split(':')[1], os.environ.get('GOLD_CACHE', '/tmp/gold'))
         if w.startswith('cond:'):          # cond:<tag>[:<log2 of the nudge, default -24>]
             parts = w.split(':')
             gen_conditioning(parts[1], perturb=2.0 ** float(parts[2]) if len(parts) > 2 else 2.0 ** -24)
