@@ -32,6 +32,12 @@ REAL = torch.float32
 # arithmetic in between stays REAL: the oracle then evaluates the reference's 16-bit GPU iteration (to its
 # f32-versus-REAL accumulation difference), the yardstick the product's 16-bit results are held to.
 EMU16 = None
+# EMU16 = torch.float32 emulates an f32 evaluation instead: EVERY block rounds at those points (num_fp16_res plays
+# no part), and with EMU_JITTER (a numpy Generator: torch draws would enter the RNG tapes that replay the
+# reference's draws) each value is first nudged by a random fraction of an f32 ulp
+# (|u| < 2^-24 relative) -- independent samples of the rounding an f32 implementation of the same algorithm
+# makes, to measure how far f32 rounding alone can move a result (tests/golden/make_golden.py `emu32:`).
+EMU_JITTER = None
 
 
 class _Round16(torch.autograd.Function):
@@ -41,6 +47,9 @@ class _Round16(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, dt):
         ctx.dt = dt
+        if dt == torch.float32 and EMU_JITTER is not None:
+            u = torch.from_numpy(EMU_JITTER.uniform(-1.0, 1.0, tuple(x.shape))).to(x.dtype)
+            x = x * (1 + u * 2.0 ** -24)
         return x.to(dt).to(x.dtype)
 
     @staticmethod
@@ -518,7 +527,7 @@ class SynthesisBlock(torch.nn.Module):
             fused_modconv = self.fused_modconv_default
         if fused_modconv == 'inference_only':
             fused_modconv = not self.training
-        q = self.use_fp16 and EMU16 is not None and not force_fp32          # :419-420 (x.to(dtype) below)
+        q = (self.use_fp16 or EMU16 == torch.float32) and EMU16 is not None and not force_fp32   # :419-420
         if self.in_channels == 0:
             x = _q(self.const, q).unsqueeze(0).repeat([ws.shape[0], 1, 1, 1])
             x = self.conv1(x, next(w_iter), fused_modconv=fused_modconv, q16=q, **layer_kwargs)
@@ -620,7 +629,7 @@ class DiscriminatorBlock(torch.nn.Module):
                                     trainable=trainable(), resample_filter=resample_filter)
 
     def forward(self, x, img, force_fp32=False):
-        q = self.use_fp16 and EMU16 is not None and not force_fp32           # :607-608
+        q = (self.use_fp16 or EMU16 == torch.float32) and EMU16 is not None and not force_fp32   # :607-608
         x = _q(x, q)
         if self.in_channels == 0 or self.architecture == 'skip':
             y = self.fromrgb(_q(img, q), q16=q)

@@ -261,6 +261,17 @@ def _group(k):
     return 'grad/' + k.split('/')[1] if k.startswith('grad/') else k.split('/')[0]
 
 
+def _conditioning(fix):
+    """The fixture's samples of how far an f32-sized change moves each result: the float64 pass at a nudged
+    state ('f64p/') and the emulated f32 evaluations ('e32_<k>/': every block tensor rounded to f32 after a
+    random sub-ulp nudge, make_golden.py `emu32:`).  -> list of summary dicts."""
+    out = []
+    pre = sorted({k.split('/', 1)[0] for k in fix if k.startswith(('f64p/', 'e32_'))})
+    for p in pre:
+        out.append({k[len(p) + 1:]: v for k, v in fix.items() if k.startswith(p + '/')})
+    return out
+
+
 def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
               groups=('grad/', 'G1/', 'D1/', 'Gema1/'), check=True, alt=None, alt_max=0):
     """f32 results against the float64 answer (fixture keys 'f64/...'), per tensor k of group g (a phase's
@@ -284,19 +295,20 @@ def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
     err, worst ratio to the bound, its tensor)}, sorted ratios) and, with alt, the list of such tensors as
     worst['rounding_events']; raises after computing everything when `check` and any tensor is out of bounds."""
     truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
-    cond = {k[5:]: v for k, v in fix.items() if k.startswith('f64p/')}
+    conds = _conditioning(fix)
     kw, kg = _keys(truth, groups), _keys(got, groups)
     _one_sided_zero(got, truth, kg, kw)
     keys = sorted(set(kw) & set(kg))
     errs = {k: (_tensor_errs(got, truth, k), _tensor_errs(fix, truth, k)) for k in keys}
-    # with conditioning summaries (f64p/: float64 at a nudged state) a tensor's reference error term is the larger
-    # of the reference's f32 error and the conditioning shift -- both are samples of the spread any f32
-    # evaluation of that tensor has
+    # with conditioning summaries (f64p/: float64 at a nudged state; e32_<k>/: emulated f32 evaluations) a tensor's
+    # reference error term is the largest of the reference's f32 error and those shifts -- all are samples of the
+    # spread any f32 evaluation of that tensor has
     for k in keys:
-        if k + '/norm' in cond:
-            (gn, gs), (rn, rs_) = errs[k]
-            cn, cs = _tensor_errs(cond, truth, k)
-            errs[k] = ((gn, gs), (max(rn, cn), max(rs_, cs)))
+        for cond in conds:
+            if k + '/norm' in cond:
+                (gn, gs), (rn, rs_) = errs[k]
+                cn, cs = _tensor_errs(cond, truth, k)
+                errs[k] = ((gn, gs), (max(rn, cn), max(rs_, cs)))
     gmax = {}
     for k, (_, (rn, rs_)) in errs.items():
         m = gmax.get(_group(k), (0.0, 0.0))
@@ -340,13 +352,13 @@ def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/',), check=T
     evaluations (measured: D1/b512.conv1.bias at C4 / p = 0); the parameters are held by the flat check.
     Returns (number of tensors checked, worst error, its key)."""
     truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
-    cond = {k[5:]: v for k, v in fix.items() if k.startswith('f64p/')}
+    conds = _conditioning(fix)
     keys = sorted(set(_keys(truth, groups)) & set(_keys(got, groups)))
     n, worst, wk, fails = 0, 0.0, '', []
     for k in keys:
         rn, rs_ = _tensor_errs(fix, truth, k)
-        cn, cs = _tensor_errs(cond, truth, k) if k + '/norm' in cond else (0.0, 0.0)
-        if max(rn, rs_, cn, cs) >= well or float(fix[k + '/norm']) == 0.0:
+        cn = max([0.0] + [max(_tensor_errs(c, truth, k)) for c in conds if k + '/norm' in c])
+        if max(rn, rs_, cn) >= well or float(fix[k + '/norm']) == 0.0:
             continue
         n += 1
         en, es = _tensor_errs(got, fix, k)
