@@ -148,17 +148,20 @@ def _isolated_phases(tr, G, D, real, c, gz, gc):
 
 
 def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False, isolated=False, deterministic=True,
-                f32_exact=False):
+                f32_exact=False, grouped_affine=True):
     """The product's iteration on `dev`.  fp16_dtype None: all-f32 (num_fp16_res=0, the reference's CPU
     arithmetic); else the reference's GPU default num_fp16_res=4 in that 16-bit type.  isolated: every phase
     from the starting state, no optimiser step (the *_iso fixtures); returns the gradients, pl_mean and stats.
     deterministic: the library's fixed-order reductions (sg2hip.deterministic) -- the result is a function of
     the inputs, so a bound is met or missed by the code, not by a run's atomic order.  f32_exact: the f32 layers
     on the f32-input MFMA kernels (SG2_F32_EXACT=1) instead of the split-bf16 products (the other f32
-    arithmetic of the library, judge_f32's `alt`)."""
+    arithmetic of the library, judge_f32's `alt`); grouped_affine False: the synthesis affine layers one GEMM
+    each (networks_stylegan2.grouped_affine), another evaluation order of the styles."""
     import sg2hip
     from torch_utils.ops import conv2d_gradfix as cg
-    prev = (os.environ.get('SG2_F32_EXACT'), cg.presplit)
+    from training import networks_stylegan2 as nets
+    prev = (os.environ.get('SG2_F32_EXACT'), cg.presplit, nets.grouped_affine)
+    nets.grouped_affine = grouped_affine
     if f32_exact:
         os.environ['SG2_F32_EXACT'] = '1'
         cg.presplit = False
@@ -171,6 +174,7 @@ def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False, i
         else:
             os.environ['SG2_F32_EXACT'] = prev[0]
         cg.presplit = prev[1]
+        nets.grouped_affine = prev[2]
 
 
 def _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated):
@@ -286,12 +290,13 @@ def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
     tensor of a phase draws the short straw is chance, so the bound also admits the reference's worst
     error in the same phase.
 
-    alt: the same evaluation in the product's other f32 arithmetic (run_product(f32_exact=True), itself judged
-    strictly).  The two differ only in how each product and sum rounds; a tensor whose value hinges on a
+    alt: the same evaluation in the product's other f32 evaluation orders (one summary or a list: the f32-input
+    MFMA arithmetic, run_product(f32_exact=True); the per-layer affine GEMMs, grouped_affine=False), each itself
+    judged the same way.  They differ only in how products and sums round; a tensor whose value hinges on a
     discrete event at rounding size (an lrelu mask at a few pixels, tools/greg_probe.py) can land on different
-    sides of it in the two.  Up to `alt_max` tensors may then exceed the bound by at most their distance to
-    the alternative evaluation; a systematic defect of one arithmetic moves many tensors and the phase's flat
-    vector (judge_flat) and fails.  Returns ({group: (worst norm err, worst sample err, worst reference norm
+    sides of it in different orders.  Up to `alt_max` tensors may then exceed the bound by at most their largest
+    distance to an alternative evaluation; a systematic defect moves many tensors and the phase's flat vector
+    (judge_flat) and fails.  Returns ({group: (worst norm err, worst sample err, worst reference norm
     err, worst ratio to the bound, its tensor)}, sorted ratios) and, with alt, the list of such tensors as
     worst['rounding_events']; raises after computing everything when `check` and any tensor is out of bounds."""
     truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
@@ -314,6 +319,7 @@ def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
         m = gmax.get(_group(k), (0.0, 0.0))
         gmax[_group(k)] = (max(m[0], rn), max(m[1], rs_))
     worst, ratios, fails, events = {}, [], [], []
+    alts = (alt if isinstance(alt, (list, tuple)) else [alt]) if alt is not None else []
     for k in keys:
         (gn, gs), (rn, rs_) = errs[k]
         g = _group(k)
@@ -324,8 +330,9 @@ def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
         ratio = max(gn / bn, gs / bs)
         ratios.append(ratio)
         worst[g] = (max(w[0], gn), max(w[1], gs), max(w[2], rn), max(w[3], ratio), k if ratio > w[3] else w[4])
-        if (gn > bn or gs > bs) and alt is not None and k + '/norm' in alt:
-            an, as_ = _tensor_errs(got, alt, k)
+        if (gn > bn or gs > bs) and alt is not None and all(k + '/norm' in a for a in alts):
+            dists = [_tensor_errs(got, a, k) for a in alts]
+            an, as_ = max(d[0] for d in dists), max(d[1] for d in dists)
             if gn <= bn + an and gs <= bs + as_:
                 events.append(f'{k}: err {gn:.3g} / {gs:.3g}, bound {bn:.3g} / {bs:.3g}, distance to the other '
                               f'f32 arithmetic {an:.3g} / {as_:.3g}')
