@@ -60,16 +60,53 @@ class _InfNorm(torch.autograd.Function):
         if not ctx.needs_input_grad[0]:
             return None, None, None
         if torch.is_grad_enabled():
-            n = t.norm(float('inf'), dim=1, keepdim=True)
-            y = t * (ctx.c / n) if ctx.mode == 0 else t / n
-            dt, = torch.autograd.grad(y, t, dy, create_graph=True)
-            return dt, None, None
+            return _InfNormVJP.apply(dy, t, nrm, ctx.c if ctx.mode == 0 else 1.0, ctx.mode), None, None
         dy, t = dy.contiguous(), t.contiguous()
         dt = torch.empty_like(t)
         _hip.check(_hip.lib().sg2_infnorm_bwd(_hip.ptr(dt), _hip.ptr(dy), _hip.ptr(t), _hip.ptr(nrm), t.shape[0],
                                               t.shape[1], float(ctx.c), ctx.mode, _hip.stream_ptr(t.device)),
                    'sg2_infnorm_bwd')
         return dt, None, None
+
+
+class _InfNormVJP(torch.autograd.Function):
+    """The first-order gradient of _InfNorm as ONE differentiable node (the path-length pass differentiates it once
+    more): forward dt = c dy / n - c P e / n^2 (sg2_infnorm_bwd), with n = max_j |t_j| per row, P = sum_j dy_j t_j and
+    e_j = sign(t_j) [|t_j| = n] / (number of maxima) -- torch's infinity-norm gradient, ties split evenly; backward
+    from the closed form (the maxima mask piecewise constant):
+        g_dy = c (g - t (g.e) / n) / n
+        g_t  = c (2 P (g.e) e / n^3 - ((g.dy) e + (g.e) dy) / n^2)
+    in ~15 launches, where autograd of the reference expression re-derived under create_graph (norm, reciprocal,
+    scale, multiply) and differentiated again ran ~40 per call (tests/test_ops_gpu.py::test_infnorm_prenorm checks
+    the second order against it)."""
+
+    @staticmethod
+    def forward(ctx, dy, t, nrm, c, mode):
+        dy, t = dy.contiguous(), t.contiguous()
+        dt = torch.empty_like(t)
+        _hip.check(_hip.lib().sg2_infnorm_bwd(_hip.ptr(dt), _hip.ptr(dy), _hip.ptr(t), _hip.ptr(nrm), t.shape[0],
+                                              t.shape[1], float(c), mode, _hip.stream_ptr(t.device)), 'sg2_infnorm_bwd')
+        ctx.save_for_backward(dy, t, nrm)
+        ctx.c = c
+        return dt
+
+    @staticmethod
+    def backward(ctx, g):
+        dy, t, nrm = ctx.saved_tensors
+        c = ctx.c
+        n = nrm[:, None]
+        m = ((t.abs() == n) | torch.isnan(t)).to(t.dtype)
+        e = torch.sign(t) * m / m.sum(1, keepdim=True)
+        ge = (g * e).sum(1, keepdim=True)
+        g_dy = g_t = None
+        if ctx.needs_input_grad[0]:
+            g_dy = (g - t * (ge / n)) * (c / n)
+        if ctx.needs_input_grad[1]:
+            gdy = (g * dy).sum(1, keepdim=True)
+            P = (dy * t).sum(1, keepdim=True)
+            n2 = n * n
+            g_t = (e * (2 * c * P * ge / (n2 * n) - c * gdy / n2)) - dy * (c * ge / n2)
+        return g_dy, g_t, None, None, None
 
 
 def _prenorm(weight, styles):
@@ -110,6 +147,8 @@ class _Demod(torch.autograd.Function):
             # the reference's composed expression; a custom Function's needs_input_grad cannot tell, so skip it
             # here instead of building its double-backward graph.
             need_w = need_w and not conv2d_gradfix.weight_gradients_disabled
+            if need_s and not need_w:
+                return None, _DemodVJP.apply(dd, d, w, s, wsq)
             gu = dd * d.pow(3) * -0.5
             gs = 2 * s * (gu @ w.square().sum([2, 3])) if need_s else None
             gw = 2 * w * (gu.t() @ s.square())[:, :, None, None] if need_w else None
@@ -122,6 +161,39 @@ class _Demod(torch.autograd.Function):
                                             _hip.ptr(w), _hip.ptr(wsq), n, o, i, kk, _hip.stream_ptr(s.device)),
                    'sg2_demod_bwd')
         return gw, gs
+
+
+class _DemodVJP(torch.autograd.Function):
+    """The styles' gradient of _Demod as one differentiable node for the path-length pass (whose first pass wants
+    no weight gradient): forward gs = 2 s (u @ wsq) with u = -dd d^3 / 2 and wsq = sum_k w^2 (sg2_demod_bwd, one
+    launch where the composed form runs seven); backward from the closed form
+        g_s = 2 G (u @ wsq),  g_u = (2 s G) @ wsq^T,  g_w = 2 w (u^T @ (2 s G)),
+        g_dd = -d^3 g_u / 2,  g_d = -3 dd d^2 g_u / 2
+    (d, w and s carry their own autograd history, so the second pass continues into _Demod, the weight and the
+    styles exactly as the composed expression did)."""
+
+    @staticmethod
+    def forward(ctx, dd, d, w, s, wsq):
+        dd = dd.float().contiguous()
+        n, o, i, kk = s.shape[0], w.shape[0], w.shape[1], w.shape[2] * w.shape[3]
+        gs = torch.empty_like(s)
+        _hip.check(_hip.lib().sg2_demod_bwd(_hip.ptr(gs), _hip.ptr(None), _hip.ptr(dd), _hip.ptr(d), _hip.ptr(s), _hip.ptr(w),
+                                            _hip.ptr(wsq), n, o, i, kk, _hip.stream_ptr(s.device)), 'sg2_demod_bwd')
+        ctx.save_for_backward(dd, d, w, s, wsq)
+        return gs
+
+    @staticmethod
+    def backward(ctx, g):
+        dd, d, w, s, wsq = ctx.saved_tensors
+        d2 = d * d
+        u = dd * d2 * d * -0.5
+        gq = s * g * 2
+        gu = gq @ wsq.t()
+        g_dd = gu * d2 * d * -0.5 if ctx.needs_input_grad[0] else None
+        g_d = gu * d2 * dd * -1.5 if ctx.needs_input_grad[1] else None
+        g_w = w * (u.t() @ gq)[:, :, None, None] * 2 if ctx.needs_input_grad[2] else None
+        g_s = (u @ wsq) * g * 2 if ctx.needs_input_grad[3] else None
+        return g_dd, g_d, g_w, g_s, None
 
 
 def _demod(weight, styles):

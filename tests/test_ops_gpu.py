@@ -899,7 +899,14 @@ def test_demod_kernel():
         gw, gs = torch.autograd.grad((d * dd.to(dev, dt)).sum(), [wd, sd], create_graph=True)
         gw2, = torch.autograd.grad((gs.square().sum() + gw.square().sum()), [wd])
         gwf, gsf = torch.autograd.grad((fn(wd, sd) * dd.to(dev, dt)).sum(), [wd, sd])   # first-order kernel path
-        ref.append([t.detach().double().cpu() for t in (d, gw, gs, gw2, gwf, gsf)])
+        # the path-length shape (_DemodVJP): first pass for the styles only under no_weight_gradients, then a
+        # second pass into both the weight and the styles through that gradient and through d itself
+        from torch_utils.ops import conv2d_gradfix as cg
+        dp = fn(wd, sd)
+        with cg.no_weight_gradients(dev.type == 'cuda'):
+            gsp, = torch.autograd.grad((dp * dd.to(dev, dt)).sum(), [sd], create_graph=True)
+        gw3, gs3 = torch.autograd.grad(gsp.square().sum() + (dp * dd.to(dev, dt)).square().sum(), [wd, sd])
+        ref.append([t.detach().double().cpu() for t in (d, gw, gs, gw2, gwf, gsf, gsp, gw3, gs3)])
     for a, b in zip(*ref):
         assert rel_err(a, b) < 1e-5
 

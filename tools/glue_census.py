@@ -1,7 +1,7 @@
 """Where the step's torch (non-HIP-kernel) launches come from (GPU, eager): records every aten op that one
 16-iteration cycle dispatches, keyed by the op and its origin -- the autograd node running it (backward)
 or the innermost frames of this repo's code (forward) -- and prints the most frequent per step.
-Usage: python tools/glue_census.py"""
+Usage: python tools/glue_census.py [phase]   (phase: count only that loss phase, e.g. Greg)"""
 import os
 import sys
 import traceback
@@ -23,10 +23,13 @@ counts = Counter()
 big = Counter()      # ops over >= 1M-element tensors: (op, origin, shape, dtype) -> count
 
 
+CUR = {'phase': None}
+
+
 class Census(TorchDispatchMode):
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         name = func.overloadpacket.__name__
-        if name not in VIEWS:
+        if name not in VIEWS and (ONLY is None or CUR['phase'] == ONLY):
             node = torch._C._current_autograd_node()
             if node is not None:
                 origin = 'bwd ' + node.name()
@@ -40,10 +43,23 @@ class Census(TorchDispatchMode):
         return func(*args, **(kwargs or {}))
 
 
+ONLY = sys.argv[1] if len(sys.argv) > 1 else None
 sys.argv = [sys.argv[0], '--graphs', 'off', '--no-cpu-baseline']
 args = bench.parse()
 dev = torch.device('cuda', 0)
 tr = bench.build(args, dev, 0, 1)
+_orig_acc = type(tr.loss).accumulate_gradients
+
+
+def _acc(self, *a, **k):
+    CUR['phase'] = k.get('phase', a[0] if a else None)
+    try:
+        return _orig_acc(self, *a, **k)
+    finally:
+        CUR['phase'] = None
+
+
+type(tr.loss).accumulate_gradients = _acc
 real, real_c = bench.make_inputs(args, dev, 0)
 for _ in range(2):
     bench.one_step(tr, args, dev, real, real_c)
