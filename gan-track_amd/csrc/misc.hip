@@ -232,6 +232,96 @@ __global__ __launch_bounds__(256) void infnorm_bwd_kernel(float* __restrict__ dt
     }
 }
 
+// Second order of the path-length pass (networks_stylegan2._DemodVJP / _InfNormVJP): the backward of the
+// first-order gradients above, each from its closed form, so that a differentiated gradient costs one or two
+// launches instead of the ~25 torch elementwise / reduction launches of its composed form.
+//
+// demod: with sg = s * g and v[n,o] = sum_i sg[n,i] wsq[o,i] (workgroup per o; wsq row in LDS, 8 lanes/sample)
+//   g_dd = -d^3 v,   g_d = -3 dd d^2 v,   g_w[o,i,k] = -2 w[o,i,k] sum_n dd d^3 sg[n,i]
+// (the styles' part, g_s = 2 g (u @ wsq) with u = -dd d^3 / 2, is demod_bwd_s_kernel with s := g).
+__global__ __launch_bounds__(256) void demod_vjp_o_kernel(float* g_dd, float* g_d, float* g_w, const float* g,
+                                                          const float* dd, const float* d, const float* s,
+                                                          const float* w, const float* wsq, int N, int O, int I,
+                                                          int KK) {
+    __shared__ float wr[1024];
+    __shared__ float z[1024];
+    const int o = blockIdx.x;
+    for (int i = threadIdx.x; i < I; i += 256) wr[i] = wsq[(int64_t)o * I + i];
+    for (int n = threadIdx.x; n < N; n += 256) {
+        const float dv = d[(int64_t)n * O + o];
+        z[n] = dd[(int64_t)n * O + o] * dv * dv * dv;
+    }
+    __syncthreads();
+    if (g_dd || g_d) {
+        const int seg = threadIdx.x & 7, len = (I + 7) / 8, i0 = seg * len, i1 = min(I, i0 + len);
+        for (int n0 = 0; n0 < N; n0 += 32) {
+            const int n = n0 + (threadIdx.x >> 3);
+            float acc = 0.f;
+            if (n < N) {
+                const float* sr = s + (int64_t)n * I;
+                const float* gr = g + (int64_t)n * I;
+#pragma unroll 8
+                for (int i = i0; i < i1; ++i) acc += sr[i] * gr[i] * wr[i];
+            }
+            acc += __shfl_xor(acc, 1);
+            acc += __shfl_xor(acc, 2);
+            acc += __shfl_xor(acc, 4);
+            if (seg == 0 && n < N) {
+                const int64_t e = (int64_t)n * O + o;
+                const float dv = d[e];
+                if (g_dd) g_dd[e] = -(dv * dv * dv) * acc;
+                if (g_d) g_d[e] = -3.f * dd[e] * dv * dv * acc;
+            }
+        }
+    }
+    if (g_w) {
+        for (int i = threadIdx.x; i < I; i += 256) {
+            float acc = 0.f;
+            for (int n = 0; n < N; ++n) acc += z[n] * s[(int64_t)n * I + i] * g[(int64_t)n * I + i];
+            const float* wk = w + ((int64_t)o * I + i) * KK;
+            float* gk = g_w + ((int64_t)o * I + i) * KK;
+            for (int k = 0; k < KK; ++k) gk[k] = -2.f * wk[k] * acc;
+        }
+    }
+}
+
+// infnorm: with e = sgn(t) [|t| = n] / cnt, ge = sum g e, gdy = sum g dy, P = sum dy t (workgroup per row),
+//   g_dy = c (g - t ge / n) / n,   g_t = e (2 c P ge / n^3 - c gdy / n^2) - dy c ge / n^2
+// (c = the mode-0 scale, 1 for the styles).
+__global__ __launch_bounds__(256) void infnorm_vjp_kernel(float* __restrict__ g_dy, float* __restrict__ g_t,
+                                                          const float* __restrict__ g, const float* __restrict__ dy,
+                                                          const float* __restrict__ t, const float* __restrict__ nrm,
+                                                          int L, float c) {
+    __shared__ float red[4];
+    const int64_t base = (int64_t)blockIdx.x * L;
+    const float n = nrm[blockIdx.x];
+    float cnt = 0.f, ge = 0.f, gdy = 0.f, P = 0.f;
+    for (int i = threadIdx.x; i < L; i += 256) {
+        const float tv = t[base + i], gv = g[base + i], dv = dy[base + i];
+        if (fabsf(tv) == n || tv != tv) {
+            cnt += 1.f;
+            ge += tv > 0.f ? gv : (tv < 0.f ? -gv : (tv != tv ? tv : 0.f));
+        }
+        gdy += gv * dv;
+        P += dv * tv;
+    }
+    cnt = block_reduce(cnt, red, false);
+    ge = block_reduce(ge, red, false) / cnt;
+    gdy = block_reduce(gdy, red, false);
+    P = block_reduce(P, red, false);
+    const float n2 = n * n;
+    const float a = 2.f * c * P * ge / (n2 * n) - c * gdy / n2, b = c * ge / n2;
+    for (int i = threadIdx.x; i < L; i += 256) {
+        const float tv = t[base + i], gv = g[base + i], dv = dy[base + i];
+        if (g_dy) g_dy[base + i] = c * (gv - tv * (ge / n)) / n;
+        if (g_t) {
+            float e = 0.f;
+            if (fabsf(tv) == n || tv != tv) e = (tv > 0.f ? 1.f : (tv < 0.f ? -1.f : (tv != tv ? tv : 0.f))) / cnt;
+            g_t[base + i] = e * a - dv * b;
+        }
+    }
+}
+
 }  // namespace
 
 __global__ void zero_fill_kernel(unsigned char* p, size_t bytes) {
@@ -281,6 +371,36 @@ extern "C" int sg2_demod_bwd(float* gs, float* gw, const float* dd, const float*
         return launch_status("sg2_demod_bwd");
     }
     return 0;
+}
+
+extern "C" int sg2_demod_vjp_bwd(float* g_dd, float* g_d, float* g_w, float* g_s, const float* g, const float* dd,
+                                 const float* d, const float* s, const float* w, const float* wsq, int N, int O, int I,
+                                 int KK, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(g && dd && d && s && w && wsq, "sg2_demod_vjp_bwd: null pointer");
+    SG2_CHECK(I <= 1024 && O <= 1024 && N <= 1024 && I > 0 && O > 0 && N > 0 && KK > 0,
+              "sg2_demod_vjp_bwd: unsupported shape");
+    hipStream_t st = as_stream(stream);
+    if (g_dd || g_d || g_w) {
+        demod_vjp_o_kernel<<<O, 256, 0, st>>>(g_dd, g_d, g_w, g, dd, d, s, w, wsq, N, O, I, KK);
+        int rc = launch_status("sg2_demod_vjp_bwd");
+        if (rc) return rc;
+    }
+    if (g_s) {
+        demod_bwd_s_kernel<<<dim3(N, (I + 63) / 64), 256, 0, st>>>(g_s, dd, d, g, wsq, N, O, I);
+        return launch_status("sg2_demod_vjp_bwd");
+    }
+    return 0;
+}
+
+extern "C" int sg2_infnorm_vjp_bwd(float* g_dy, float* g_t, const float* g, const float* dy, const float* t,
+                                   const float* nrm, int rows, int L, float c, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(g && dy && t && nrm, "sg2_infnorm_vjp_bwd: null pointer");
+    SG2_CHECK(rows >= 0 && L > 0, "sg2_infnorm_vjp_bwd: bad shape");
+    if (rows == 0 || (!g_dy && !g_t)) return 0;
+    infnorm_vjp_kernel<<<rows, 256, 0, as_stream(stream)>>>(g_dy, g_t, g, dy, t, nrm, L, c);
+    return launch_status("sg2_infnorm_vjp_bwd");
 }
 
 extern "C" int sg2_adam_multi(const int64_t* seg, const float* coef, const int64_t* blocks, int nblocks,

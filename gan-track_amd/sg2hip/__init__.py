@@ -76,13 +76,15 @@ SIGNATURES = {
     'sg2_moments': [_vp, _vp, _i64, _i, _vp],
     'sg2_demod_fwd': [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp],
     'sg2_demod_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
+    'sg2_demod_vjp_bwd': [_vp] * 10 + [_i, _i, _i, _i, _vp],
     'sg2_adam_multi': [_vp, _vp, _vp, _i, _vp, _vp, _vp, _f, _f, _f, _f, _i, _vp],
     'sg2_lerp_multi': [_vp, _vp, _i, _f, _vp],
     'sg2_infnorm_fwd': [_vp, _vp, _vp, _i, _i, _f, _i, _vp],
     'sg2_infnorm_bwd': [_vp, _vp, _vp, _vp, _i, _i, _f, _i, _vp],
+    'sg2_infnorm_vjp_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _f, _vp],
     'sg2_pack_weight': [_vp, _i, _vp, _i, _i, _i, _i, _i64, _i64, _i64, _i, _f, _vp],
 }
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lib = None
 

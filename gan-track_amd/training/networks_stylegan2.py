@@ -76,9 +76,9 @@ class _InfNormVJP(torch.autograd.Function):
     from the closed form (the maxima mask piecewise constant):
         g_dy = c (g - t (g.e) / n) / n
         g_t  = c (2 P (g.e) e / n^3 - ((g.dy) e + (g.e) dy) / n^2)
-    in ~15 launches, where autograd of the reference expression re-derived under create_graph (norm, reciprocal,
-    scale, multiply) and differentiated again ran ~40 per call (tests/test_ops_gpu.py::test_infnorm_prenorm checks
-    the second order against it)."""
+    in one launch (sg2_infnorm_vjp_bwd), where autograd of the reference expression re-derived under create_graph
+    (norm, reciprocal, scale, multiply) and differentiated again ran ~40 per call (tests/test_ops_gpu.py::
+    test_infnorm_prenorm checks the second order against it)."""
 
     @staticmethod
     def forward(ctx, dy, t, nrm, c, mode):
@@ -93,19 +93,12 @@ class _InfNormVJP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         dy, t, nrm = ctx.saved_tensors
-        c = ctx.c
-        n = nrm[:, None]
-        m = ((t.abs() == n) | torch.isnan(t)).to(t.dtype)
-        e = torch.sign(t) * m / m.sum(1, keepdim=True)
-        ge = (g * e).sum(1, keepdim=True)
-        g_dy = g_t = None
-        if ctx.needs_input_grad[0]:
-            g_dy = (g - t * (ge / n)) * (c / n)
-        if ctx.needs_input_grad[1]:
-            gdy = (g * dy).sum(1, keepdim=True)
-            P = (dy * t).sum(1, keepdim=True)
-            n2 = n * n
-            g_t = (e * (2 * c * P * ge / (n2 * n) - c * gdy / n2)) - dy * (c * ge / n2)
+        g = g.float().contiguous()
+        g_dy = torch.empty_like(dy) if ctx.needs_input_grad[0] else None
+        g_t = torch.empty_like(t) if ctx.needs_input_grad[1] else None
+        _hip.check(_hip.lib().sg2_infnorm_vjp_bwd(_hip.ptr(g_dy), _hip.ptr(g_t), _hip.ptr(g), _hip.ptr(dy),
+                                                  _hip.ptr(t), _hip.ptr(nrm), t.shape[0], t.shape[1], float(ctx.c),
+                                                  _hip.stream_ptr(t.device)), 'sg2_infnorm_vjp_bwd')
         return g_dy, g_t, None, None, None
 
 
@@ -166,7 +159,7 @@ class _Demod(torch.autograd.Function):
 class _DemodVJP(torch.autograd.Function):
     """The styles' gradient of _Demod as one differentiable node for the path-length pass (whose first pass wants
     no weight gradient): forward gs = 2 s (u @ wsq) with u = -dd d^3 / 2 and wsq = sum_k w^2 (sg2_demod_bwd, one
-    launch where the composed form runs seven); backward from the closed form
+    launch where the composed form runs seven); backward from the closed form in two (sg2_demod_vjp_bwd)
         g_s = 2 G (u @ wsq),  g_u = (2 s G) @ wsq^T,  g_w = 2 w (u^T @ (2 s G)),
         g_dd = -d^3 g_u / 2,  g_d = -3 dd d^2 g_u / 2
     (d, w and s carry their own autograd history, so the second pass continues into _Demod, the weight and the
@@ -185,14 +178,17 @@ class _DemodVJP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         dd, d, w, s, wsq = ctx.saved_tensors
-        d2 = d * d
-        u = dd * d2 * d * -0.5
-        gq = s * g * 2
-        gu = gq @ wsq.t()
-        g_dd = gu * d2 * d * -0.5 if ctx.needs_input_grad[0] else None
-        g_d = gu * d2 * dd * -1.5 if ctx.needs_input_grad[1] else None
-        g_w = w * (u.t() @ gq)[:, :, None, None] * 2 if ctx.needs_input_grad[2] else None
-        g_s = (u @ wsq) * g * 2 if ctx.needs_input_grad[3] else None
+        g = g.float().contiguous()
+        need = ctx.needs_input_grad
+        g_dd = torch.empty_like(dd) if need[0] else None
+        g_d = torch.empty_like(d) if need[1] else None
+        g_w = torch.empty_like(w) if need[2] else None
+        g_s = torch.empty_like(s) if need[3] else None
+        n, o, i, kk = s.shape[0], w.shape[0], w.shape[1], w.shape[2] * w.shape[3]
+        _hip.check(_hip.lib().sg2_demod_vjp_bwd(_hip.ptr(g_dd), _hip.ptr(g_d), _hip.ptr(g_w), _hip.ptr(g_s),
+                                                _hip.ptr(g), _hip.ptr(dd), _hip.ptr(d), _hip.ptr(s), _hip.ptr(w),
+                                                _hip.ptr(wsq), n, o, i, kk, _hip.stream_ptr(s.device)),
+                   'sg2_demod_vjp_bwd')
         return g_dd, g_d, g_w, g_s, None
 
 

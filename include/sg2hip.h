@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define SG2_ABI_VERSION 6
+#define SG2_ABI_VERSION 7
 
 enum sg2_dtype { SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2, SG2_F32S3 = 3 };
 
@@ -308,6 +308,16 @@ int sg2_demod_fwd(float* d, float* wsq, const float* s, const float* w, int N, i
 int sg2_demod_bwd(float* gs, float* gw, const float* dd, const float* d, const float* s, const float* w,
                   const float* wsq, int N, int O, int I, int KK, void* stream);
 
+/* Backward of sg2_demod_bwd's styles gradient gs = 2 s (u @ wsq), u = -dd d^3 / 2 (ABI 7; the path-length pass
+ * differentiates it once more -- the reference by autograd of networks_stylegan2.py:59-63 under create_graph):
+ * given g = dL/dgs [N,I],
+ *   g_dd = -d^3 v,  g_d = -3 dd d^2 v  (v = (s g) @ wsq^T),   g_w[o,i,k] = 2 w (u^T @ 2 s g)[o,i],
+ *   g_s = 2 g (u @ wsq).
+ * Any output may be NULL; w [O,I*KK], wsq [O,I] as written by sg2_demod_fwd. */
+int sg2_demod_vjp_bwd(float* g_dd, float* g_d, float* g_w, float* g_s, const float* g, const float* dd,
+                      const float* d, const float* s, const float* w, const float* wsq, int N, int O, int I, int KK,
+                      void* stream);
+
 /* Convolution weight pack (replaces the strided-permute copies that feed every conv launch,
  * conv2d_gradfix.py _pack_conv / _pack_convT; the reference feeds cuDNN the [O,I,kh,kw] weight
  * directly, networks_stylegan2.py:70/176):  out[a][k][b] = in[a*sa + b*sb + k'*sk], k' = K-1-k when
@@ -327,6 +337,14 @@ int sg2_infnorm_fwd(float* y, float* nrm, const float* t, int rows, int L, float
  * evenly between tied maxima). */
 int sg2_infnorm_bwd(float* dt, const float* dy, const float* t, const float* nrm, int rows, int L, float c, int mode,
                     void* stream);
+
+/* Backward of sg2_infnorm_bwd (ABI 7; the path-length pass's second order through the fp16 pre-normalisation,
+ * reference: autograd of networks_stylegan2.py:52-54 under create_graph).  With the first-order gradient
+ * dt = c dy / n - c P e / n^2, P = sum dy t, e = sgn(t) [|t| = n] / cnt, and g = dL/ddt [rows, L]:
+ *   g_dy = c (g - t (g.e) / n) / n,   g_t = c (2 P (g.e) e / n^3 - ((g.dy) e + (g.e) dy) / n^2).
+ * c = the mode-0 scale (1 for mode 1); either output may be NULL. */
+int sg2_infnorm_vjp_bwd(float* g_dy, float* g_t, const float* g, const float* dy, const float* t, const float* nrm,
+                        int rows, int L, float c, void* stream);
 
 /* Multi-tensor launches of the optimiser step.  A segment is one parameter tensor; `blocks` [nblocks] lists
  * the work items as (segment << 40) | start, one per 4096 elements of a segment (start = 0, 4096, ...),
