@@ -9,7 +9,9 @@
 // Two kernels:
 //  * upfirdn_nhwc_vec: channels-last activations with C % V == 0 (the network's feature maps);
 //    each lane owns one 16-byte channel vector of one output pixel, so every tap read is a
-//    coalesced 16-byte load and neighbouring taps hit L1/L2.
+//    coalesced 16-byte load and neighbouring taps hit L1/L2.  Its specialisations: upfirdn_nhwc_f4 /
+//    upfirdn_nhwc_f4s (4x4, up 1: LDS-staged tiles, column strips) and upfirdn_nhwc_up2 (4x4, up 2, down 1:
+//    a 2 x 2 output cell per lane from one 3 x 3 input neighbourhood).
 //  * upfirdn_generic : any 4-D strides (images, NCHW tensors, odd channel counts).
 #include <cstdlib>
 
@@ -192,8 +194,10 @@ __device__ __forceinline__ void store_out(const UpfParams& p, T* y, const float*
 }
 
 
-// channels-last, C % V == 0, xs_c == ys_c == 1.
-template <typename T>
+// channels-last, C % V == 0, xs_c == ys_c == 1.  IDX: the flat output index type -- unsigned 32-bit when
+// N*OH*OW*C/V < 2^31 (the host checks), where the 64-bit divisions and remainders that split it into
+// (n, oy, ox, cv) cost ~4x the rest of the lane's work (the up-2 adjoint FIRs of the D skips).
+template <typename T, typename IDX>
 __global__ __launch_bounds__(256) void upfirdn_nhwc_vec(UpfParams p) {
     constexpr int V = VecN<T>::N;
     typedef T vecT __attribute__((ext_vector_type(V)));
@@ -201,14 +205,13 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_vec(UpfParams p) {
     stage_filter(sf, p);
     const T* x = (const T*)p.x;
     T* y = (T*)p.y;
-    const int CV = p.C / V;
-    const int64_t total = (int64_t)p.N * p.OH * p.OW * CV;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        int64_t r = idx;
+    const IDX CV = (IDX)(p.C / V), OW = (IDX)p.OW, OH = (IDX)p.OH;
+    const IDX total = (IDX)((int64_t)p.N * p.OH * p.OW * (p.C / V));
+    for (IDX idx = (IDX)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (IDX)gridDim.x * blockDim.x) {
+        IDX r = idx;
         const int cv = (int)(r % CV); r /= CV;
-        const int ox = (int)(r % p.OW); r /= p.OW;
-        const int oy = (int)(r % p.OH); r /= p.OH;
+        const int ox = (int)(r % OW); r /= OW;
+        const int oy = (int)(r % OH); r /= OH;
         const int n = (int)r;
         int ty0, iy0, tx0, ix0;
         axis_taps(oy, p.downy, p.pady0, p.upy, ty0, iy0);
@@ -229,6 +232,80 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_vec(UpfParams p) {
             }
         }
         store_out<T, V, vecT>(p, y, acc, n, oy, ox, cv);
+    }
+}
+
+// 4x4 filter, up = 2, down = 1 on both axes, channels-last (the adjoint of every down-2 FIR: the D skips'
+// input gradients; upsample2d): a lane owns one channel vector of a 2 x 2 output cell (2 cy + py, 2 cx + px).
+// Each output reads 2 x 2 input pixels and the cell's four outputs read inside one 3 x 3 neighbourhood,
+// so the lane issues its 9 loads at once (vs 16 dependent ones for four upfirdn_nhwc_vec iterations) and
+// all index math is 32-bit (the host checks the cell count).
+template <typename T>
+__global__ __launch_bounds__(256) void upfirdn_nhwc_up2(UpfParams p) {
+    constexpr int V = VecN<T>::N;
+    typedef T vecT __attribute__((ext_vector_type(V)));
+    __shared__ float sf[16];
+    if (threadIdx.x < 16) {
+        const int ty = threadIdx.x >> 2, tx = threadIdx.x & 3;
+        sf[threadIdx.x] = p.f[(p.flip ? ty : 3 - ty) * 4 + (p.flip ? tx : 3 - tx)] * p.gain;
+    }
+    __syncthreads();
+    const unsigned CV = p.C / V, CW = (p.OW + 1) >> 1, CH = (p.OH + 1) >> 1;
+    const unsigned total = (unsigned)p.N * CH * CW * CV;
+    const unsigned idx = blockIdx.x * 256u + threadIdx.x;
+    if (idx >= total) return;
+    unsigned r = idx;
+    const int cv = (int)(r % CV); r /= CV;
+    const int cx = (int)(r % CW); r /= CW;
+    const int cy = (int)(r % CH);
+    const int n = (int)(r / CH);
+    // per output row / column of the cell: first tap and its input index (axis_taps), relative to the first
+    int ty[2], iy[2], tx[2], ix[2];
+    axis_taps(2 * cy, 1, p.pady0, 2, ty[0], iy[0]);
+    axis_taps(2 * cy + 1, 1, p.pady0, 2, ty[1], iy[1]);
+    axis_taps(2 * cx, 1, p.padx0, 2, tx[0], ix[0]);
+    axis_taps(2 * cx + 1, 1, p.padx0, 2, tx[1], ix[1]);
+    const int y0 = min(iy[0], iy[1]), x0 = min(ix[0], ix[1]);
+    const T* xb = (const T*)p.x + n * p.xs_n + cv * V;
+    vecT xv[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const int yy = y0 + a, xx = x0 + b;
+            const bool ok = yy >= 0 && yy < p.H && xx >= 0 && xx < p.W;
+            xv[a][b] = ok ? *(const vecT*)(xb + yy * p.xs_h + xx * p.xs_w) : vecT{};
+        }
+#pragma unroll
+    for (int py = 0; py < 2; ++py) {
+        const int oy = 2 * cy + py;
+        if (oy >= p.OH) continue;
+        const int dy = iy[py] - y0;
+#pragma unroll
+        for (int px = 0; px < 2; ++px) {
+            const int ox = 2 * cx + px;
+            if (ox >= p.OW) continue;
+            const int dx = ix[px] - x0;
+            float acc[V];
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[j] = 0.f;
+            // taps (ty + 2 a, tx + 2 b) on inputs (iy + a, ix + b), a, b in {0, 1}, in upfirdn_nhwc_vec's order
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const int t1 = ty[py] + 2 * a;
+                if (t1 >= 4) continue;
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const int t2 = tx[px] + 2 * b;
+                    if (t2 >= 4) continue;
+                    const float w = sf[t1 * 4 + t2];
+                    const vecT v = dy ? (dx ? xv[1 + a][1 + b] : xv[1 + a][b]) : (dx ? xv[a][1 + b] : xv[a][b]);
+#pragma unroll
+                    for (int j = 0; j < V; ++j) acc[j] += (float)v[j] * w;
+                }
+            }
+            store_out<T, V, vecT>(p, (T*)p.y, acc, n, oy, ox, cv);
+        }
     }
 }
 
@@ -498,6 +575,14 @@ int launch(const UpfParams& p, bool vec, hipStream_t s) {
             return launch_status("sg2_upfirdn2d");
         }
     }
+    if (vec && p.upx == 2 && p.upy == 2 && p.downx == 1 && p.downy == 1 && p.fw == 4 && p.fh == 4 &&
+        !getenv("SG2_UPF_UP2_OFF")) {
+        const int64_t cells = (int64_t)p.N * ((p.OH + 1) / 2) * ((p.OW + 1) / 2) * (p.C / VecN<T>::N);
+        if (cells < INT32_MAX - 256) {
+            upfirdn_nhwc_up2<T><<<(unsigned)cdiv(cells, 256), 256, 0, s>>>(p);
+            return launch_status("sg2_upfirdn2d");
+        }
+    }
     if (!vec && !p.epi) {
         const bool horiz = p.fh == 1 && p.upy == 1 && p.downy == 1 && p.pady0 == 0 && p.OH == p.H && p.fw <= 64;
         const bool vert = p.fw == 1 && p.upx == 1 && p.downx == 1 && p.padx0 == 0 && p.OW == p.W && p.fh <= 64;
@@ -515,8 +600,10 @@ int launch(const UpfParams& p, bool vec, hipStream_t s) {
     }
     const int64_t work = vec ? (int64_t)p.N * p.OH * p.OW * (p.C / VecN<T>::N) : (int64_t)p.N * p.C * p.OH * p.OW;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(work, 256), 256 * 32));
-    if (vec)
-        upfirdn_nhwc_vec<T><<<grid, 256, 0, s>>>(p);
+    if (vec && work < INT32_MAX && (int64_t)grid * 256 < INT32_MAX)
+        upfirdn_nhwc_vec<T, unsigned><<<grid, 256, 0, s>>>(p);
+    else if (vec)
+        upfirdn_nhwc_vec<T, int64_t><<<grid, 256, 0, s>>>(p);
     else
         upfirdn_generic<T><<<grid, 256, 0, s>>>(p);
     return launch_status("sg2_upfirdn2d");

@@ -112,11 +112,12 @@ def test_upfirdn2d_vec_path(dtype):
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
-def test_upfirdn2d_up2_blocks(dtype):
-    """2x up-FIR on channels-last feature maps (upfirdn_nhwc_vec; the adjoint of the D skip's FIR-down-2):
-    even / odd / asymmetric / zero padding, odd output sizes, flipped and asymmetric filters, vs the
-    oracle.  (A 2 x 2-output-block kernel for this case passed this test but measured 1.8x slower than the
-    per-output kernel: profiles/r02_v9_fir_up2_ab.log.)"""
+def test_upfirdn2d_up2_blocks(dtype, monkeypatch):
+    """2x up-FIR on channels-last feature maps (upfirdn_nhwc_up2, a 2 x 2 output cell per lane; the adjoint of
+    the D skip's FIR-down-2): even / odd / asymmetric / zero padding, odd output sizes, flipped and asymmetric
+    filters, vs the oracle, and bitwise against the per-output kernel it replaced (upfirdn_nhwc_vec,
+    SG2_UPF_UP2_OFF=1; same taps in the same order).  (Round 2's LDS-staged 2 x 2-block kernel measured 1.8x
+    slower, profiles/r02_v9_fir_up2_ab.log; this register form is 1.5-1.7x faster, profiles/r04_v4_upf_up2_ab.log.)"""
     from torch_utils.ops import upfirdn2d
     torch.manual_seed(5)
     tol = {torch.float32: 1e-5, torch.float16: 2e-3, torch.bfloat16: 1e-2}[dtype]
@@ -131,6 +132,10 @@ def test_upfirdn2d_up2_blocks(dtype):
                     r = O.upfirdn2d(x, f, up=2, padding=pad, flip_filter=flip, gain=4)
                     assert y.shape == r.shape
                     assert rel_err(y.float(), r) < tol, (fk, n, c, h, w, pad, flip)
+                    monkeypatch.setenv('SG2_UPF_UP2_OFF', '1')
+                    y2 = upfirdn2d.upfirdn2d(xd, f.to(DEV), up=2, padding=pad, flip_filter=flip, gain=4)
+                    monkeypatch.delenv('SG2_UPF_UP2_OFF')
+                    assert torch.equal(y, y2), (fk, n, c, h, w, pad, flip)
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
