@@ -235,6 +235,19 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_vec(UpfParams p) {
     }
 }
 
+// f16 operand (low / high half of a packed pair) times an f32 weight plus an f32 accumulator in one
+// v_fma_mix_f32: the exact f16 -> f32 conversion and a single-rounding FMA, bitwise what cvt + fma give.
+__device__ __forceinline__ float fma_mix_lo(unsigned h2, float w, float acc) {
+    float r;
+    asm volatile("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h2), "v"(w), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ float fma_mix_hi(unsigned h2, float w, float acc) {
+    float r;
+    asm volatile("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h2), "v"(w), "v"(acc));
+    return r;
+}
+
 // 4x4 filter, up = 2, down = 1 on both axes, channels-last (the adjoint of every down-2 FIR: the D skips'
 // input gradients; upsample2d): a lane owns one channel vector of a 2 x 2 output cell (2 cy + py, 2 cx + px).
 // Each output reads 2 x 2 input pixels and the cell's four outputs read inside one 3 x 3 neighbourhood,
@@ -300,8 +313,18 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_up2(UpfParams p) {
                     if (t2 >= 4) continue;
                     const float w = sf[t1 * 4 + t2];
                     const vecT v = dy ? (dx ? xv[1 + a][1 + b] : xv[1 + a][b]) : (dx ? xv[a][1 + b] : xv[a][b]);
+                    if constexpr (std::is_same<T, f16_t>::value) {
+                        typedef unsigned u32v __attribute__((ext_vector_type(V / 2)));
+                        const u32v u = __builtin_bit_cast(u32v, v);
 #pragma unroll
-                    for (int j = 0; j < V; ++j) acc[j] += (float)v[j] * w;
+                        for (int q = 0; q < V / 2; ++q) {
+                            acc[2 * q] = fma_mix_lo(u[q], w, acc[2 * q]);
+                            acc[2 * q + 1] = fma_mix_hi(u[q], w, acc[2 * q + 1]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < V; ++j) acc[j] += (float)v[j] * w;
+                    }
                 }
             }
             store_out<T, V, vecT>(p, (T*)p.y, acc, n, oy, ox, cv);
@@ -369,8 +392,18 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_f4(UpfParams p) {
             for (int kx = 0; kx < F; ++kx) {
                 const float w = sf[ky * F + kx];
                 const vecT v = base[(ky * IW + kx) * CG];
+                if constexpr (std::is_same<T, f16_t>::value) {   // conversion + FMA in one v_fma_mix_f32
+                    typedef unsigned u32v __attribute__((ext_vector_type(V / 2)));
+                    const u32v u = __builtin_bit_cast(u32v, v);
 #pragma unroll
-                for (int j = 0; j < V; ++j) acc[j] += (float)v[j] * w;
+                    for (int q = 0; q < V / 2; ++q) {
+                        acc[2 * q] = fma_mix_lo(u[q], w, acc[2 * q]);
+                        acc[2 * q + 1] = fma_mix_hi(u[q], w, acc[2 * q + 1]);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < V; ++j) acc[j] += (float)v[j] * w;
+                }
             }
         store_out<T, V, vecT>(p, (T*)p.y, acc, n, oy, ox, cv0 + c);
     }
@@ -382,8 +415,11 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_f4(UpfParams p) {
 // is branch-free apart from the uniform noise/residual/aux pointer tests.
 // SEP: the 4x4 taps are an exact outer product wf[ky][kx] = fy[ky] * fx[kx] (the [1,3,3,1] resample
 // filter): every input row is filtered horizontally once (4 FMAs) and the output rows combine those
-// row sums vertically (4 FMAs), 9.5 FMAs per output vector instead of 16.
-template <typename T, int V, typename vecT, int TW, int TH, int CG, bool SEP>
+// row sums vertically (4 FMAs), 9.5 FMAs per output vector instead of 16.  For fp16 the horizontal FMAs
+// take their operand straight from the packed halves (v_fma_mix_f32: the exact f16 -> f32 conversion and
+// the FMA in one instruction, where cvt + v_pk_fma_f32 costs 1.5 per tap and element).
+// EPI = false (no layer epilogue): the rounded FIR sum is stored as is, none of the epilogue arithmetic runs.
+template <typename T, int V, typename vecT, int TW, int TH, int CG, bool SEP, bool EPI>
 __device__ __forceinline__ void fir4_strip(const UpfParams& p, const vecT* base, const float* wf, const float* fy,
                                            const float* fx, int n, int ty0, int ox, int cv) {
     constexpr int F = 4, IW = TW + F - 1, IH = TH + F - 1;
@@ -412,11 +448,26 @@ __device__ __forceinline__ void fir4_strip(const UpfParams& p, const vecT* base,
         for (int kx = 0; kx < F; ++kx) v[kx] = base[(ry * IW + kx) * CG];
         if constexpr (SEP) {
             float h[V];
+            if constexpr (std::is_same<T, f16_t>::value) {
+                typedef unsigned u32v __attribute__((ext_vector_type(V / 2)));
 #pragma unroll
-            for (int j = 0; j < V; ++j) {
-                h[j] = 0.f;
+                for (int j = 0; j < V; ++j) h[j] = 0.f;
 #pragma unroll
-                for (int kx = 0; kx < F; ++kx) h[j] += (float)v[kx][j] * fx[kx];
+                for (int kx = 0; kx < F; ++kx) {
+                    const u32v u = __builtin_bit_cast(u32v, v[kx]);
+#pragma unroll
+                    for (int q = 0; q < V / 2; ++q) {
+                        h[2 * q] = fma_mix_lo(u[q], fx[kx], h[2 * q]);
+                        h[2 * q + 1] = fma_mix_hi(u[q], fx[kx], h[2 * q + 1]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    h[j] = 0.f;
+#pragma unroll
+                    for (int kx = 0; kx < F; ++kx) h[j] += (float)v[kx][j] * fx[kx];
+                }
             }
 #pragma unroll
             for (int ky = 0; ky < F; ++ky) {
@@ -440,6 +491,14 @@ __device__ __forceinline__ void fir4_strip(const UpfParams& p, const vecT* base,
         if (od < 0) continue;
         const int oy = ty0 + od;
         const int64_t dst = n * p.ys_n + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w + cv * V;
+        if constexpr (!EPI) {
+            vecT o;
+#pragma unroll
+            for (int j = 0; j < V; ++j) o[j] = (T)acc[od][j];
+            *(vecT*)((T*)p.y + dst) = o;
+            __builtin_amdgcn_sched_barrier(0);
+            continue;
+        }
         const float nv = noise ? (float)((const T*)p.noise)[((int64_t)n * p.OH + oy) * p.OW + ox] * p.noise_gain : 0.f;
         vecT o, ax;
 #pragma unroll
@@ -529,10 +588,14 @@ __global__ __launch_bounds__(256, 2) void upfirdn_nhwc_f4s(UpfParams p) {
     }
 #pragma unroll
     for (int t = 0; t < F * F; ++t) sep = sep && (fy[t / F] * fx[t % F] == wf[t]);
-    if (sep)
-        fir4_strip<T, V, vecT, TW, TH, CG, true>(p, tile + col * CG + c, wf, fy, fx, n, ty0, tx0 + col, cv0 + c);
-    else
-        fir4_strip<T, V, vecT, TW, TH, CG, false>(p, tile + col * CG + c, wf, fy, fx, n, ty0, tx0 + col, cv0 + c);
+    const vecT* tb = tile + col * CG + c;
+    if (sep) {
+        if (p.epi) fir4_strip<T, V, vecT, TW, TH, CG, true, true>(p, tb, wf, fy, fx, n, ty0, tx0 + col, cv0 + c);
+        else fir4_strip<T, V, vecT, TW, TH, CG, true, false>(p, tb, wf, fy, fx, n, ty0, tx0 + col, cv0 + c);
+    } else {
+        if (p.epi) fir4_strip<T, V, vecT, TW, TH, CG, false, true>(p, tb, wf, fy, fx, n, ty0, tx0 + col, cv0 + c);
+        else fir4_strip<T, V, vecT, TW, TH, CG, false, false>(p, tb, wf, fy, fx, n, ty0, tx0 + col, cv0 + c);
+    }
 }
 
 template <typename T>
