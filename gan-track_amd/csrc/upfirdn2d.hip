@@ -47,6 +47,7 @@ struct UpfParams {
     // written as zeros (their exact value: the image's support ends inside the extent), the rest of the
     // static buffer is left untouched -- no consumer reads it.  Generic kernel only.
     const int* lim;
+    int xcd;                  // f4 kernel: XCD-contiguous block order (default on)
 };
 
 constexpr int kZeroBand = 32;
@@ -356,6 +357,11 @@ __global__ __launch_bounds__(256) void upfirdn_nhwc_f4(UpfParams p) {
     const int ngroups = (CV + CG - 1) / CG;
     const int tiles_x = (p.OW + TW - 1) / TW, tiles_y = (p.OH + TH - 1) / TH;
     int64_t b = blockIdx.x;
+    // XCD-contiguous renumbering (SG2_FIR_XCD=0 disables, for A/B): workgroups are dealt to the 8 XCDs round
+    // robin, so without it the channel groups of one tile -- which split each pixel's cache lines -- and
+    // neighbouring tiles -- which share halo rows -- land in different L2s
+    const int64_t nb = gridDim.x;
+    if ((nb & 7) == 0 && p.xcd) b = (b & 7) * (nb >> 3) + (b >> 3);
     const int cg = (int)(b % ngroups); b /= ngroups;
     const int tx0 = (int)(b % tiles_x) * TW; b /= tiles_x;
     const int ty0 = (int)(b % tiles_y) * TH; b /= tiles_y;
@@ -698,6 +704,7 @@ extern "C" int sg2_upfirdn2d_fused(void* y, const void* x, const float* f, int d
     p.ys_n = out_stride[0]; p.ys_c = out_stride[1]; p.ys_h = out_stride[2]; p.ys_w = out_stride[3];
     p.fw = fw; p.fh = fh; p.upx = upx; p.upy = upy; p.downx = downx; p.downy = downy;
     p.padx0 = padx0; p.pady0 = pady0; p.flip = flip; p.gain = gain; p.lim = nullptr;
+    { const char* e = getenv("SG2_FIR_XCD"); p.xcd = e ? atoi(e) : 1; }
     p.out_scale = nullptr; p.noise = nullptr; p.bias = nullptr; p.residual = nullptr; p.aux = nullptr;
     p.noise_gain = 0.f; p.alpha = 0.f; p.egain = 1.f; p.clamp = -1.f; p.act = 0; p.aux_mode = 0; p.epi = 0;
     if (epi) {
