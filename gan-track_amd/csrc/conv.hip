@@ -267,9 +267,10 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
     const bool clamp_on = on && a.e.clamp >= 0.f;
     const float cl = a.e.clamp;
     const int aux_mode = on ? a.e.aux_mode : 0;
+    const bool i32 = total + (int64_t)gridDim.x * 256 < INT32_MAX;   // 32-bit divisions when they fit
     for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-        const int64_t pix = idx / OG;
-        const int n = (int)(pix / HW);
+        const int64_t pix = i32 ? (int64_t)((unsigned)idx / (unsigned)OG) : idx / OG;
+        const int n = i32 ? (int)((unsigned)pix / (unsigned)HW) : (int)(pix / HW);
         float xv[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -396,8 +397,9 @@ __global__ __launch_bounds__(256) void conv1x1_smallo_kernel(ConvArgs a) {
     const T* x = (const T*)a.x;
     const T* w = (const T*)a.w;
     const bool on = a.e.on;
+    const bool i32 = npix < INT32_MAX;   // 32-bit division when it fits (the 64-bit one is ~40 instructions)
     for (int64_t pix = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3; pix < npix; pix += (int64_t)gridDim.x * 32) {
-        const int n = (int)(pix / HW);
+        const int n = i32 ? (int)((unsigned)pix / (unsigned)HW) : (int)(pix / HW);
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
         for (int ch = g; ch < NCH; ch += 8) {
             vec8 v = *(const vec8*)(x + pix * a.Cin + ch * 8);
@@ -1007,59 +1009,91 @@ __global__ __launch_bounds__(256) void wgrad1x1_smallb_kernel(WgradArgs a) {
 }
 
 // Mirror for a tiny output depth (A <= 4, toRGB): the lane owns 8 input channels b of the wide x.
-template <typename T>
+// AT: A as a compile-time count (1..4; the toRGB weight gradient has A = img_channels), so a pixel costs A FMAs
+// per element rather than four; IDX: unsigned 32-bit index math when M * B / 8 < 2^31 (the host checks) --
+// the 64-bit divisions that split the flat index into (pixel, sample) cost more than the FMAs.
+template <typename T, int AT, typename IDX>
 __global__ __launch_bounds__(256) void wgrad1x1_smalla_kernel(WgradArgs a) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
     __shared__ float red[2048];                       // [A][B], A * B <= 2048
-    const int BG = a.B / 8;
-    for (int i = threadIdx.x; i < a.A * a.B; i += 256) red[i] = 0.f;
+    const IDX BG = (IDX)(a.B / 8);
+    for (int i = threadIdx.x; i < AT * a.B; i += 256) red[i] = 0.f;
     __syncthreads();
-    const int64_t total = (int64_t)a.M * BG;
-    const int per = a.OH * a.OW;
+    const IDX total = (IDX)((int64_t)a.M * (a.B / 8));
+    const IDX per = (IDX)(a.OH * a.OW);
     const T* g = (const T*)a.g;
     const T* x = (const T*)a.x;
-    int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    IDX idx = (IDX)blockIdx.x * 256 + threadIdx.x;
     const int b0 = (int)(idx % BG) * 8;
-    float acc[4][8];
+    float acc[AT][8];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < AT; ++k)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
-    for (; idx < total; idx += (int64_t)gridDim.x * 256) {
-        const int64_t pix = idx / BG;
+    // U pixels per trip with all their loads issued first (one 16-byte load in flight per lane left the
+    // kernel latency-bound at ~1.4 TB/s); the accumulation order is the plain loop's
+    constexpr int U = 4;
+    const IDX stride = (IDX)gridDim.x * 256;
+    // the x operand's modulation row b_scale[n, b0 .. b0 + 7] is re-read only when the sample changes
+    int cur_n = -1;
+    float bs[8];
+    auto body = [&](const vec8& xv, const float* graw, IDX pix) {
         const int n = (int)(pix / per);
-        const vec8 xv = *(const vec8*)(x + pix * a.B + b0);
-        float gk[4];
+        if (a.b_scale && n != cur_n) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float v = k < a.A ? (float)g[pix * a.A + k] : 0.f;
-            if (a.a_scale && k < a.A) v = (float)(T)(v * a.a_scale[(int64_t)n * a.A + k]);
+            for (int j = 0; j < 8; ++j) bs[j] = a.b_scale[(int64_t)n * a.B + b0 + j];
+            cur_n = n;
+        }
+        float gk[AT];
+#pragma unroll
+        for (int k = 0; k < AT; ++k) {
+            float v = graw[k];
+            if (a.a_scale) v = (float)(T)(v * a.a_scale[(int64_t)n * AT + k]);
             gk[k] = v;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             float xj = (float)xv[j];
-            if (a.b_scale) xj = (float)(T)(xj * a.b_scale[(int64_t)n * a.B + b0 + j]);
+            if (a.b_scale) xj = (float)(T)(xj * bs[j]);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) acc[k][j] += gk[k] * xj;
+            for (int k = 0; k < AT; ++k) acc[k][j] += gk[k] * xj;
         }
+    };
+    for (; idx + (U - 1) * stride < total; idx += U * stride) {
+        vec8 xv[U];
+        float gr[U][AT];
+        IDX pix[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            pix[u] = (idx + u * stride) / BG;
+            xv[u] = *(const vec8*)(x + (int64_t)pix[u] * a.B + b0);
+#pragma unroll
+            for (int k = 0; k < AT; ++k) gr[u][k] = (float)g[(int64_t)pix[u] * AT + k];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) body(xv[u], gr[u], pix[u]);
+    }
+    for (; idx < total; idx += stride) {
+        const IDX pix = idx / BG;
+        float gr[AT];
+#pragma unroll
+        for (int k = 0; k < AT; ++k) gr[k] = (float)g[(int64_t)pix * AT + k];
+        body(*(const vec8*)(x + (int64_t)pix * a.B + b0), gr, pix);
     }
     if (a.det) {
-        const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / BG;
+        const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / (a.B / 8);
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < AT; ++k)
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (k < a.A) a.det[row * a.A * a.B + k * a.B + b0 + j] = acc[k][j] * a.alpha;
+            for (int j = 0; j < 8; ++j) a.det[row * AT * a.B + k * a.B + b0 + j] = acc[k][j] * a.alpha;
         return;
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < AT; ++k)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (k < a.A) atomicAdd(&red[k * a.B + b0 + j], acc[k][j]);
+        for (int j = 0; j < 8; ++j) atomicAdd(&red[k * a.B + b0 + j], acc[k][j]);
     __syncthreads();
-    for (int i = threadIdx.x; i < a.A * a.B; i += 256) atomicAdd(a.dw + i, red[i] * a.alpha);
+    for (int i = threadIdx.x; i < AT * a.B; i += 256) atomicAdd(a.dw + i, red[i] * a.alpha);
 }
 
 template <typename T, int BM, int BN, bool VEC, bool S3, bool P3 = false>
@@ -1668,7 +1702,11 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
         DetArena arena;
         const int64_t rows = (int64_t)g_ * 256 / (B / 8);
         if (det_on()) SG2_DET_GET(a.det, arena, rows * A * B, "sg2_conv2d_wgrad (1x1, small A)");
-        SG2_DISPATCH(dtype, T, { wgrad1x1_smalla_kernel<T><<<g_, 256, 0, s>>>(a); });
+        const bool i32 = (int64_t)a.M * (B / 8) + (int64_t)g_ * 256 < INT32_MAX && !getenv("SG2_WG1_OLD");
+#define WG1(AT_) { if (i32) wgrad1x1_smalla_kernel<T, AT_, unsigned><<<g_, 256, 0, s>>>(a); \
+                   else wgrad1x1_smalla_kernel<T, AT_, int64_t><<<g_, 256, 0, s>>>(a); }
+        SG2_DISPATCH(dtype, T, { if (A == 1) WG1(1) else if (A == 2) WG1(2) else if (A == 3) WG1(3) else WG1(4) });
+#undef WG1
         int rc1 = launch_status("sg2_conv2d_wgrad (1x1, small A)");
         if (rc1 || !a.det) return rc1;
         e = det_sum(dw, 0, a.det, 0, (int64_t)A * B, 1, rows, (int64_t)A * B, arena, s);
