@@ -952,60 +952,68 @@ __device__ __forceinline__ v8_t<T> frag_tr(const T* base, int ld, int k0, int c0
 // sum_p g[p,a] x[p,b] is a reduction of the A-wide gradient over all pixels, HBM-bound on g.  A lane
 // owns 8 output channels (fixed, as the grid stride is a multiple of A/8) and accumulates over its
 // pixels in registers; the block reduces through LDS and adds once per element to dw (zeroed).
-template <typename T>
+// BT: B as a compile-time count (1..4; the fromRGB weight gradient has B = img_channels); IDX: 32-bit index
+// math when it fits; the g operand's modulation row a_scale[n, a0 .. a0 + 7] is re-read only when the sample
+// changes (re-reading it per pixel doubled the load traffic, as in wgrad1x1_smalla).
+template <typename T, int BT, typename IDX>
 __global__ __launch_bounds__(256) void wgrad1x1_smallb_kernel(WgradArgs a) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
     __shared__ float red[2048];                       // [A][B], A * B <= 2048
-    const int OG = a.A / 8;
-    for (int i = threadIdx.x; i < a.A * a.B; i += 256) red[i] = 0.f;
+    const IDX OG = (IDX)(a.A / 8);
+    for (int i = threadIdx.x; i < a.A * BT; i += 256) red[i] = 0.f;
     __syncthreads();
-    const int64_t total = (int64_t)a.M * OG;
-    const int per = a.OH * a.OW;
+    const IDX total = (IDX)((int64_t)a.M * (a.A / 8));
+    const IDX per = (IDX)(a.OH * a.OW);
     const T* g = (const T*)a.g;
     const T* x = (const T*)a.x;
-    int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    IDX idx = (IDX)blockIdx.x * 256 + threadIdx.x;
     const int a0 = (int)(idx % OG) * 8;
-    float acc[8][4];
+    float acc[8][BT];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) acc[j][k] = 0.f;
-    for (; idx < total; idx += (int64_t)gridDim.x * 256) {
-        const int64_t pix = idx / OG;
+        for (int k = 0; k < BT; ++k) acc[j][k] = 0.f;
+    int cur_n = -1;
+    float as[8];
+    for (; idx < total; idx += (IDX)gridDim.x * 256) {
+        const IDX pix = idx / OG;
         const int n = (int)(pix / per);
-        const vec8 gv = *(const vec8*)(g + pix * a.A + a0);
-        float xv[4];
+        const vec8 gv = *(const vec8*)(g + (int64_t)pix * a.A + a0);
+        float xv[BT];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float v = k < a.B ? (float)x[pix * a.B + k] : 0.f;
-            if (a.b_scale && k < a.B) v = (float)(T)(v * a.b_scale[(int64_t)n * a.B + k]);
+        for (int k = 0; k < BT; ++k) {
+            float v = (float)x[(int64_t)pix * BT + k];
+            if (a.b_scale) v = (float)(T)(v * a.b_scale[(int64_t)n * BT + k]);
             xv[k] = v;
+        }
+        if (a.a_scale && n != cur_n) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) as[j] = a.a_scale[(int64_t)n * a.A + a0 + j];
+            cur_n = n;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             float gj = (float)gv[j];
-            if (a.a_scale) gj = (float)(T)(gj * a.a_scale[(int64_t)n * a.A + a0 + j]);
+            if (a.a_scale) gj = (float)(T)(gj * as[j]);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) acc[j][k] += gj * xv[k];
+            for (int k = 0; k < BT; ++k) acc[j][k] += gj * xv[k];
         }
     }
     if (a.det) {
         // one slot per row of OG lanes (every lane of a row owns 8 distinct a): [row][A][B]
-        const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / OG;
+        const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / (a.A / 8);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < a.B) a.det[row * a.A * a.B + (a0 + j) * a.B + k] = acc[j][k] * a.alpha;
+            for (int k = 0; k < BT; ++k) a.det[row * a.A * BT + (a0 + j) * BT + k] = acc[j][k] * a.alpha;
         return;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (k < a.B) atomicAdd(&red[(a0 + j) * a.B + k], acc[j][k]);
+        for (int k = 0; k < BT; ++k) atomicAdd(&red[(a0 + j) * BT + k], acc[j][k]);
     __syncthreads();
-    for (int i = threadIdx.x; i < a.A * a.B; i += 256) atomicAdd(a.dw + i, red[i] * a.alpha);
+    for (int i = threadIdx.x; i < a.A * BT; i += 256) atomicAdd(a.dw + i, red[i] * a.alpha);
 }
 
 // Mirror for a tiny output depth (A <= 4, toRGB): the lane owns 8 input channels b of the wide x.
@@ -1689,7 +1697,11 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
         DetArena arena;
         const int64_t rows = (int64_t)g_ * 256 / (A / 8);
         if (det_on()) SG2_DET_GET(a.det, arena, rows * A * B, "sg2_conv2d_wgrad (1x1, small B)");
-        SG2_DISPATCH(dtype, T, { wgrad1x1_smallb_kernel<T><<<g_, 256, 0, s>>>(a); });
+        const bool i32 = (int64_t)a.M * (A / 8) + (int64_t)g_ * 256 < INT32_MAX;
+#define WGB(BT_) { if (i32) wgrad1x1_smallb_kernel<T, BT_, unsigned><<<g_, 256, 0, s>>>(a); \
+                   else wgrad1x1_smallb_kernel<T, BT_, int64_t><<<g_, 256, 0, s>>>(a); }
+        SG2_DISPATCH(dtype, T, { if (B == 1) WGB(1) else if (B == 2) WGB(2) else if (B == 3) WGB(3) else WGB(4) });
+#undef WGB
         int rc1 = launch_status("sg2_conv2d_wgrad (1x1, small B)");
         if (rc1 || !a.det) return rc1;
         e = det_sum(dw, 0, a.det, 0, (int64_t)A * B, 1, rows, (int64_t)A * B, arena, s);
@@ -1702,7 +1714,7 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
         DetArena arena;
         const int64_t rows = (int64_t)g_ * 256 / (B / 8);
         if (det_on()) SG2_DET_GET(a.det, arena, rows * A * B, "sg2_conv2d_wgrad (1x1, small A)");
-        const bool i32 = (int64_t)a.M * (B / 8) + (int64_t)g_ * 256 < INT32_MAX && !getenv("SG2_WG1_OLD");
+        const bool i32 = (int64_t)a.M * (B / 8) + (int64_t)g_ * 256 < INT32_MAX;
 #define WG1(AT_) { if (i32) wgrad1x1_smalla_kernel<T, AT_, unsigned><<<g_, 256, 0, s>>>(a); \
                    else wgrad1x1_smalla_kernel<T, AT_, int64_t><<<g_, 256, 0, s>>>(a); }
         SG2_DISPATCH(dtype, T, { if (A == 1) WG1(1) else if (A == 2) WG1(2) else if (A == 3) WG1(3) else WG1(4) });

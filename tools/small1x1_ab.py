@@ -1,6 +1,6 @@
 """Timing of the small-depth 1x1 kernels of the toRGB / fromRGB layers (GPU): conv1x1_smallk (fromRGB,
-Cin = 1), conv1x1_smallo (toRGB, Cout = 1) and wgrad1x1_smalla (toRGB weight gradient, A = 1), at 256^2
-bs32 / bs64, against HBM bytes.  SG2_WG1_OLD=1 selects the 64-bit-index weight-gradient form.
+Cin = 1), conv1x1_smallo (toRGB, Cout = 1), wgrad1x1_smalla (toRGB weight gradient, A = 1) at 256^2
+bs32 / bs64, and wgrad1x1_smallb (fromRGB weight gradient, B = 1), against HBM bytes.
 Usage: python tools/small1x1_ab.py"""
 import os
 import sys
@@ -38,7 +38,8 @@ for n in (32, 64):
     t_k = timeit(lambda: cg.conv_fused(img, w_from, c, h, h, 1, 1, 1, (0, 0), bias=torch.zeros(c, device=dev), act=1,
                                        gain=2 ** 0.5, aux_mode=1))
     t_w = timeit(lambda: cg._wgrad_raw(img, x, 1, 1, 1, (0, 0), x_scale=s))
+    t_b = timeit(lambda: cg._wgrad_raw(x, img, 1, 1, 1, (0, 0)))
     bx = x.numel() * 2
     print(f'N={n}: toRGB conv {t_o:.4f} ms ({bx / t_o / 1e6:.0f} GB/s) | fromRGB conv {t_k:.4f} ms '
-          f'({(2 * bx + img.numel() * 2) / t_k / 1e6:.0f} GB/s) | toRGB wgrad {t_w:.4f} ms ({bx / t_w / 1e6:.0f} GB/s)',
-          flush=True)
+          f'({(2 * bx + img.numel() * 2) / t_k / 1e6:.0f} GB/s) | toRGB wgrad {t_w:.4f} ms ({bx / t_w / 1e6:.0f} GB/s)'
+          f' | fromRGB wgrad {t_b:.4f} ms ({bx / t_b / 1e6:.0f} GB/s)', flush=True)
