@@ -247,7 +247,8 @@ __device__ __forceinline__ float epi_full(const Epi& e, float c, int n, int o, i
 // product, HBM-bound on the Cout-wide output, so no GEMM tiling -- a lane owns one pixel x 8 output
 // channels, reads Cin inputs and 8 x Cin weights, applies the fused epilogue and writes 16 / 32 bytes.
 // Same operand rounding as conv_fwd_kernel (x * in_scale rounded to T before the product).
-template <typename T>
+// CK: Cin as a compile-time count (1..4; fromRGB has Cin = img_channels): CK FMAs per output, not four
+template <typename T, int CK>
 __global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
     const int OG = a.Cout / 8, HW = a.H * a.W;      // the host guarantees 256 % OG == 0: o0 is fixed per lane
@@ -255,11 +256,11 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
     const T* x = (const T*)a.x;
     const T* w = (const T*)a.w;
     const int o0 = (int)(((int64_t)blockIdx.x * 256 + threadIdx.x) % OG) * 8;
-    float wv[8][4], bj[8];
+    float wv[8][CK], bj[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) wv[j][k] = k < a.Cin ? (float)w[(o0 + j) * a.Cin + k] : 0.f;
+        for (int k = 0; k < CK; ++k) wv[j][k] = (float)w[(o0 + j) * CK + k];
         bj[j] = (a.e.on && a.e.bias) ? (float)(T)a.e.bias[o0 + j] : 0.f;
     }
     const bool on = a.e.on;
@@ -271,11 +272,11 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
     for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
         const int64_t pix = i32 ? (int64_t)((unsigned)idx / (unsigned)OG) : idx / OG;
         const int n = i32 ? (int)((unsigned)pix / (unsigned)HW) : (int)(pix / HW);
-        float xv[4];
+        float xv[CK];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            float v = c < a.Cin ? (float)x[pix * a.Cin + c] : 0.f;
-            if (a.in_scale && c < a.Cin) v = (float)(T)(v * a.in_scale[(int64_t)n * a.Cin + c]);
+        for (int c = 0; c < CK; ++c) {
+            float v = (float)x[pix * CK + c];
+            if (a.in_scale) v = (float)(T)(v * a.in_scale[(int64_t)n * CK + c]);
             xv[c] = v;
         }
         const float nv = (on && a.e.noise) ? (float)((const T*)a.e.noise)[pix] * a.e.noise_gain : 0.f;
@@ -286,7 +287,7 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
         for (int j = 0; j < 8; ++j) {
             float c = 0.f;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) c += xv[k] * wv[j][k];
+            for (int k = 0; k < CK; ++k) c += xv[k] * wv[j][k];
             float v = c;
             if (on && a.e.out_scale) v *= a.e.out_scale[(int64_t)n * a.Cout + o0 + j];
             v = v + nv + bj[j];                       // epi_full order: scale, noise, bias, act, gain, clamp
@@ -1565,7 +1566,12 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
         }
         const int64_t total = (int64_t)N * H * W * (Cout / 8);
         const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 64);
-        SG2_DISPATCH(dtype, T, { conv1x1_smallk_kernel<T><<<g, 256, 0, s>>>(base); });
+        SG2_DISPATCH(dtype, T, {
+            if (Cin == 1) conv1x1_smallk_kernel<T, 1><<<g, 256, 0, s>>>(base);
+            else if (Cin == 2) conv1x1_smallk_kernel<T, 2><<<g, 256, 0, s>>>(base);
+            else if (Cin == 3) conv1x1_smallk_kernel<T, 3><<<g, 256, 0, s>>>(base);
+            else conv1x1_smallk_kernel<T, 4><<<g, 256, 0, s>>>(base);
+        });
         return launch_status("sg2_conv2d (1x1, small Cin)");
     }
     SG2_DISPATCH(dtype, T, {
