@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_kernel(ConvArgs a) {
 // channels' products in registers, the workgroup combines them in LDS and adds Cout floats to dot_out
 // (instead of the implicit GEMM padding K = Cin to 32 and reducing through per-element atomics).
 constexpr int SK_ITERS = 16;
-template <typename T>
+template <typename T, int CK>   // CK = Cin (1..4), as in conv1x1_smallk
 __global__ __launch_bounds__(256) void conv1x1_smallk_dot_kernel(ConvArgs a) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
     __shared__ float red[2048];
@@ -317,11 +317,11 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_dot_kernel(ConvArgs a) {
     const T* x = (const T*)a.x;
     const T* w = (const T*)a.w;
     const int o0 = (threadIdx.x % OG) * 8;
-    float wv[8][4], bj[8], dacc[8];
+    float wv[8][CK], bj[8], dacc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) wv[j][k] = k < a.Cin ? (float)w[(o0 + j) * a.Cin + k] : 0.f;
+        for (int k = 0; k < CK; ++k) wv[j][k] = (float)w[(o0 + j) * CK + k];
         bj[j] = (a.e.on && a.e.bias) ? (float)(T)a.e.bias[o0 + j] : 0.f;
         dacc[j] = 0.f;
     }
@@ -331,9 +331,9 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_dot_kernel(ConvArgs a) {
     const bool clamp_on = on && a.e.clamp >= 0.f;
     const float cl = a.e.clamp;
     const int aux_mode = on ? a.e.aux_mode : 0;
-    float isc[4], osc[8];
+    float isc[CK], osc[8];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) isc[c] = (a.in_scale && c < a.Cin) ? a.in_scale[(int64_t)n * a.Cin + c] : 1.f;
+    for (int c = 0; c < CK; ++c) isc[c] = a.in_scale ? a.in_scale[(int64_t)n * CK + c] : 1.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) osc[j] = (on && a.e.out_scale) ? a.e.out_scale[(int64_t)n * a.Cout + o0 + j] : 1.f;
     const int p_begin = blockIdx.x * SK_ITERS * PPI;
@@ -342,11 +342,11 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_dot_kernel(ConvArgs a) {
         const int p = p_begin + it * PPI + threadIdx.x / OG;
         if (p >= HW) break;
         const int64_t pix = (int64_t)n * HW + p;
-        float xv[4];
+        float xv[CK];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            float v = c < a.Cin ? (float)x[pix * a.Cin + c] : 0.f;
-            if (a.in_scale && c < a.Cin) v = (float)(T)(v * isc[c]);
+        for (int c = 0; c < CK; ++c) {
+            float v = (float)x[pix * CK + c];
+            if (a.in_scale) v = (float)(T)(v * isc[c]);
             xv[c] = v;
         }
         const float nv = (on && a.e.noise) ? (float)((const T*)a.e.noise)[pix] * a.e.noise_gain : 0.f;
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256) void conv1x1_smallk_dot_kernel(ConvArgs a) {
         for (int j = 0; j < 8; ++j) {
             float c = 0.f;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) c += xv[k] * wv[j][k];
+            for (int k = 0; k < CK; ++k) c += xv[k] * wv[j][k];
             dacc[j] += (float)(T)c * (float)ds[j];
             float v = c * osc[j];
             v = v + nv + bj[j];
@@ -1556,7 +1556,12 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
             dim3 g((unsigned)cdiv((int64_t)H * W, ppb), (unsigned)N);
             DetArena arena;
             if (det_on()) SG2_DET_GET(base.e.det_dot, arena, (int64_t)g.x * N * Cout, "sg2_conv2d (1x1, small Cin, dot)");
-            SG2_DISPATCH(dtype, T, { conv1x1_smallk_dot_kernel<T><<<g, 256, 0, s>>>(base); });
+            SG2_DISPATCH(dtype, T, {
+                if (Cin == 1) conv1x1_smallk_dot_kernel<T, 1><<<g, 256, 0, s>>>(base);
+                else if (Cin == 2) conv1x1_smallk_dot_kernel<T, 2><<<g, 256, 0, s>>>(base);
+                else if (Cin == 3) conv1x1_smallk_dot_kernel<T, 3><<<g, 256, 0, s>>>(base);
+                else conv1x1_smallk_dot_kernel<T, 4><<<g, 256, 0, s>>>(base);
+            });
             int rc1 = launch_status("sg2_conv2d (1x1, small Cin, dot)");
             if (rc1 || !base.e.det_dot) return rc1;
             hipError_t e = det_sum(base.e.dot_out, 0, base.e.det_dot, 0, (int64_t)N * Cout, 1, g.x, (int64_t)N * Cout,
