@@ -16,8 +16,10 @@ on the device each iteration, random one-hot labels; networks randomly initialis
 A "step" = one training iteration with the reference's phase schedule (Gmain + Dmain every step,
 Greg every 4th, Dreg every 16th, gradient all-reduce, Adam, EMA, ADA); the phase counter is reset
 at the start of the timed region, so K steps contain the schedule's phases as they fall from step 0:
-K = 16 is exactly one cycle (4 Greg, 1 Dreg); K = 20 has 5 Greg and 2 Dreg (10 % Dreg steps against the
-schedule's 6.25 %, so a 20-step value is slightly pessimistic).
+K = 16 is exactly one cycle (4 Greg, 1 Dreg); the default K = 112 is seven whole cycles (>= 100 timed
+iterations covering whole 16-iteration cycles, ~5 s timed).  A K that is not a multiple of 16 carries a partial cycle:
+K = 20 has 5 Greg and 2 Dreg (10 % Dreg steps against the schedule's 6.25 %, so a 20-step value is slightly
+pessimistic).
 value = images processed by all ranks / max-over-ranks wall time of the K timed steps.
 
 Extra fields: `roofline` for the dominant kernel (the MFMA implicit-GEMM convolution of the 256^2
@@ -46,8 +48,8 @@ HBM_PEAK = 8000.0         # GB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=16)
-    ap.add_argument('--warmup', type=int, default=4)
+    ap.add_argument('--steps', type=int, default=112)
+    ap.add_argument('--warmup', type=int, default=8)
     ap.add_argument('--res', type=int, default=256)
     ap.add_argument('--batch-gpu', type=int, default=32)
     ap.add_argument('--cbase', type=int, default=16384)
@@ -235,6 +237,143 @@ def roofline(device, res, cbase, dtype, N=32):
     return out
 
 
+def exchange_diagnostics(tr, args, device, real, real_c, world):
+    """After the timed region, at N > 1: one eager 16-step cycle with HIP events per phase (Trainer.exchange_timing)
+    -> per phase the flat gradient bytes all-reduced, the bucket count, the forward + backward time and the exposed
+    exchange time (backward issued -> every bucket's all_reduce complete, on the compute stream): what the
+    bucketed, hook-overlapped RCCL exchange did not hide behind the backward (reference exchange:
+    training_loop_mi_multimodal.py:341-351).  Also a standalone all_reduce of each module's flat buffer (the
+    unhidden cost for comparison)."""
+    graphs = tr.graphs
+    tr.graphs = False
+    tr.exchange_timing = {}
+    tr.batch_idx = 0
+    for _ in range(16):
+        one_step(tr, args, device, real, real_c)
+    torch.cuda.synchronize(device)
+    res = {}
+    for ph in tr.phases:
+        evs = tr.exchange_timing.get(ph.name, [])
+        if not evs:
+            continue
+        fb = [a.elapsed_time(b) for a, b, _ in evs]
+        ex = [b.elapsed_time(c) for _, b, c in evs]
+        res[ph.name] = {'allreduce_bytes': int(ph.exchange.total * 4), 'buckets': len(ph.exchange.buckets),
+                        'fwd_bwd_ms': round(float(np.mean(fb)), 3), 'exposed_exchange_ms': round(float(np.mean(ex)), 3),
+                        'steps': len(evs)}
+    for name, ph in (('G', tr.phases[0]), ('D', tr.phases[-1])):
+        flat = ph.exchange.flat
+        if flat is None:
+            continue
+        buf = flat.clone()
+        res[f'standalone_allreduce_{name}_ms'] = round(_time_ms(lambda: torch.distributed.all_reduce(buf), reps=5), 3)
+    tr.exchange_timing = None
+    tr.graphs = graphs
+    return res
+
+
+def _time_ms(fn, reps=20):
+    """Average ms per call of fn (one or more launches on the current stream) with HIP events on that stream."""
+    for _ in range(3):
+        fn()
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def _roof_entry(kernel, shape, ms, flops, byts):
+    """One family's roofline: the binding roof of the launch is min(MFMA peak, AI x HBM peak); frac = achieved rate
+    / that roof, in the roof's unit."""
+    ai = flops / byts if byts else float('inf')
+    tfl = flops / (ms * 1e-3) / 1e12
+    gbps = byts / (ms * 1e-3) / 1e9
+    hbm_bound = ai * HBM_PEAK * 1e9 < MFMA_PEAK_FP16 * 1e12
+    e = {'kernel': kernel, 'shape': shape, 'ms_per_launch': round(ms, 4), 'algorithmic_flops_per_launch': flops,
+         'algorithmic_hbm_bytes_per_launch': byts, 'arithmetic_intensity': round(ai, 1)}
+    if hbm_bound:
+        e.update({'bound': 'hbm', 'achieved': round(gbps, 1), 'peak': HBM_PEAK, 'unit': 'GB/s',
+                  'frac': round(gbps / HBM_PEAK, 4)})
+    else:
+        e.update({'bound': 'mfma', 'achieved': round(tfl, 1), 'peak': MFMA_PEAK_FP16, 'unit': 'TFLOP/s',
+                  'frac': round(tfl / MFMA_PEAK_FP16, 4)})
+    if flops:
+        e['mfma_tflops'] = round(tfl, 1)
+    return e
+
+
+def roofline_families(device, dtype=torch.float16):
+    """Rooflines of the kernel families that dominate the 256^2 step (profiles/r0*_step_breakdown.txt), each on its
+    largest launch of the bench workload, timed with HIP events on the launching stream.  Algorithmic cost per
+    launch: a conv 2 N Cout Cin taps OH OW FLOP and its input + output bytes (weights negligible); the FIR and the
+    fused layer backward their input + output bytes (no FLOP counted: VALU work far under the HBM roof)."""
+    from torch_utils.ops import conv2d_gradfix as cg, upfirdn2d
+    import sg2hip
+    esz = torch.tensor([], dtype=dtype).element_size()
+    cl = torch.channels_last
+    out = {}
+
+    def rnd(*shape):
+        return torch.randn(shape, device=device, dtype=dtype).contiguous(memory_format=cl)
+
+    # generic implicit GEMM (conv_fwd_kernel): the D down-2 conv of the 256^2 block after its FIR (Dmain batch 64)
+    N, Ci, H, Co = 64, 64, 257, 128
+    OH = (H - 3) // 2 + 1
+    x = rnd(N, Ci, H, H)
+    wp = cg._pack_conv((torch.randn(Co, Ci, 3, 3, device=device) / 24).to(dtype))
+    b = torch.zeros(Co, device=device)
+    ms = _time_ms(lambda: cg.conv_fused(x, wp, Co, OH, OH, 3, 3, 2, (0, 0), bias=b, act=1, gain=1.41, clamp=256.0))
+    out['conv_fwd_generic'] = _roof_entry('conv_fwd_kernel (implicit GEMM)', f'D down-2 3x3 N{N} {Ci}x{H}^2 -> {Co}x{OH}^2',
+                                          ms, 2.0 * N * Co * Ci * 9 * OH * OH, (N * Ci * H * H + N * Co * OH * OH) * esz)
+    del x
+    # halo conv: the 128^2 C=128 synthesis layer (G forward, bs32)
+    N, C, R = 32, 128, 128
+    x = rnd(N, C, R, R)
+    wp = cg._pack_conv((torch.randn(C, C, 3, 3, device=device) / 34).to(dtype))
+    s_ = torch.rand(N, C, device=device) + 0.5
+    ms = _time_ms(lambda: cg.conv3x3_fused(x, wp, C, in_scale=s_, out_scale=s_, bias=torch.zeros(C, device=device),
+                                           act=1, gain=1.41, clamp=256.0))
+    out['halo_conv'] = _roof_entry('conv3x3_halo_kernel', f'3x3 s1 N{N} C{C} {R}^2 (modulated, fused epilogue)', ms,
+                                   2.0 * N * C * C * 9 * R * R, 2 * N * C * R * R * esz)
+    # halo weight gradient at the same shape
+    g = rnd(N, C, R, R)
+    ms = _time_ms(lambda: cg._wgrad_raw(g, x, 3, 3, 1, (1, 1)))
+    out['halo_wgrad'] = _roof_entry('wgrad3x3 (LDS-DMA halo)', f'3x3 s1 N{N} C{C}x{C} {R}^2', ms,
+                                    2.0 * N * C * C * 9 * R * R, 2 * N * C * R * R * esz)
+    del x, g
+    # fused synthesis-layer first-order backward (sg2_layer_bwd) on the 256^2 C=64 layer
+    N, C, R = 32, 64, 256
+    dy, y, c = rnd(N, C, R, R), rnd(N, C, R, R), rnd(N, C, R, R)
+    dc = torch.empty_like(dy)
+    d = torch.rand(N, C, device=device) + 0.5
+    db, dd = torch.zeros(C, device=device), torch.zeros(N, C, device=device)
+    dn = torch.zeros(N, R, R, device=device)
+    lib = sg2hip.lib()
+
+    def lbwd():
+        sg2hip.check(lib.sg2_layer_bwd(sg2hip.ptr(dc), sg2hip.ptr(db), sg2hip.ptr(dd), sg2hip.ptr(dn), sg2hip.ptr(dy),
+                                       sg2hip.ptr(y), sg2hip.ptr(c), sg2hip.ptr(d), sg2hip.dtype_code(dy), N, R * R, C, 1, 0.2,
+                                       1.41, 256.0, sg2hip.stream_ptr(device)), 'sg2_layer_bwd')
+    ms = _time_ms(lbwd)
+    out['layer_bwd'] = _roof_entry('layer_bwd_kernel', f'N{N} C{C} {R}^2: dy, y, c in; dc out (+ db, dd, dnoise)', ms,
+                                   0, 4 * N * C * R * R * esz)
+    del dy, y, c, dc
+    # 4x4 FIR, up 1 / down 1 (upfirdn_nhwc_f4s): the D 256^2 pad-FIR before the down-2 conv (256^2 -> 257^2)
+    x = rnd(64, 64, 256, 256)
+    f = upfirdn2d.setup_filter([1, 3, 3, 1], device=device)
+    ms = _time_ms(lambda: upfirdn2d.upfirdn2d(x, f, padding=2))
+    out['fir_f4s'] = _roof_entry('upfirdn_nhwc_f4s', 'N64 C64 256^2 -> 257^2 (pad 2)', ms, 0,
+                                 (64 * 64 * 256 * 256 + 64 * 64 * 257 * 257) * esz)
+    del x
+    weakest = min(out, key=lambda k: out[k]['frac'])
+    out['weakest'] = weakest
+    return out
+
+
 def cpu_baseline(args):
     """CPU oracle (oracle/sg2_oracle.py, the reference's algorithm restated in PyTorch-CPU fp32) timed on
     the host cores: one Gmain, Greg, Dmain and Dreg phase at the bench resolution with batch 4
@@ -338,6 +477,9 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
 
+    exch = None
+    if world > 1:
+        exch = exchange_diagnostics(tr, args, device, real, real_c, world)
     imgs = args.steps * args.batch_gpu * num_gpus
     value = imgs / elapsed
     phase_ms = None
@@ -348,6 +490,9 @@ def main():
     if not args.no_roofline:
         roof = roofline(device, args.res, args.cbase, torch.float16 if args.fp16_dtype == 'fp16' else torch.bfloat16,
                         args.batch_gpu)
+    fams = None
+    if not args.no_roofline and args.res == 256:
+        fams = roofline_families(device, torch.float16 if args.fp16_dtype == 'fp16' else torch.bfloat16)
     cpu = None
     if rank == 0 and num_gpus == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -368,6 +513,7 @@ def main():
             'imgs_per_sec_per_gpu': round(value / num_gpus, 3),
             'sec_per_kimg': round(1000.0 / value, 3),
             'roofline': roof,
+            'roofline_families': fams,
             'cpu_baseline': cpu,
         }
         # what torch.distributed actually initialised (a scaling run can be checked from the line alone), and
@@ -376,6 +522,8 @@ def main():
                         'world_size': torch.distributed.get_world_size() if world > 1 else 1,
                         'buckets': {ph.name: len(ph.exchange.buckets) for ph in tr.phases},
                         'bucket_mb': 32, 'overlapped': num_gpus > 1}
+        if exch is not None:
+            line['dist']['exchange'] = exch
         if phase_ms is not None:
             line['last_phase_ms'] = phase_ms
         print(json.dumps(line), flush=True)

@@ -744,6 +744,21 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
                             //  256: whole-line store addressing with the data misplaced)
 #endif
 
+#if SG2_RDIAG & 512
+// Diagnostic build only (tools/ring_stamps.py): per wave, the summed cycles of each loop phase of the ring kernel
+// from s_memtime stamps (issue DMAs | MFMAs issued | epilogue + stores issued | DMA wait | barrier), the first and
+// last stamp and the hardware wave id, written once at the end by lane 0 (vector stores; nothing in the loop).
+constexpr int RST_WAVES = 4096, RST_F = 8;
+__device__ unsigned long long g_ring_stamps[RST_WAVES * RST_F];
+__device__ __forceinline__ unsigned long long ring_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#endif
+
 __device__ __forceinline__ unsigned lds_addr(const void* p) {    // byte address in LDS of a __shared__ pointer
     return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
 }
@@ -754,7 +769,7 @@ __device__ __forceinline__ void wait_vm() {           // s_waitcnt vmcnt(N) (gfx
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <typename T, bool SI, bool EPI, bool RAW, int R_TH, int WR, bool PIPE, bool STG>
+template <typename T, bool SI, bool EPI, bool RAW, int R_TH, int WR, bool PIPE, int STG>
 __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER_CU)) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
     typedef Ring<R_TH, WR> RG;
@@ -883,6 +898,53 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
         }
     };
 
+    // STG & 4 (TH = 4, 4 waves): the same DMAs with the tile-independent parts of their addresses hoisted out of the
+    // loop and every column group a compile-time constant of the instruction: wave w loads halo row w (column groups
+    // 0..4), then waves 0 / 1 row 4 / 5 column groups 0..2 and waves 2 / 3 row 4 / 5 column groups 3, 4 and the
+    // epilogue table (both: duplicates write the same bytes).  Per DMA: one scalar add for the row base (twice a
+    // tile), one vector add, a select on the border columns only -- where the generic issue above spends ~20
+    // instructions (a runtime division, the row-validity branch and the per-lane kill logic) on each.
+    const int rs_w = a.W * 128;
+    auto issue_fast = [&](int t, int slot, int eslot) {
+        if constexpr (R_TH == 4 && NW == 4) {
+            if (SG2_RDIAG & 16) return;
+            int n, ty, tx;
+            tile_of(t, n, ty, tx);
+            const int base0 = ((n * a.H + ty - 1) * a.W + tx - 1) * 128;     // halo row 0, column -1
+            const int rowA = wave, rowB = 4 + (wave & 1);
+            // an invalid row: every lane out of range (INT_MIN + < 8 KiB stays above any buffer of < 2^31 - 2^16 B)
+            const int bA = (rowA == 0 && ty == 0) ? (int)0x80000000 : base0 + rowA * rs_w;
+            const int bB = (rowB == R_TH + 1 && ty + R_TH == a.H) ? (int)0x80000000 : base0 + rowB * rs_w;
+            const bool killL = (tx == 0) & (lx == 0);
+            const bool killR = (!(SG2_RDIAG & 128) & (lx >= 2)) | ((tx + R_TW == a.W) & (lx == 1));
+            char* sb = smem_raw + slot * R_SLOT;
+            auto dma = [&](int b, int row, int cg) {
+                int off = b + cg * 1024 + hlane;
+                if (cg == 0) off = killL ? -1 : off;
+                if (cg == 4) off = killR ? -1 : off;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rxb, (lds_ptr_t)(sb + (row * 5 + cg) * 1024), 16, off, 0, 0, 0);
+            };
+#pragma unroll
+            for (int cg = 0; cg < 5; ++cg) dma(bA, rowA, cg);
+            if (wave < 2) {
+#pragma unroll
+                for (int cg = 0; cg < 3; ++cg) dma(bB, rowB, cg);
+            } else {
+                dma(bB, rowB, 3);
+                dma(bB, rowB, 4);
+                const char* nb = has_noise ? epi_src0 + (int64_t)((n * a.H + ty) * a.W + tx) * (int)sizeof(T) : epi_src0;
+                const char* db = has_d ? epi_src1 + n * 256 : epi_src1;
+                const char* src = (lane < 32 ? nb : db) + elane;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                 (lds_ptr_t)(epil + eslot * R_EPI), 16, 0, 0);
+            }
+        }
+    };
+    auto issue_any = [&](int t, int slot, int eslot) {
+        if constexpr ((STG & 4) != 0) issue_fast(t, slot, eslot);
+        else issue(t, slot, eslot);
+    };
+
     // MFMA B-fragment addressing: pixel fragment i of the wave at tap (ky, kx), chunk c reads position
     // (2 wr + (i >> 1) + ky) * 40 + (i & 1) * 16 + l16 + kx, piece c * 4 + q (swizzled as at the DMA)
     int boff[3][2];
@@ -898,6 +960,7 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     const float clampv = (EPI && a.clamp >= 0.f) ? a.clamp : __builtin_inff();
     const float ngain = a.noise_gain * a.gain;
     const int ch0 = 32 * h + 8 * q;                   // this lane's 8 output channels
+    const int perm_src = ((lane >> 2) + 16 * (lane & 3)) * 4;   // STG 2: ds_bpermute source (byte address of a lane)
 
     // The epilogue tables are read by inline-asm ds_reads: an LDS-DMA writes this ring, so hipcc would put an
     // s_waitcnt vmcnt(0) before any ds_read it can see here, draining the tiles in flight.  The ring discipline
@@ -956,8 +1019,21 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
             int dst = (pix * 64 + ch0) * (int)sizeof(T) | -(int)((SG2_RDIAG & 32) != 0);   // timing-only build: dropped
             if (SG2_RDIAG & 256)   // timing-only build: the same bytes as whole-line stores (8 px x 128 B an instruction)
                 dst = (((n * a.H + ty + WR * wr + h) * a.W + tx + i * 8 + (lane >> 3)) * 64 + (lane & 7) * 8) * (int)sizeof(T);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, dst, 0, 0);
-            if (RAW) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, dst, 0, 0);
+            u32x4 yq = __builtin_bit_cast(u32x4, yv), rq = __builtin_bit_cast(u32x4, rv);
+            if constexpr ((STG & 2) != 0) {
+                // lane-permuted stores: lane 4m + j takes piece j of pixel m (from lane m + 16 j), so each group of 4
+                // consecutive lanes writes one pixel's 64 contiguous bytes (the texture-address path coalesces
+                // consecutive lanes; the MFMA layout gives consecutive lanes consecutive PIXELS)
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    yq[d] = (unsigned)__builtin_amdgcn_ds_bpermute(perm_src, (int)yq[d]);
+                    if (RAW) rq[d] = (unsigned)__builtin_amdgcn_ds_bpermute(perm_src, (int)rq[d]);
+                }
+                dst = ((((n * a.H + ty + r) * a.W + tx + (i & 1) * 16 + (lane >> 2)) * 64 + 32 * h + 8 * (lane & 3)) *
+                       (int)sizeof(T)) | -(int)((SG2_RDIAG & 32) != 0);
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(yq, ryb, dst, 0, 0);
+            if (RAW) __builtin_amdgcn_raw_buffer_store_b128(rq, ryr, dst, 0, 0);
         }
     };
     // STG: the same epilogue with whole-line stores.  The tile's outputs go through the slot its MFMAs just
@@ -1041,9 +1117,9 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     };
 
     // ---- prologue: tiles 0 .. NSLOT - 2 in flight, wait for tile 0 ----
-    issue(t_begin, 0, 0);
+    issue_any(t_begin, 0, 0);
     if (R_NSLOT == 3) {
-        issue(min(t_begin + 1, t_end - 1), 1, 1);
+        issue_any(min(t_begin + 1, t_end - 1), 1, 1);
         wait_vm<R_DMA>();
     } else {
         wait_vm<0>();
@@ -1052,22 +1128,32 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     __builtin_amdgcn_s_barrier();
 
     int k = 0;
+#if SG2_RDIAG & 512
+    unsigned long long st_sum[5] = {0, 0, 0, 0, 0}, st_first = ring_stamp(), st_prev = st_first;
+    auto st = [&](int ph) { const unsigned long long t = ring_stamp(); st_sum[ph] += t - st_prev; st_prev = t; };
+#define RING_STAMP(ph) st(ph)
+#else
+#define RING_STAMP(ph) ((void)0)
+#endif
     if constexpr (!PIPE) {
         f32x4 acc[NF][2];
         for (int t = t_begin; t < t_end; ++t, ++k) {
             const int slot = k % R_NSLOT;
-            issue(min(t + R_NSLOT - 1, t_end - 1), (k + R_NSLOT - 1) % R_NSLOT, (k + R_NSLOT - 1) % R_NEPI);
+            issue_any(min(t + R_NSLOT - 1, t_end - 1), (k + R_NSLOT - 1) % R_NSLOT, (k + R_NSLOT - 1) % R_NEPI);
             int n, ty, tx;
             tile_of(t, n, ty, tx);
             if (SI && n != cur_n) {                   // a new sample: re-modulate the weights (rare)
                 cur_n = n;
                 load_weights(n);
             }
+            RING_STAMP(0);
             mfma_tile(acc, smem_raw + slot * R_SLOT);
+            RING_STAMP(1);
             float bb[8], dd[8], nz[NF];
             epi_table(k % R_NEPI, bb, dd, nz);
-            if constexpr (STG) epi_store_staged(acc, slot, n, ty, tx, bb, dd, nz);
+            if constexpr (STG == 1) epi_store_staged(acc, slot, n, ty, tx, bb, dd, nz);
             else epi_store(acc, n, ty, tx, bb, dd, nz);
+            RING_STAMP(2);
             // tile t + 1's DMAs must have landed: everything but the youngest ops of this wave.  3 slots: t + 1
             // was issued one iteration ago, younger are this iteration's DMAs and stores and the previous
             // iteration's stores; 2 slots: t + 1 was issued at the top of this iteration, younger are this
@@ -1075,8 +1161,10 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
             if (R_NSLOT == 2) wait_vm<S>();
             else if (k == 0) wait_vm<R_DMA + S>();
             else wait_vm<R_DMA + 2 * S>();
+            RING_STAMP(3);
             __builtin_amdgcn_s_waitcnt(0xc07f);       // lgkmcnt(0): this tile's LDS reads are done
             __builtin_amdgcn_s_barrier();
+            RING_STAMP(4);
         }
     } else {
         // Pipelined epilogue (3-slot form): iteration k runs tile k's MFMAs into one accumulator set and tile
@@ -1125,9 +1213,23 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
         else epi_store(acc1, pn, pty, ptx, bb, dd, nz);
     }
     wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
+#if SG2_RDIAG & 512
+    {
+        const int gw = blockIdx.x * NW + wave;
+        if (lane == 0 && gw < RST_WAVES) {
+            unsigned long long* o = g_ring_stamps + gw * RST_F;
+            for (int ph = 0; ph < 5; ++ph) o[ph] = st_sum[ph];
+            o[5] = st_first;
+            o[6] = st_prev;
+            o[7] = ((unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) << 32) |
+                   (unsigned)(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 16 | (t_end - t_begin));
+        }
+    }
+#endif
+#undef RING_STAMP
 }
 
-template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, bool STG>
+template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, int STG>
 int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
     typedef Ring<TH, WR> RG;
     auto kern = conv3x3_c64r_kernel<T, SI, EPI, RAW, TH, WR, PIPE, STG>;
@@ -1140,7 +1242,7 @@ int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band
     return launch_status("sg2_conv3x3 (c64 ring)");
 }
 
-template <typename T, bool SI, bool EPI, int TH, int WR, bool PIPE = false, bool STG = false>
+template <typename T, bool SI, bool EPI, int TH, int WR, bool PIPE = false, int STG = 0>
 int launch_c64r_raw(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
     return a.y_raw ? launch_c64r<T, SI, EPI, true, TH, WR, PIPE, STG>(a, s, tiles, grid, band)
                    : launch_c64r<T, SI, EPI, false, TH, WR, PIPE, STG>(a, s, tiles, grid, band);
@@ -1153,12 +1255,15 @@ int launch_c64r_raw(const Conv3Args& a, hipStream_t s, int tiles, int grid, int 
 // VGPRs and is not instantiated.)
 template <typename T, bool SI, bool EPI>
 int launch_c64r_form(const Conv3Args& a, hipStream_t s, int form) {
-    const int th = (form == 4 || form == 44) ? 4 : 8;
+    const int th = (form == 4 || (form >= 44 && form <= 47)) ? 4 : 8;
     const int tiles = a.N * (a.H / th) * (a.W / R_TW);
     const int ty = a.H / th;
     const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
     if (form == 4) return launch_c64r_raw<T, SI, EPI, 4, 2>(a, s, tiles, 2 * num_cus(), band);
-    if (form == 44) return launch_c64r_raw<T, SI, EPI, 4, 2, false, true>(a, s, tiles, 2 * num_cus(), band);
+    if (form == 44) return launch_c64r_raw<T, SI, EPI, 4, 2, false, 1>(a, s, tiles, 2 * num_cus(), band);
+    if (form == 45) return launch_c64r_raw<T, SI, EPI, 4, 2, false, 2>(a, s, tiles, 2 * num_cus(), band);
+    if (form == 46) return launch_c64r_raw<T, SI, EPI, 4, 2, false, 4>(a, s, tiles, 2 * num_cus(), band);
+    if (form == 47) return launch_c64r_raw<T, SI, EPI, 4, 2, false, 6>(a, s, tiles, 2 * num_cus(), band);
     if (form == 84) return launch_c64r_raw<T, SI, EPI, 8, 4>(a, s, tiles, num_cus(), band);
     return launch_c64r_raw<T, SI, EPI, 8, 2>(a, s, tiles, num_cus(), band);
 }
@@ -1182,15 +1287,17 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     // SG2_C64_RING: 0 off, else the ring form (launch_c64r_form: 4 default, 8, 84)
     const char* ring_env = getenv("SG2_C64_RING");   // read per launch: tests switch forms in one process
     const int ring = ring_env ? atoi(ring_env) : 4;
-    const int rth = (ring == 4 || ring == 44) ? 4 : 8;
+    const int rth = (ring == 4 || (ring >= 44 && ring <= 47)) ? 4 : 8;
     if (ring && !a.dot_out && a.Cin == P_C && a.Cout == P_C && a.H % rth == 0 && a.W % R_TW == 0 &&
         ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 && ((uintptr_t)a.noise % 16) == 0 &&
         ((uintptr_t)a.out_scale % 16) == 0 && ((uintptr_t)a.in_scale % 16) == 0 &&
         (!epi || (a.gain > 0.f && (a.act == 0 || (a.alpha >= 0.f && a.alpha <= 1.f))))) {
         const int tiles = a.N * (a.H / rth) * (a.W / R_TW);
         const int grid = (rth == 4 ? 2 : 1) * num_cus();
-        if (tiles >= 2 * grid && tiles <= 128 * grid && a.N < 4096 && a.H / rth < 1024 && a.W / R_TW < 1024) {
-            const int form = (ring == 84 || ring == 44) ? ring : rth;
+        // (the fast DMA issue marks an invalid halo row with base INT_MIN: the image must stay below 2^31 - 2^16 B)
+        if (tiles >= 2 * grid && tiles <= 128 * grid && a.N < 4096 && a.H / rth < 1024 && a.W / R_TW < 1024 &&
+            (int64_t)a.N * a.H * a.W * 64 * (int64_t)sizeof(T) < 0x7fff0000ll) {
+            const int form = (ring == 84 || (ring >= 44 && ring <= 47)) ? ring : rth;
             if (si) { if (epi) return launch_c64r_form<T, true, true>(a, s, form); return launch_c64r_form<T, true, false>(a, s, form); }
             if (epi) return launch_c64r_form<T, false, true>(a, s, form);
             return launch_c64r_form<T, false, false>(a, s, form);
@@ -1479,3 +1586,11 @@ extern "C" int sg2_conv3x3_up2(void* y, const void* x, const void* w, int dtype,
     if (dtype == SG2_F16) return in_scale ? launch_up2<f16_t, true>(a, s) : launch_up2<f16_t, false>(a, s);
     return in_scale ? launch_up2<bf16_t, true>(a, s) : launch_up2<bf16_t, false>(a, s);
 }
+
+#if SG2_RDIAG & 512
+extern "C" int sg2_diag_ring_stamps(void* dst, long long bytes) {
+    const size_t n = sizeof(sg2::g_ring_stamps) < (size_t)bytes ? sizeof(sg2::g_ring_stamps) : (size_t)bytes;
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(sg2::g_ring_stamps), n, 0, hipMemcpyDeviceToHost);
+}
+#endif
+

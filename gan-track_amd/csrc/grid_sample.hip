@@ -136,8 +136,10 @@ __global__ __launch_bounds__(256) void grid_sample_bwd_gather_kernel(GSParams p)
             const double c0 = (((double)t[0] * (1.0 / p.Wo - 1.0) + (double)t[1] * (1.0 / p.Ho - 1.0) + t[2] + 1.0) * Wi - 1.0) * 0.5;
             const double c1 = (((double)t[3] * (1.0 / p.Wo - 1.0) + (double)t[4] * (1.0 / p.Ho - 1.0) + t[5] + 1.0) * Hi - 1.0) * 0.5;
             const double det = a00 * a11 - a01 * a10;
-            double oxmin = 1e30, oxmax = -1e30, oymin = 1e30, oymax = -1e30;
+            // a (near-)singular map: scan the whole output (the bounds below clamp to it)
+            double oxmin = -1e30, oxmax = 1e30, oymin = -1e30, oymax = 1e30;
             if (fabs(det) > 1e-12) {
+                oxmin = 1e30; oxmax = -1e30; oymin = 1e30; oymax = -1e30;
                 for (int cy = 0; cy < 2; ++cy)
                     for (int cx = 0; cx < 2; ++cx) {
                         const double u = (X - 1 + 2 * cx) - c0, v = (Y - 1 + 2 * cy) - c1;
@@ -146,8 +148,10 @@ __global__ __launch_bounds__(256) void grid_sample_bwd_gather_kernel(GSParams p)
                         oymin = fmin(oymin, oy); oymax = fmax(oymax, oy);
                     }
             }
-            const int ox0 = max(0, (int)floor(oxmin) - 2), ox1 = min(p.Wo - 1, (int)ceil(oxmax) + 2);
-            const int oy0 = max(0, (int)floor(oymin) - 2), oy1 = min(p.Ho - 1, (int)ceil(oymax) + 2);
+            // clamped in double before the int conversion (a huge or NaN bound is undefined as an int)
+            auto cl = [](double v, int hi) { return v > -4.0 ? (v < hi + 4.0 ? v : hi + 4.0) : -4.0; };
+            const int ox0 = max(0, (int)floor(cl(oxmin, p.Wo)) - 2), ox1 = min(p.Wo - 1, (int)ceil(cl(oxmax, p.Wo)) + 2);
+            const int oy0 = max(0, (int)floor(cl(oymin, p.Ho)) - 2), oy1 = min(p.Ho - 1, (int)ceil(cl(oymax, p.Ho)) + 2);
             for (int oy = oy0; oy <= oy1; ++oy)
                 for (int ox = ox0; ox <= ox1; ++ox) {
                     const Corners k = corners(p, n, oy, ox, Hi, Wi);

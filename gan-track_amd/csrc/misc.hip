@@ -468,7 +468,7 @@ __global__ __launch_bounds__(256) void moments_kernel(double* row, const float* 
     double a = 0.0, b = 0.0;
     for (int64_t i = tid; i < n; i += 256) {
         float x = v[i];
-        if (mode == 1) x = x > 0.f ? 1.f : (x < 0.f ? -1.f : x);   // torch.sign: 0 -> 0, NaN -> NaN
+        if (mode == 1) x = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);   // torch.sign: (0 < x) - (x < 0): 0 and NaN -> 0
         const double d = (double)x;
         a += d;
         b += d * d;

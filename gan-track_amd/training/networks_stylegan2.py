@@ -320,8 +320,11 @@ _PLAN_CACHE = {}
 
 def _style_plan(layers, n, num_ws, device):
     """Index / gain tensors of grouped_styles for one batch size: (elem index into S, elem index into the
-    [N, sum C] bias matrix, elem alpha, column beta, ones [N, 1], per-layer (offset, C))."""
-    key = (tuple((id(a), k, float(g)) for a, k, g in layers), n, num_ws, device)
+    [N, sum C] bias matrix, elem alpha, column beta, ones [N, 1], per-layer (offset, C)).  The plan is a pure
+    function of each layer's width, gains, w index and out gain (no module identity in the key: ids are reused
+    once a network is freed)."""
+    key = (tuple((int(a.out_features), float(a.weight_gain), float(a.bias_gain), int(k), float(g)) for a, k, g in layers),
+           n, num_ws, str(device))
     plan = _PLAN_CACHE.get(key)
     if plan is not None:
         return plan

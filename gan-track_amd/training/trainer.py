@@ -168,6 +168,17 @@ class GradExchange:
         return part
 
 
+class _HostEvent:
+    """Host-clock stand-in for a timing HIP event (exchange diagnostics on a CPU device: the gloo tests)."""
+
+    def record(self, stream=None):
+        import time
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, end):
+        return (end.t - self.t) * 1e3
+
+
 class Trainer:
     def __init__(self, G, D, G_ema, loss, G_opt_kwargs, D_opt_kwargs, G_reg_interval=4, D_reg_interval=16,
                  batch_size=32, batch_gpu=32, num_gpus=1, rank=0, device=None, ema_kimg=10, ema_rampup=0.05,
@@ -211,6 +222,10 @@ class Trainer:
         self.cur_nimg = 0
         self.batch_idx = 0
         self.on_grads = None   # optional callback(phase_name, module) after the gradient exchange
+        # exchange diagnostics (bench.py at N > 1, eager steps only): per phase a list of (start, backward issued,
+        # exchange complete) HIP events on the compute stream -- complete - issued is the part of the bucketed
+        # all-reduce the backward did not hide
+        self.exchange_timing = None
         # HIP-graph mode: each phase's forward + backward (all micro-batches) and its bucket fills are
         # captured once and replayed (with the gradient exchange); the optimiser, EMA and ADA stay eager.  Capture the
         # first time a phase runs in graph mode -- run at least one eager step first so every lazily created
@@ -358,14 +373,25 @@ class Trainer:
         for phase, phase_gen_z, phase_gen_c in active:
             if phase.start_event is not None:
                 phase.start_event.record(torch.cuda.current_stream(self.device))
-            part, stepped = None, False
+            part, stepped, finished = None, False, False
             if self.graphs:
                 part, stepped = self._graph_phase(phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)
             else:
+                evs = None
+                if self.exchange_timing is not None:
+                    cuda = self.device is not None and self.device.type == 'cuda'
+                    evs = [torch.cuda.Event(enable_timing=True) if cuda else _HostEvent() for _ in range(3)]
+                    stream = torch.cuda.current_stream(self.device) if cuda else None
+                    evs[0].record(stream)
                 phase.opt.zero_grad(set_to_none=True)
                 phase.module.requires_grad_(True)
                 self._accumulate(phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c)
                 phase.module.requires_grad_(False)
+                if evs is not None:
+                    evs[1].record(stream)
+                    part, finished = phase.exchange.finish(phase.name), True
+                    evs[2].record(stream)
+                    self.exchange_timing.setdefault(phase.name, []).append(evs)
             with torch.autograd.profiler.record_function(phase.name + '_opt'):
                 ex = phase.exchange
                 if stepped:
@@ -376,7 +402,7 @@ class Trainer:
                     if phase.end_event is not None:
                         phase.end_event.record(torch.cuda.current_stream(self.device))
                     continue
-                part = ex.finish(phase.name, part) if not self.graphs else part
+                part = ex.finish(phase.name, part) if not (self.graphs or finished) else part
                 if isinstance(phase.opt, FlatAdam):
                     phase.opt.step_flat(ex.flat, ex.offsets, part, grad_scale=1.0 / self.num_gpus,
                                         write_grad=self.on_grads is not None, tag=phase.name)

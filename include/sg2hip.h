@@ -20,8 +20,13 @@
  *   SG3/training/training_loop_mi_multimodal.py:358-366 (G_ema lerp)      -> sg2_lerp_multi
  *
  * Conventions
- *  - Every pointer is a device pointer; the library never allocates or frees device memory and keeps
- *    no mutable global state (re-entrant; safe to capture into a hipGraph).
+ *  - Every pointer is a device pointer; the library never allocates or frees device memory.
+ *  - Mutable state: three mode switches, set between launches and read by every later launch --
+ *      sg2_set_deterministic (PROCESS-WIDE: the caller's scratch arena for fixed-order slot reductions; process-
+ *        wide because autograd runs a deterministic scope's backward on its own device thread),
+ *      sg2_set_zeroed_accumulators, sg2_set_clean_workspace (PER HOST THREAD),
+ *    plus the per-thread sg2_last_error() message.  Otherwise the kernels are re-entrant and capturable into a
+ *    hipGraph; do not change the process-wide deterministic arena while another thread is launching.
  *  - `stream` is a hipStream_t (pass the caller's current stream; NULL = default stream).
  *  - dtype codes: SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2 (arithmetic is always f32 internally).
  *  - 4-D activations are NHWC in memory (torch channels_last); sizes are given as [N, C, H, W]

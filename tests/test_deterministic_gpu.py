@@ -202,3 +202,27 @@ def test_det_isolated_iteration_c2(dt):
     assert not diff, f'{len(diff)} summaries differ between deterministic runs, e.g. {diff[:3]}'
     for (n1, v1), (n2, v2) in zip(s1, s2):
         assert n1 == n2 and np.array_equal(v1, v2), n1
+
+
+def test_det_affine_grid_sample_bwd_singular():
+    """A singular affine map (det 0: both output axes sample along one input line): the deterministic gather has
+    no finite inverse to bound its scan, so it scans the whole output; its input gradient must still equal
+    grid_sample's in float64, as the atomic scatter's does."""
+    from torch_utils.ops import grid_sample_gradfix as gs
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(2, 3, 40, 36, generator=g)
+    theta = torch.tensor([[[0.5, 0.5, 0.1], [0.5, 0.5, -0.1]], [[0.0, 0.0, 0.2], [0.0, 0.0, 0.3]]])
+    size = [2, 3, 44, 40]
+    dy = torch.randn(size, generator=g)
+    grid = F.affine_grid(theta.double(), size, align_corners=False)
+    xr = x.double().requires_grad_(True)
+    ref, = torch.autograd.grad(F.grid_sample(xr, grid, align_corners=False), [xr], dy.double())
+    xd = x.to(DEV).requires_grad_(True)
+
+    def fn():
+        y = gs.affine_grid_sample(xd, theta.to(DEV), size)
+        return torch.autograd.grad(y, [xd], dy.to(DEV))[0]
+    with sg2hip.deterministic():
+        u = fn().clone()
+    w = fn()
+    assert rel_err(u, ref) < 1e-5 and rel_err(w, ref) < 1e-5, (rel_err(u, ref), rel_err(w, ref))

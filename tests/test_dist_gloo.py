@@ -47,7 +47,7 @@ def _worker(rank, world, port, paths, result_q):
         zs = torch.randn([4, B, 16], generator=g)
         c = torch.zeros([4, B, 0])
 
-        def run(num_gpus, overlap=True, bucket_mb=0.0005):
+        def run(num_gpus, overlap=True, bucket_mb=0.0005, timing=False):
             G.load_state_dict(init[0])
             D.load_state_dict(init[1])
             G_ema = copy.deepcopy(G).eval()
@@ -62,6 +62,8 @@ def _worker(rank, world, port, paths, result_q):
                         grads[f'{name}/{n}'] = p.grad.detach().clone()
 
             tr.on_grads = cb
+            if timing:
+                tr.exchange_timing = {}     # bench.py's N > 1 exchange diagnostics (events around finish())
             torch.manual_seed(1234 + rank)
             chunks = lambda t: list(t.split(B // 2))  # noqa: E731
             tr.step(chunks(real), chunks(torch.zeros([B, 0])), [chunks(zs[i]) for i in range(4)],
@@ -87,6 +89,14 @@ def _worker(rank, world, port, paths, result_q):
         misc.check_ddp_consistency(G, ignore_regex=r'.*\.[^.]+_(avg|ema)')
         misc.check_ddp_consistency(D)
         nbuckets = len(tr.phases[0].exchange.buckets)
+        # with the exchange diagnostics on: the same gradients (finish() runs once per phase, nothing reduced
+        # twice) and one (start, issued, complete) record per phase
+        timed, trt = run(world, timing=True)
+        assert sorted(timed) == sorted(plain)
+        for k in plain:
+            worst = max(worst, float((timed[k] - plain[k]).abs().max() / (plain[k].abs().max() + 1e-12)))
+        assert sorted(trt.exchange_timing) == sorted(ph.name for ph in trt.phases), sorted(trt.exchange_timing)
+        assert all(len(v) == 1 and v[0][1].elapsed_time(v[0][2]) >= 0 for v in trt.exchange_timing.values())
         result_q.put((rank, worst, len(local), nbuckets))
     finally:
         dist.destroy_process_group()

@@ -62,3 +62,27 @@ def test_grouped_styles_match_per_layer(n):
         assert torch.allclose(x, y, rtol=1e-5, atol=1e-5)
     for x, y in zip(a[3], b[3]):
         assert torch.allclose(x, y, rtol=1e-4, atol=1e-6)
+
+
+def test_grouped_styles_plan_follows_widths():
+    """Two networks of different widths built one after the other (the first freed, so its module ids may be
+    reused): each one's grouped styles equal its per-layer affine (the style plan's cache key holds the layers'
+    widths and gains, not their identities)."""
+    from training import networks_stylegan2 as net
+    for cmax in (64, 32, 64):
+        torch.manual_seed(cmax)
+        G = net.Generator(z_dim=16, c_dim=0, w_dim=32, img_resolution=32, img_channels=1, channel_base=256,
+                          channel_max=cmax, mapping_kwargs=dict(num_layers=2))
+        for m in G.modules():
+            if isinstance(m, net.FullyConnectedLayer) and m.bias is not None:
+                with torch.no_grad():
+                    m.bias.add_(torch.randn_like(m.bias) * 0.3)
+        plan = _plan(G.synthesis)
+        ws = torch.randn(2, G.synthesis.num_ws, 32)
+        with torch.no_grad():
+            got = net.grouped_styles(ws, plan)
+            ref = [a(ws[:, k], out_gain=g) for a, k, g in plan]
+        for x, y in zip(got, ref):
+            assert x.shape == y.shape
+            assert torch.allclose(x, y, rtol=1e-5, atol=1e-6)
+        del G, plan

@@ -1324,11 +1324,12 @@ def test_fused_conv_wgain_weight_grad(mode):
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize('shape', [(4, 256, 256), (11, 48, 256), (13, 40, 256), (3, 64, 704)])
 @pytest.mark.parametrize('form', ['mod_epi_raw', 'mod_epi', 'mod_only', 'plain_epi', 'plain', 'epi_no_noise'])
-@pytest.mark.parametrize('ring', ['4', '44', '8', '84'])
+@pytest.mark.parametrize('ring', ['4', '44', '45', '46', '47', '8', '84'])
 def test_conv3x3_c64_ring(dtype, shape, form, ring, monkeypatch):
     """The 64 -> 64 channel ring kernel (LDS-DMA halo ring, weights in registers modulated per sample;
     conv3x3.hip conv3x3_c64r_kernel) in its three forms (ring 4: two workgroups per CU on 32 x 4 tiles, 2-slot rings;
-    ring 44: ring 4 with whole-line stores staged through LDS; ring 8: one workgroup of 8 waves on 32 x 8 tiles,
+    ring 44: ring 4 with whole-line stores staged through LDS; 45: lane-permuted stores; 46: the hoisted DMA issue;
+    47: both; ring 8: one workgroup of 8 waves on 32 x 8 tiles,
     3-slot ring; ring 84: the same tiles with 4 waves of 4 rows)
     and every form the layers use -- the synthesis forward
     (modulation, demod, noise, bias, lrelu, clamp, raw output), the path-length pass's scaled transposed conv
@@ -1339,7 +1340,7 @@ def test_conv3x3_c64_ring(dtype, shape, form, ring, monkeypatch):
     monkeypatch.setenv('SG2_C64_RING', ring)
     N, H, W = shape
     C = 64
-    th = 4 if ring in ('4', '44') else 8
+    th = 4 if ring in ('4', '44', '45', '46', '47') else 8
     wgs = (2 if th == 4 else 1) * torch.cuda.get_device_properties(DEV).multi_processor_count
     assert N * (H // th) * (W // 32) >= 2 * wgs      # the ring kernel's minimum of two tiles per workgroup
     torch.manual_seed(17)
@@ -1525,3 +1526,59 @@ def test_training_stats_moments(n):
     vd, sd = v.double().flatten(), v.sign().double().flatten()
     want = torch.tensor([[n, vd.sum(), vd.square().sum()], [n, sd.sum(), sd.square().sum()]], dtype=torch.float64)
     assert torch.allclose(got, want, rtol=1e-12, atol=1e-9), (got, want)
+
+
+@pytest.mark.gpu
+def test_training_stats_sign_nan():
+    """report_sign of a value holding NaN: sg2_moments' sign maps NaN to 0 as torch.sign does on the same device
+    ((0 < x) - (x < 0)), so divergent logits keep Loss/signs/* finite (the ADA heuristic's input)."""
+    from torch_utils import training_stats as ts
+    v = torch.tensor([[1.5], [float('nan')], [-2.0], [0.0], [float('nan')]], device=DEV)
+    table = ts._board.table(DEV)
+    r = ts._board.row('test/signs/nan')
+    before = table[r].clone()
+    ts.report_sign('test/signs/nan', v)
+    got = (table[r] - before).cpu()
+    sd = v.sign().double().flatten().cpu()
+    want = torch.tensor([v.numel(), sd.sum(), sd.square().sum()], dtype=torch.float64)
+    assert torch.isfinite(got).all() and torch.equal(got, want), (got, want)
+
+
+def test_vjp_nodes_upstream_gradient():
+    """The path-length pass's second-order nodes with an upstream gradient that itself depends on a leaf
+    (_InfNormVJP's g_dy, _DemodVJP's g_dd and g_d): the second pass differentiates into that leaf too, against
+    autograd of the reference expressions (networks_stylegan2.py:52-54, :59-63) in float64."""
+    from training import networks_stylegan2 as net
+    from torch_utils.ops import conv2d_gradfix as cg
+    torch.manual_seed(9)
+    w = torch.randn(24, 20, 3, 3)
+    w[3, 5, 1, 1] = w[3].abs().max() + 1.0
+    w[3, 7, 0, 2] = -w[3, 5, 1, 1]
+    s = torch.randn(4, 20)
+    aw0, as0 = torch.randn_like(w), torch.randn_like(s)
+    qw, qs = torch.randn_like(w), torch.randn_like(s)
+    dd0, qd = torch.randn(4, 24), torch.randn(4, 20)
+
+    def ref_prenorm(w_, s_):
+        return (w_ * (1 / np.sqrt(20 * 9) / w_.norm(float('inf'), dim=[1, 2, 3], keepdim=True)),
+                s_ / s_.norm(float('inf'), dim=1, keepdim=True))
+
+    def ref_demod(w_, s_):
+        return ((w_[None] * s_[:, None, :, None, None]).square().sum([2, 3, 4]) + 1e-8).rsqrt()
+
+    out = []
+    for dev, dt, pre, dem in [(DEV, torch.float32, net._prenorm, net._demod),
+                              (torch.device('cpu'), torch.float64, ref_prenorm, ref_demod)]:
+        L = lambda t: t.to(dev, dt).requires_grad_(True)  # noqa: E731
+        wd, sd, aw, as_ = L(w), L(s), L(aw0), L(as0)
+        yw, ys = pre(wd, sd)
+        g1w, g1s = torch.autograd.grad((yw * aw).sum() + (ys * as_).sum(), [wd, sd], create_graph=True)
+        r1 = torch.autograd.grad((g1w * qw.to(dev, dt)).sum() + (g1s * qs.to(dev, dt)).sum(), [wd, sd, aw, as_])
+        ws, ss, ddl = L(w), L(s.abs() + 0.2), L(dd0)
+        d = dem(ws, ss)
+        with cg.no_weight_gradients(dev.type == 'cuda'):
+            gs, = torch.autograd.grad((d * ddl).sum(), [ss], create_graph=True)
+        r2 = torch.autograd.grad((gs * qd.to(dev, dt)).sum() + (d * ddl).square().sum(), [ws, ss, ddl])
+        out.append([t.detach().double().cpu() for t in (*r1, *r2)])
+    for i, (a, b) in enumerate(zip(*out)):
+        assert rel_err(a, b) < 1e-5, (i, rel_err(a, b))
