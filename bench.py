@@ -215,7 +215,7 @@ def roofline(device, res, cbase, dtype, N=32):
     key = f'sg2_conv3x3 fused {res}^2 C={C} N={N} {str(dtype).split(".")[-1]}'
     gbps = byts / (ms * 1e-3) / 1e9
     tflops = flops / (ms * 1e-3) / 1e12
-    ring = C == 64 and os.environ.get('SG2_C64_RING', '1') != '0'
+    ring = C == 64 and os.environ.get('SG2_C64_RING', '49') != '0'
     kname = ('conv3x3_c64r_kernel (LDS-DMA halo ring, weights in registers)' if ring else
              'conv3x3_c64p_kernel (persistent, weights in LDS)') if C == 64 else 'conv3x3_halo_kernel'
     out = {'kernel': f'{kname} ({key}: modulation + demod/noise/bias/lrelu/clamp epilogue)'}

@@ -731,7 +731,7 @@ template <int TH, int WR> struct Ring {
     static constexpr int SLOT = HPOS * 128;                           // 51,200 / 30,720 B
     static constexpr int HALO_I = HPOS / 8;                           // halo DMA wave-instructions per tile
     static constexpr int DMA = (HALO_I + 1 + NW - 1) / NW;            // per wave and tile (+ the epilogue table)
-    static constexpr size_t LDS = (size_t)NSLOT * SLOT + R_NEPI * R_EPI + 64 * 4;   // + gain * bias [64]
+    static constexpr size_t LDS = (size_t)NSLOT * SLOT + R_NEPI * R_EPI + 64 * 4 + 16;   // + gain * bias [64], a broadcast word
     static constexpr int WGS_PER_CU = TH == 8 ? 1 : 2;
     static_assert(LDS * WGS_PER_CU <= 160 * 1024, "ring LDS");
     static_assert((DMA - 1) * NW <= HALO_I && DMA * NW > HALO_I, "the last DMA round holds the epilogue table");
@@ -748,7 +748,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // Diagnostic build only (tools/ring_stamps.py): per wave, the summed cycles of each loop phase of the ring kernel
 // from s_memtime stamps (issue DMAs | MFMAs issued | epilogue + stores issued | DMA wait | barrier), the first and
 // last stamp and the hardware wave id, written once at the end by lane 0 (vector stores; nothing in the loop).
-constexpr int RST_WAVES = 4096, RST_F = 8;
+constexpr int RST_WAVES = 4096, RST_F = 10;
 __device__ unsigned long long g_ring_stamps[RST_WAVES * RST_F];
 __device__ __forceinline__ unsigned long long ring_stamp() {
     unsigned long long t;
@@ -769,8 +769,27 @@ __device__ __forceinline__ void wait_vm() {           // s_waitcnt vmcnt(N) (gfx
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// STG & 16: a dynamic tail within each sample.  The ring kernel is persistent with a static split of the tiles, and
+// the CUs do not run at one speed (the in-kernel clock differs by ~8 % between XCDs under this load and the
+// slowest workgroup of a launch ended ~17 % after the median one, tools/ring_stamps.py).  Here the workgroups of a
+// sample (grid / N of them, dealt round-robin over the XCDs) keep static runs of `dyn.s_per_wg` tiles and take the
+// sample's remaining tiles in chunks of two vertically adjacent tiles from the sample's device-scope counter: a
+// workgroup grabs its next chunk one tile before it needs it (one returning atomic by one lane, broadcast through
+// LDS at the tile's barrier) and leaves when the counter passes the sample's last chunk.  Every chunk is in the
+// workgroup's own sample, so its weights stay modulated (a chunk of another sample re-modulated them: tried, the
+// reloads cost more than the balance gained).  The last workgroup of a sample to leave resets the sample's counter
+// pair for the next launch.  Which workgroup runs a tile never changes its result (no cross-tile reductions).
+struct RingDyn {
+    int* q;             // [grab counter per sample][N], then [done counter per sample][N] (zero between launches)
+    int s_per_wg;       // static tiles per workgroup (>= 2)
+    int wg_per_n;       // workgroups per sample (grid = N wg_per_n)
+    int nchunks;        // dynamic chunks of 2 tiles per sample after its static runs
+};
+constexpr int RQ_SLOTS = 64, RQ_MAXN = 4096;
+__device__ int g_ring_q[RQ_SLOTS * 2 * RQ_MAXN];
+
 template <typename T, bool SI, bool EPI, bool RAW, int R_TH, int WR, bool PIPE, int STG>
-__global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER_CU)) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band) {
+__global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER_CU)) void conv3x3_c64r_kernel(Conv3Args a, int tiles_total, int band, RingDyn dyn) {
     typedef T vec8 __attribute__((ext_vector_type(8)));
     typedef Ring<R_TH, WR> RG;
     constexpr int NF = 2 * WR;                        // pixel fragments (16 px) per wave
@@ -784,8 +803,13 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l16 = lane & 15, q = lane >> 4;
     const int h = wave & 1, wr = wave >> 1;           // channel half, tile row group (rows WR wr .. + WR - 1)
-    const int t_begin = (int)((int64_t)blockIdx.x * tiles_total / gridDim.x);
-    const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles_total / gridDim.x);
+    constexpr bool DYN = (STG & 16) != 0;
+    const int dyn_n = DYN ? (int)blockIdx.x / dyn.wg_per_n : 0;                       // the workgroup's sample
+    const int dyn_per_n = DYN ? tiles_total / a.N : 0;
+    const int t_begin = DYN ? dyn_n * dyn_per_n + ((int)blockIdx.x - dyn_n * dyn.wg_per_n) * dyn.s_per_wg
+                            : (int)((int64_t)blockIdx.x * tiles_total / gridDim.x);
+    const int t_end = DYN ? t_begin + dyn.s_per_wg : (int)((int64_t)(blockIdx.x + 1) * tiles_total / gridDim.x);
+    const int dyn_base = DYN ? dyn_n * dyn_per_n + dyn.wg_per_n * dyn.s_per_wg : 0;
     if (t_begin >= t_end) return;
     // tile t -> (n, ty, tx): samples, bands of `band` tile rows, column-major inside a band (vertical neighbours,
     // which share two halo rows, are consecutive in a CU's run).  Lane j of tinfo0 / tinfo1 holds tile
@@ -800,7 +824,9 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     const int tinfo1 = t_begin + 64 + lane < t_end ? pack_tile(t_begin + 64 + lane) : 0;
     auto tile_of = [&](int t, int& n, int& ty, int& tx) {
         const int j = t - t_begin;
-        const int v = j < 64 ? __builtin_amdgcn_readlane(tinfo0, j) : __builtin_amdgcn_readlane(tinfo1, j - 64);
+        int v;
+        if (DYN && (unsigned)j >= (unsigned)(t_end - t_begin)) v = __builtin_amdgcn_readfirstlane(pack_tile(t));   // a dynamic tile
+        else v = j < 64 ? __builtin_amdgcn_readlane(tinfo0, j) : __builtin_amdgcn_readlane(tinfo1, j - 64);
         n = (int)((unsigned)v >> 20);      // unsigned: a sample index >= 2048 sets bit 31
         ty = ((v >> 10) & 1023) * R_TH;
         tx = (v & 1023) * R_TW;
@@ -960,7 +986,6 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     const float clampv = (EPI && a.clamp >= 0.f) ? a.clamp : __builtin_inff();
     const float ngain = a.noise_gain * a.gain;
     const int ch0 = 32 * h + 8 * q;                   // this lane's 8 output channels
-    const int perm_src = ((lane >> 2) + 16 * (lane & 3)) * 4;   // STG 2: ds_bpermute source (byte address of a lane)
 
     // The epilogue tables are read by inline-asm ds_reads: an LDS-DMA writes this ring, so hipcc would put an
     // s_waitcnt vmcnt(0) before any ds_read it can see here, draining the tiles in flight.  The ring discipline
@@ -1019,21 +1044,8 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
             int dst = (pix * 64 + ch0) * (int)sizeof(T) | -(int)((SG2_RDIAG & 32) != 0);   // timing-only build: dropped
             if (SG2_RDIAG & 256)   // timing-only build: the same bytes as whole-line stores (8 px x 128 B an instruction)
                 dst = (((n * a.H + ty + WR * wr + h) * a.W + tx + i * 8 + (lane >> 3)) * 64 + (lane & 7) * 8) * (int)sizeof(T);
-            u32x4 yq = __builtin_bit_cast(u32x4, yv), rq = __builtin_bit_cast(u32x4, rv);
-            if constexpr ((STG & 2) != 0) {
-                // lane-permuted stores: lane 4m + j takes piece j of pixel m (from lane m + 16 j), so each group of 4
-                // consecutive lanes writes one pixel's 64 contiguous bytes (the texture-address path coalesces
-                // consecutive lanes; the MFMA layout gives consecutive lanes consecutive PIXELS)
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    yq[d] = (unsigned)__builtin_amdgcn_ds_bpermute(perm_src, (int)yq[d]);
-                    if (RAW) rq[d] = (unsigned)__builtin_amdgcn_ds_bpermute(perm_src, (int)rq[d]);
-                }
-                dst = ((((n * a.H + ty + r) * a.W + tx + (i & 1) * 16 + (lane >> 2)) * 64 + 32 * h + 8 * (lane & 3)) *
-                       (int)sizeof(T)) | -(int)((SG2_RDIAG & 32) != 0);
-            }
-            __builtin_amdgcn_raw_buffer_store_b128(yq, ryb, dst, 0, 0);
-            if (RAW) __builtin_amdgcn_raw_buffer_store_b128(rq, ryr, dst, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, dst, 0, 0);
+            if (RAW) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, dst, 0, 0);
         }
     };
     // STG: the same epilogue with whole-line stores.  The tile's outputs go through the slot its MFMAs just
@@ -1130,12 +1142,55 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     int k = 0;
 #if SG2_RDIAG & 512
     unsigned long long st_sum[5] = {0, 0, 0, 0, 0}, st_first = ring_stamp(), st_prev = st_first;
+    const unsigned long long rt_first = __builtin_amdgcn_s_memrealtime();
     auto st = [&](int ph) { const unsigned long long t = ring_stamp(); st_sum[ph] += t - st_prev; st_prev = t; };
 #define RING_STAMP(ph) st(ph)
 #else
 #define RING_STAMP(ph) ((void)0)
 #endif
-    if constexpr (!PIPE) {
+    if constexpr (DYN) {
+        static_assert(R_NSLOT == 2 && !PIPE, "dynamic tail: the 2-slot form");
+        int* qlds = (int*)(blds + 64);               // the broadcast word (16 bytes past the bias table)
+        int* qn = dyn.q + dyn_n;                      // this sample's grab counter
+        f32x4 acc[NF][2];
+        int cur = t_begin, rend = t_end, gv = 0;
+        for (;; ++k) {
+            int nxt;
+            if (cur + 1 < rend) {
+                nxt = cur + 1;
+            } else {
+                unsigned qv;
+                asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(qv) : "v"(lds_addr(qlds)));
+                const int qc = __builtin_amdgcn_readfirstlane((int)qv);
+                nxt = qc < dyn.nchunks ? dyn_base + 2 * qc : -1;
+            }
+            const bool grab = cur + 2 == rend;            // second-to-last tile of its run / chunk: grab the next chunk
+            if (grab && wave == 0 && lane == 0) gv = __hip_atomic_fetch_add(qn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int slot = k % R_NSLOT;
+            issue_any(nxt >= 0 ? nxt : cur, (k + 1) % R_NSLOT, (k + 1) % R_NEPI);
+            int n, ty, tx;
+            tile_of(cur, n, ty, tx);
+            RING_STAMP(0);
+            mfma_tile(acc, smem_raw + slot * R_SLOT);
+            RING_STAMP(1);
+            float bb[8], dd[8], nz[NF];
+            epi_table(k % R_NEPI, bb, dd, nz);
+            epi_store(acc, n, ty, tx, bb, dd, nz);
+            RING_STAMP(2);
+            if (grab && wave == 0) {
+                const int g0 = __builtin_amdgcn_readfirstlane(gv);
+                asm volatile("ds_write_b32 %0, %1" :: "v"(lds_addr(qlds)), "v"(g0) : "memory");
+            }
+            wait_vm<S>();
+            RING_STAMP(3);
+            __builtin_amdgcn_s_waitcnt(0xc07f);       // lgkmcnt(0): this tile's LDS reads (and the q write) are done
+            __builtin_amdgcn_s_barrier();
+            RING_STAMP(4);
+            if (nxt < 0) break;
+            if (nxt != cur + 1) rend = nxt + 2;        // a new chunk
+            cur = nxt;
+        }
+    } else if constexpr (!PIPE) {
         f32x4 acc[NF][2];
         for (int t = t_begin; t < t_end; ++t, ++k) {
             const int slot = k % R_NSLOT;
@@ -1213,6 +1268,18 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
         else epi_store(acc1, pn, pty, ptx, bb, dd, nz);
     }
     wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
+    if constexpr (DYN) {
+        // every grab of this workgroup has returned: count it out of its sample; the sample's last one resets the
+        // sample's pair for the next launch
+        if (wave == 0 && lane == 0) {
+            int* dn = dyn.q + a.N + dyn_n;
+            const int d = __hip_atomic_fetch_add(dn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (d == dyn.wg_per_n - 1) {
+                __hip_atomic_exchange(dyn.q + dyn_n, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_exchange(dn, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
 #if SG2_RDIAG & 512
     {
         const int gw = blockIdx.x * NW + wave;
@@ -1223,10 +1290,24 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
             o[6] = st_prev;
             o[7] = ((unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) << 32) |
                    (unsigned)(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 16 | (t_end - t_begin));
+            o[8] = rt_first;
+            o[9] = __builtin_amdgcn_s_memrealtime();
         }
     }
 #endif
 #undef RING_STAMP
+}
+
+int* ring_queue_slot() {
+    // one counter table per launch in flight (a rotating slot; each is left zero by its launch's workgroups);
+    // device globals start zeroed
+    static int* base = nullptr;
+    static int next = 0;           // (launches are issued from one host thread per stream; a race only shares a slot)
+    if (!base && hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_ring_q)) != hipSuccess) base = nullptr;
+    if (!base) return nullptr;
+    int* p = base + 2 * RQ_MAXN * (next % RQ_SLOTS);
+    ++next;
+    return p;
 }
 
 template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, int STG>
@@ -1238,7 +1319,24 @@ int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RG::LDS);
         attr_set = true;
     }
-    kern<<<grid, RG::NW * 64, RG::LDS, s>>>(a, tiles, band);
+    RingDyn dyn{nullptr, 0, 0, 0};
+    if ((STG & 16) != 0) {
+        // the caller (launch_c64r_form) checked grid % N == 0; SG2_RING_DYN: percent of a sample's tiles handed out
+        // dynamically (default 12), the dynamic part a whole number of 2-tile chunks
+        static const int pct = [] { const char* e = getenv("SG2_RING_DYN"); return e ? std::max(0, std::min(50, atoi(e))) : 12; }();
+        const int per_n = tiles / a.N, gpn = grid / a.N;
+        int sp = std::max(2, (int)((int64_t)per_n * (100 - pct) / (100 * (int64_t)gpn)));
+        while (sp > 2 && (per_n - gpn * sp) % 2) --sp;
+        dyn.q = ring_queue_slot();
+        dyn.s_per_wg = sp;
+        dyn.wg_per_n = gpn;
+        dyn.nchunks = (per_n - gpn * sp) / 2;
+        if (!dyn.q || gpn * sp > per_n || (per_n - gpn * sp) % 2 || a.N > RQ_MAXN) {
+            set_error("sg2_conv3x3 (c64 ring): dynamic tail unavailable");
+            return -1;
+        }
+    }
+    kern<<<grid, RG::NW * 64, RG::LDS, s>>>(a, tiles, band, dyn);
     return launch_status("sg2_conv3x3 (c64 ring)");
 }
 
@@ -1248,22 +1346,30 @@ int launch_c64r_raw(const Conv3Args& a, hipStream_t s, int tiles, int grid, int 
                    : launch_c64r<T, SI, EPI, false, TH, WR, PIPE, STG>(a, s, tiles, grid, band);
 }
 
-// form: 4 = 32 x 4 tiles, two workgroups of 4 waves per CU; 8 = 32 x 8 tiles, one workgroup of 8 waves;
+// form: 4 = 32 x 4 tiles, two workgroups of 4 waves per CU; 46 = form 4 with the hoisted DMA issue (issue_fast,
+// the default); 8 = 32 x 8 tiles, one workgroup of 8 waves;
 // 44 = form 4 with whole-line stores staged through the consumed slot; 84 = 32 x 8 tiles, one workgroup of 4
 // waves with 4 rows each (one wave per SIMD, 512 registers).  (The PIPE
 // template form -- tile k - 1's epilogue beside tile k's MFMAs -- spills at 512 registers with the weights in
 // VGPRs and is not instantiated.)
 template <typename T, bool SI, bool EPI>
 int launch_c64r_form(const Conv3Args& a, hipStream_t s, int form) {
-    const int th = (form == 4 || (form >= 44 && form <= 47)) ? 4 : 8;
+    const int th = (form == 4 || form == 44 || form == 46 || form == 49) ? 4 : 8;
     const int tiles = a.N * (a.H / th) * (a.W / R_TW);
     const int ty = a.H / th;
     const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
     if (form == 4) return launch_c64r_raw<T, SI, EPI, 4, 2>(a, s, tiles, 2 * num_cus(), band);
     if (form == 44) return launch_c64r_raw<T, SI, EPI, 4, 2, false, 1>(a, s, tiles, 2 * num_cus(), band);
-    if (form == 45) return launch_c64r_raw<T, SI, EPI, 4, 2, false, 2>(a, s, tiles, 2 * num_cus(), band);
+
     if (form == 46) return launch_c64r_raw<T, SI, EPI, 4, 2, false, 4>(a, s, tiles, 2 * num_cus(), band);
-    if (form == 47) return launch_c64r_raw<T, SI, EPI, 4, 2, false, 6>(a, s, tiles, 2 * num_cus(), band);
+    if (form == 49) {     // the dynamic tail needs whole samples per workgroup group and >= 8 tiles per workgroup
+        const int grid = 2 * num_cus(), per_n = tiles / a.N;
+        if (grid % a.N == 0 && per_n / (grid / a.N) >= 8)
+            return launch_c64r_raw<T, SI, EPI, 4, 2, false, 20>(a, s, tiles, grid, band);
+        return launch_c64r_raw<T, SI, EPI, 4, 2, false, 4>(a, s, tiles, grid, band);
+    }
+
+
     if (form == 84) return launch_c64r_raw<T, SI, EPI, 8, 4>(a, s, tiles, num_cus(), band);
     return launch_c64r_raw<T, SI, EPI, 8, 2>(a, s, tiles, num_cus(), band);
 }
@@ -1284,10 +1390,12 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         return launch3<T, 32, false, false, 1, 2>(a, s);
     }
     static const bool persist = [] { const char* e = getenv("SG2_HALO_PERSIST"); return !e || atoi(e) != 0; }();
-    // SG2_C64_RING: 0 off, else the ring form (launch_c64r_form: 4 default, 8, 84)
+    // SG2_C64_RING: 0 off, else the ring form (launch_c64r_form: 49 default -- form 4 with the hoisted DMA issue
+    // and the per-sample dynamic tail, 0.146-0.150 ms on the bench launch against 0.154-0.156 for 46 (hoisted issue
+    // only) and 0.161 for 4, profiles/r05_ring_forms.txt --, 46, 4, 44, 8, 84)
     const char* ring_env = getenv("SG2_C64_RING");   // read per launch: tests switch forms in one process
-    const int ring = ring_env ? atoi(ring_env) : 4;
-    const int rth = (ring == 4 || (ring >= 44 && ring <= 47)) ? 4 : 8;
+    const int ring = ring_env ? atoi(ring_env) : 49;
+    const int rth = (ring == 4 || ring == 44 || ring == 46 || ring == 49) ? 4 : 8;
     if (ring && !a.dot_out && a.Cin == P_C && a.Cout == P_C && a.H % rth == 0 && a.W % R_TW == 0 &&
         ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 && ((uintptr_t)a.noise % 16) == 0 &&
         ((uintptr_t)a.out_scale % 16) == 0 && ((uintptr_t)a.in_scale % 16) == 0 &&
@@ -1297,7 +1405,7 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         // (the fast DMA issue marks an invalid halo row with base INT_MIN: the image must stay below 2^31 - 2^16 B)
         if (tiles >= 2 * grid && tiles <= 128 * grid && a.N < 4096 && a.H / rth < 1024 && a.W / R_TW < 1024 &&
             (int64_t)a.N * a.H * a.W * 64 * (int64_t)sizeof(T) < 0x7fff0000ll) {
-            const int form = (ring == 84 || (ring >= 44 && ring <= 47)) ? ring : rth;
+            const int form = (ring == 84 || ring == 44 || ring == 46 || ring == 49) ? ring : rth;
             if (si) { if (epi) return launch_c64r_form<T, true, true>(a, s, form); return launch_c64r_form<T, true, false>(a, s, form); }
             if (epi) return launch_c64r_form<T, false, true>(a, s, form);
             return launch_c64r_form<T, false, false>(a, s, form);

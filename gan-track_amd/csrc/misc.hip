@@ -3,6 +3,8 @@
 // fused in front, the G_ema lerp).  All HBM- or latency-bound.
 #include "sg2_common.h"
 
+#include <algorithm>
+
 namespace sg2 {
 namespace {
 
@@ -173,6 +175,63 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(Tout* __restrict__ out
     float v = to_f32(in[(int64_t)a * sa + (int64_t)b * sb + kk * sk]) * scale;
     asm volatile("" : "+v"(v));
     out[e] = from_f32<Tout>(v);
+}
+
+// Every conv-weight pack of a training phase in one launch per 64 packs (sg2_pack_weight_multi): workgroup b
+// serves elements [(b - blk0[d]) 1024, + 1024) of descriptor d with blk0[d] <= b < blk0[d + 1], and does for each what
+// pack_weight_kernel does for that descriptor -- the same element map, product and rounding, so each pack is
+// bitwise the single-launch pack.  The phase's packs (~40 per phase, 158 launches per step) were each a
+// few-microsecond launch.
+__device__ __forceinline__ float ld_any(const void* p, int64_t i, int dt) {
+    return dt == SG2_F32 ? ((const float*)p)[i] : dt == SG2_F16 ? (float)((const f16_t*)p)[i] : (float)((const bf16_t*)p)[i];
+}
+__device__ __forceinline__ void st_any(void* p, unsigned i, int dt, float v) {
+    if (dt == SG2_F32) ((float*)p)[i] = v;
+    else if (dt == SG2_F16) ((f16_t*)p)[i] = (f16_t)v;
+    else ((bf16_t*)p)[i] = (bf16_t)v;
+}
+// The table travels in the kernel arguments (scalar loads through the constant cache): a workgroup finds its
+// descriptor by a binary search over block0 there, with no dependent global loads before its element loads.
+// 1024 elements per workgroup, 4 per lane, every load of a lane issued before its first store.
+constexpr int PACK_PER_LAUNCH = 64, PACK_EPT = 4;
+struct PackDescK {
+    void* out;
+    const void* in;
+    int sa, sb, sk, A, B, K, block0;
+    float scale;
+    unsigned char out_dt, in_dt, flip, pad_;
+};
+struct PackTable {
+    PackDescK d[PACK_PER_LAUNCH];
+    int n;
+};
+__global__ __launch_bounds__(256) void pack_weight_multi_kernel(const PackTable t) {
+    const int b = blockIdx.x;
+    int lo = 0, hi = t.n - 1;                      // last d with block0 <= b (wave-uniform: scalar loads)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (t.d[mid].block0 <= b) lo = mid; else hi = mid - 1;
+    }
+    const PackDescK& d = t.d[lo];
+    const unsigned total = (unsigned)d.A * d.B * d.K;
+    const unsigned e0 = (unsigned)(b - d.block0) * (256u * PACK_EPT) + threadIdx.x;
+    float v[PACK_EPT];
+#pragma unroll
+    for (int j = 0; j < PACK_EPT; ++j) {
+        const unsigned e = e0 + j * 256u;
+        const unsigned ec = e < total ? e : total - 1;     // (a clamped index: loads stay in bounds, no branch)
+        const unsigned r = ec / (unsigned)d.B, bb = ec - r * d.B;
+        const unsigned a = r / (unsigned)d.K, k = r - a * d.K;
+        const int kk = d.flip ? d.K - 1 - (int)k : (int)k;
+        v[j] = ld_any(d.in, (int64_t)a * d.sa + (int64_t)bb * d.sb + kk * d.sk, d.in_dt) * d.scale;
+    }
+#pragma unroll
+    for (int j = 0; j < PACK_EPT; ++j) {
+        const unsigned e = e0 + j * 256u;
+        float x = v[j];
+        asm volatile("" : "+v"(x));              // (as pack_weight_kernel: the f32 product, then one rounding)
+        if (e < total) st_any(d.out, e, d.out_dt, x);
+    }
 }
 
 // Row-wise infinity-norm pre-normalisation of the fp16 modulated layers (networks_stylegan2.py:52-54):
@@ -435,6 +494,34 @@ extern "C" int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_
     SG2_DISPATCH(in_dtype, Tin, SG2_DISPATCH(out_dtype, Tout,
         pack_weight_kernel<Tin, Tout><<<grid, 256, 0, s>>>((Tout*)out, (const Tin*)in, A, B, K, sa, sb, sk, flip, scale)));
     return launch_status("sg2_pack_weight");
+}
+
+extern "C" int sg2_pack_weight_multi(const sg2_pack_desc* descs, int n, void* stream) {
+    using namespace sg2;
+    SG2_CHECK(descs != nullptr && n > 0, "sg2_pack_weight_multi: empty table");
+    hipStream_t s = as_stream(stream);
+    for (int i0 = 0; i0 < n; i0 += PACK_PER_LAUNCH) {
+        PackTable t{};
+        t.n = std::min(PACK_PER_LAUNCH, n - i0);
+        int blk = 0;
+        for (int j = 0; j < t.n; ++j) {
+            const sg2_pack_desc& d = descs[i0 + j];
+            SG2_CHECK(d.out && d.in && d.A > 0 && d.B > 0 && d.K >= 1 && d.K <= 9 &&
+                      (int64_t)d.A * d.B * d.K < (1LL << 31) && d.sa < (1LL << 31) && d.sb < (1LL << 31) &&
+                      d.sk < (1LL << 31) && d.sa >= 0 && d.sb >= 0 && d.sk >= 0,
+                      "sg2_pack_weight_multi: unsupported descriptor (K <= 9, A*B*K < 2^31, 32-bit strides)");
+            SG2_CHECK((d.in_dtype == SG2_F32 || d.in_dtype == SG2_F16 || d.in_dtype == SG2_BF16) &&
+                      (d.out_dtype == SG2_F32 || d.out_dtype == SG2_F16 || d.out_dtype == SG2_BF16),
+                      "sg2_pack_weight_multi: unsupported dtype");
+            t.d[j] = PackDescK{d.out, d.in, (int)d.sa, (int)d.sb, (int)d.sk, d.A, d.B, d.K, blk, d.scale,
+                               (unsigned char)d.out_dtype, (unsigned char)d.in_dtype, (unsigned char)(d.flip != 0), 0};
+            blk += (int)cdiv((int64_t)d.A * d.B * d.K, 256 * PACK_EPT);
+        }
+        pack_weight_multi_kernel<<<blk, 256, 0, s>>>(t);
+        const int rc = launch_status("sg2_pack_weight_multi");
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 extern "C" int sg2_infnorm_fwd(float* y, float* nrm, const float* t, int rows, int L, float c, int mode,

@@ -83,8 +83,9 @@ SIGNATURES = {
     'sg2_infnorm_bwd': [_vp, _vp, _vp, _vp, _i, _i, _f, _i, _vp],
     'sg2_infnorm_vjp_bwd': [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _f, _vp],
     'sg2_pack_weight': [_vp, _i, _vp, _i, _i, _i, _i, _i64, _i64, _i64, _i, _f, _vp],
+    'sg2_pack_weight_multi': [_vp, _i, _vp],
 }
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lib = None
 

@@ -18,6 +18,7 @@ import contextlib
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 import sg2hip as _hip
@@ -230,22 +231,79 @@ def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None, alpha=1.0,
 
 
 _pack_cache = None   # {key: packed} while a pack_cache() scope is open
+_pack_record = None  # the entries of the plan being recorded (pack_cache(plan=...) without a plan yet)
+prepack_enabled = os.environ.get('SG2_PREPACK', '1') != '0'
+
+
+class _PackPlan:
+    """Every parameter pack a training phase makes, done at the phase start in ONE sg2_pack_weight_multi launch
+    into persistent buffers (bitwise the per-call sg2_pack_weight results), which the phase's pack requests then
+    find in the cache: ~40 launches per phase (158 per step) become one per 64 packs.  Recorded from the phase's
+    first run; the buffers and the source addresses are fixed and the table travels in the kernel arguments, so the
+    launch can be captured into the phase's HIP graph and replayed after every optimiser step."""
+
+    DESC = np.dtype([('out', '<u8'), ('in', '<u8'), ('sa', '<i8'), ('sb', '<i8'), ('sk', '<i8'), ('out_dtype', '<i4'),
+                     ('in_dtype', '<i4'), ('A', '<i4'), ('B', '<i4'), ('K', '<i4'), ('flip', '<i4'), ('scale', '<f4'),
+                     ('block0', '<i4')])   # include/sg2hip.h sg2_pack_desc (72 bytes)
+
+    def __init__(self, entries):
+        self.entries = entries                   # (base param, storage offset, shape, stride, a_dim, dtype, flip, scale)
+        self.outs, rows = [], []
+        for base, off, shape, stride, a_dim, dtype, flip, scale in entries:
+            b_dim = 1 - a_dim
+            A, B, kh, kw = shape[a_dim], shape[b_dim], shape[2], shape[3]
+            out = torch.empty([A, kh, kw, B], dtype=dtype or base.dtype, device=base.device)
+            self.outs.append(out)
+            rows.append((out.data_ptr(), self._addr(base, off), stride[a_dim], stride[b_dim],
+                         stride[3], _hip._DTYPES[out.dtype], _hip._DTYPES[base.dtype], A, B, kh * kw, int(flip),
+                         float(scale), 0))                 # (block0: set by the library)
+        self.table = np.array(rows, dtype=self.DESC)   # host table: the library copies it into the launch arguments
+        self.src = [e[0].data_ptr() for e in entries]
+
+    @staticmethod
+    def _addr(base, off):
+        return base.untyped_storage().data_ptr() + off * base.element_size()
+
+    def valid(self):
+        return all(e[0].data_ptr() == p for e, p in zip(self.entries, self.src))
+
+    def run(self, cache):
+        dev = self.entries[0][0].device
+        _hip.check(_hip.lib().sg2_pack_weight_multi(self.table.ctypes.data, len(self.entries), _hip.stream_ptr(dev)),
+                   'sg2_pack_weight_multi')
+        for (base, off, shape, stride, a_dim, dtype, flip, scale), out in zip(self.entries, self.outs):
+            key = (self._addr(base, off), base._version, shape, stride, a_dim, dtype, bool(flip), float(scale))
+            cache[key] = (out, base)
 
 
 @contextlib.contextmanager
-def pack_cache():
+def pack_cache(plan=None):
     """Reuse weight packs inside the scope: a training phase packs every conv weight of D twice per form
     (the fake and the real pass of Dmain, their backward), with the parameters unchanged in between.  Only
     packs of parameters (or views of them) are cached, keyed by storage, version, view geometry and the
     pack form; the trainer opens one scope per phase (eagerly or while capturing the phase's graph), so
-    the optimizer step never runs inside one."""
-    global _pack_cache
-    prev = _pack_cache
+    the optimizer step never runs inside one.  plan: a dict owned by the caller (the trainer's phase) that holds
+    the scope's pack set under 'pack_plan': its first scope records the packs, later scopes make them all up front
+    in one launch (_PackPlan)."""
+    global _pack_cache, _pack_record
+    prev, prev_rec = _pack_cache, _pack_record
     _pack_cache = {} if prev is None else prev
+    recording = None
+    if plan is not None and prev is None and prepack_enabled:
+        pl = plan.get('pack_plan')
+        if pl is not None and not pl.valid():
+            pl = plan['pack_plan'] = None
+        if pl is not None:
+            pl.run(_pack_cache)
+        else:
+            recording = _pack_record = []
     try:
         yield
     finally:
         _pack_cache = prev
+        _pack_record = prev_rec
+        if recording and all(e[0].is_cuda for e in recording):
+            plan['pack_plan'] = _PackPlan(recording)
 
 
 def _pack(w, a_dim, dtype, flip, scale=1.0):
@@ -262,6 +320,10 @@ def _pack(w, a_dim, dtype, flip, scale=1.0):
     out = _pack_raw(w, a_dim, dtype, flip, scale)
     if key is not None:
         _pack_cache[key] = (out, w)    # (w keeps the parameter view alive for the scope)
+        if _pack_record is not None and w.dim() == 4 and w.shape[2] * w.shape[3] <= 9 and \
+                w.stride(2) == w.shape[3] * w.stride(3):
+            _pack_record.append((base, w.storage_offset(), tuple(w.shape), tuple(w.stride()), a_dim, dtype,
+                                 bool(flip), float(scale)))
     return out
 
 

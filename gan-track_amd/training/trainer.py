@@ -244,7 +244,9 @@ class Trainer:
 
     def _accumulate(self, phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c):
         chunks = list(zip(phase_real_img, phase_real_c, phase_gen_z, phase_gen_c))
-        with conv2d_gradfix.pack_cache():   # the phase's weights are fixed until its optimizer step
+        # the phase's weights are fixed until its optimizer step: every pack made once, all in one launch at the
+        # phase start from the second run on (the plan recorded by the first, kept on the phase)
+        with conv2d_gradfix.pack_cache(plan=phase):
             for ci, (real_img, real_c, gen_z, gen_c) in enumerate(chunks):
                 if ci == len(chunks) - 1:
                     passes = self.loss.backward_passes(phase.name, gen_z.shape[0] + real_img.shape[0]) \

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SG2_ABI_VERSION 7
+#define SG2_ABI_VERSION 8
 
 enum sg2_dtype { SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2, SG2_F32S3 = 3 };
 
@@ -332,6 +332,20 @@ int sg2_demod_vjp_bwd(float* g_dd, float* g_d, float* g_w, float* g_s, const flo
  * reference's `self.weight * self.weight_gain` (networks_stylegan2.py:173) in the same pass. */
 int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_dtype, int A, int B, int K, int64_t sa,
                     int64_t sb, int64_t sk, int flip, float scale, void* stream);
+
+/* Many packs in one launch per 64 (ABI 8): `descs` is a HOST array of n sg2_pack_desc (copied into the launch's
+ * kernel arguments, so the call can be captured into a hipGraph; block0 is ignored).  Each pack is bitwise what
+ * sg2_pack_weight computes for the same arguments; strides must fit 32 bits.  Used by conv2d_gradfix.pack_cache to
+ * pack all of a training phase's conv weights at the phase start. */
+typedef struct sg2_pack_desc {
+    void* out;
+    const void* in;
+    int64_t sa, sb, sk;
+    int out_dtype, in_dtype, A, B, K, flip;
+    float scale;
+    int block0;
+} sg2_pack_desc;
+int sg2_pack_weight_multi(const sg2_pack_desc* descs, int n, void* stream);
 
 /* fp16 range pre-normalisation, row-wise (SG3/training/networks_stylegan2.py:52-54): t [rows, L] f32,
  * n[r] = max_i |t[r,i]| (written to nrm [rows]); mode 0: y = t * ((1/n) * c)  (the weight, c = 1/sqrt(fan_in)),

@@ -520,6 +520,41 @@ def gen_conditioning(tag, cache_dir=None, perturb=2.0 ** -24):
     np.savez_compressed(path, **pack(z))
     print(tag, 'conditioning written', flush=True)
 
+def gen_emulated16_nudged(tag, dt, seed, cache_dir):
+    """One more sample of the emulated reference 16-bit evaluation: the same emulation (oracle EMU16) at the
+    fixture's state nudged by (1 +- 2^-24) (seeded signs; a state equal within f32 rounding), saved to
+    <cache_dir>/q16n_<tag>_<dt>_<seed>.npz; emu16merge folds the samples in as '<q16|qbf>n<seed>/...'.  The spread of
+    these samples is the reference's own 16-bit spread on each error measure (tests/test_config_gpu.py)."""
+    import config_parity as cp
+    path = os.path.join(OUT, f'train_{tag}.npz')
+    with np.load(path, allow_pickle=False) as f:
+        cfg, inp, tape, _ = cp.load_fixture(f)
+    out, _ = cp.run_oracle_f64(cfg, inp, tape, cfg.get('aug_p', 0.3), perturb=2.0 ** -24, perturb_seed=int(seed),
+                               isolated=cfg.get('isolated', False),
+                               emu16={'fp16': torch.float16, 'bf16': torch.bfloat16}[dt])
+    os.makedirs(cache_dir, exist_ok=True)
+    np.savez_compressed(os.path.join(cache_dir, f'q16n_{tag}_{dt}_{seed}.npz'), **pack(out))
+    print(tag, dt, seed, 'nudged 16-bit emulation sample written', flush=True)
+
+
+def merge_emulated16_nudged(tag, cache_dir):
+    from golden_init import unpack
+    import glob
+    path = os.path.join(OUT, f'train_{tag}.npz')
+    with np.load(path, allow_pickle=False) as f:
+        z = unpack(f)
+    z = {k: v for k, v in z.items() if not (k.startswith(('q16n', 'qbfn')))}
+    n = 0
+    for fn in sorted(glob.glob(os.path.join(cache_dir, f'q16n_{tag}_*.npz'))):
+        dt, seed = fn[:-4].rsplit('_', 2)[1:]
+        pre = {'fp16': 'q16', 'bf16': 'qbf'}[dt] + 'n' + seed
+        with np.load(fn, allow_pickle=False) as f:
+            z.update({f'{pre}/{k}': v for k, v in unpack(f).items()})
+        n += 1
+    np.savez_compressed(path, **pack(z))
+    print(tag, n, 'nudged 16-bit emulation samples merged', flush=True)
+
+
 def gen_emulated16(tag, dt):
     """Add 'q16/...' (dt fp16) or 'qbf/...' (bf16) to train_<tag>.npz: the oracle's emulation of the reference's
     16-bit GPU evaluation of the fixture (oracle.sg2_oracle.EMU16: the num_fp16_res = 4 blocks round every tensor
@@ -597,6 +632,11 @@ if __name__ == '__main__':
         if w.startswith('emu:'):           # emu:<tag>:<fp16|bf16>
             parts = w.split(':')
             gen_emulated16(parts[1], parts[2])
+        if w.startswith('emu16n:'):        # emu16n:<tag>:<fp16|bf16>:<seed>   (to $GOLD_CACHE)
+            parts = w.split(':')
+            gen_emulated16_nudged(parts[1], parts[2], parts[3], os.environ.get('GOLD_CACHE', '/tmp/gold'))
+        if w.startswith('emu16nmerge:'):   # emu16nmerge:<tag>
+            merge_emulated16_nudged(w.split(':')[1], os.environ.get('GOLD_CACHE', '/tmp/gold'))
         if w.startswith('emu32:'):         # emu32:<tag>:<sample k>   (to $GOLD_CACHE, default /tmp/gold)
             parts = w.split(':')
             gen_emulated32(parts[1], parts[2], os.environ.get('GOLD_CACHE', '/tmp/gold'))

@@ -203,4 +203,4 @@ def test_train_iteration_c1_width():
     worst, _ = judge_f32(got, fix)
     judge_stats_f32(stats, fix)
     judge_pl_mean(got, fix)
-    print({k: tuple(f'{x:.2g}' for x in v[:4]) for k, v in worst.items()})
+    print({k: tuple(f'{x:.2g}' for x in v[:4]) for k, v in worst.items() if isinstance(v, tuple)}, worst.get('bound_terms'))

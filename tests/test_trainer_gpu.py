@@ -139,3 +139,68 @@ def test_graph_exchange_overlap_simulated_ranks(monkeypatch):
         return sorted(d, reverse=True)[:4]
     assert rel_err(res[1], res[0]) < 1e-6, worst(res[1], res[0])
     assert rel_err(res[2], res[0]) < 1e-5, worst(res[2], res[0])
+
+
+def test_pack_weight_multi_bitwise():
+    """sg2_pack_weight_multi (every pack of a phase in one launch) == the per-call sg2_pack_weight, bitwise, over
+    mixed dtypes, transposed views, flips and gains."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    g = torch.Generator().manual_seed(3)
+    ws = [torch.nn.Parameter(torch.randn(s, generator=g).to(DEV)) for s in [(512, 512, 3, 3), (64, 1, 1, 1),
+                                                                            (3, 70, 3, 3), (96, 40, 3, 3)]]
+    forms = [(ws[0], 0, torch.float16, False, 0.04), (ws[0], 1, torch.bfloat16, True, 1.0), (ws[1], 0, None, False, 2.0),
+             (ws[2], 0, torch.float16, True, 0.5), (ws[3].transpose(0, 1), 0, torch.float16, False, 1.0),
+             (ws[3], 1, torch.float32, True, 0.25)]
+    ref = [cg._pack_raw(w, a, dt, fl, sc) for w, a, dt, fl, sc in forms]
+    holder = {}
+    for rnd in range(2):                          # first scope records the plan, the second packs up front
+        with cg.pack_cache(plan=holder):
+            got = [cg._pack(w, a, dt, fl, sc) for w, a, dt, fl, sc in forms]
+        assert (holder.get('pack_plan') is not None) and (rnd == 0 or all(
+            any(o.data_ptr() == x.data_ptr() for o in holder['pack_plan'].outs) for x in got))
+        for a, b in zip(got, ref):
+            assert a.dtype == b.dtype and torch.equal(a, b)
+
+
+@pytest.mark.parametrize('graphs', [False, True], ids=['eager', 'graph'])
+def test_prepack_steps_bitwise(graphs):
+    """Training steps with the phase-start multi-pack (conv2d_gradfix._PackPlan) == without it, bitwise (fp16
+    network, deterministic mode): the packs it makes up front are the packs the phase would make."""
+    import sg2hip
+    from training.trainer import Trainer
+    from golden_util import load
+    from parity_train import build_product, CLARO_AUG
+    from training import augment_mi, loss as loss_mod
+    from torch_utils.ops import conv2d_gradfix as cg
+    z = load('train_claro.npz')
+    res = []
+    for pre in (False, True):
+        cg.prepack_enabled = pre
+        try:
+            cfg, G, D = build_product(z, DEV, fp16=True)
+            G_ema = copy.deepcopy(G).eval()
+            aug = augment_mi.AugmentPipe(run_dir=None, batch_size=cfg['batch'], **CLARO_AUG).train().requires_grad_(False).to(DEV)
+            aug.p.copy_(torch.as_tensor(0.3))
+            loss = loss_mod.StyleGAN2Loss(device=DEV, G=G, D=D, augment_pipe=aug, r1_gamma=0.4096, style_mixing_prob=0.9,
+                                          pl_weight=2, pl_no_weight_grad=True)
+            opt = dict(class_name='torch.optim.Adam', lr=0.0025, betas=[0, 0.99], eps=1e-8)
+            tr = Trainer(G, D, G_ema, loss, opt, opt, G_reg_interval=2, D_reg_interval=2, batch_size=cfg['batch'],
+                         batch_gpu=cfg['batch'], num_gpus=1, rank=0, device=DEV)
+            gen = torch.Generator(device=DEV)
+            gen.manual_seed(5)
+            torch.manual_seed(123)
+            with sg2hip.deterministic(device=DEV):
+                for it in range(5):
+                    if it == 2:
+                        tr.graphs = graphs
+                    real = torch.rand([cfg['batch'], 1, 32, 32], device=DEV, generator=gen) * 2 - 1
+                    c = torch.nn.functional.one_hot(torch.randint(0, 2, [cfg['batch']], device=DEV, generator=gen), 2).float()
+                    gz = torch.randn([4, cfg['batch'], cfg['z_dim']], device=DEV, generator=gen)
+                    tr.step([real], [c], [[gz[i]] for i in range(4)], [[c] for _ in range(4)])
+                torch.cuda.synchronize()
+            if pre:
+                assert all(ph.get('pack_plan') is not None for ph in tr.phases), 'a phase recorded no pack plan'
+            res.append(torch.cat([p.detach().double().flatten() for m in (G, D, G_ema) for p in m.parameters()]))
+        finally:
+            cg.prepack_enabled = True
+    assert torch.equal(res[0], res[1])

@@ -22,7 +22,7 @@ res = []
 for r in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
     ms, fl, by = bench._layer_launch(dev, 256, 64, torch.float16)
     res.append(ms)
-print(f"ring={os.environ.get('SG2_C64_RING', '1')} dbg={os.environ.get('SG2_RING_DBG', '0')} fused launch ms "
+print(f"ring={os.environ.get('SG2_C64_RING', '49')} dbg={os.environ.get('SG2_RING_DBG', '0')} fused launch ms "
       f"{' '.join(f'{m:.4f}' for m in res)}  best frac {by / (min(res) * 1e-3) / 8e12:.3f}", flush=True)
 # plain conv (D layer form: bias + lrelu, no modulation) and the dgrad DOT form
 N, C, R = 32, 64, 256

@@ -23,9 +23,9 @@ print(f'launch {ms:.4f} ms (diag build, stamps on)', flush=True)
 lib = sg2hip.lib()
 f = lib.sg2_diag_ring_stamps
 f.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
-buf = np.zeros(4096 * 8, dtype=np.uint64)
+buf = np.zeros(4096 * 10, dtype=np.uint64)
 assert f(buf.ctypes.data, buf.nbytes) == 0
-r = buf.reshape(4096, 8)
+r = buf.reshape(4096, 10)
 r = r[r[:, 5] > 0]
 ntile = (r[:, 7] & 0xffff).astype(np.float64)
 names = ['issue DMAs', 'MFMAs', 'epilogue+stores', 'DMA wait', 'barrier']
@@ -39,4 +39,15 @@ hw = (r[:, 7] >> 32).astype(np.int64)
 simd = (hw >> 4) & 3
 wave_slot = hw & 15
 xcc = ((r[:, 7] >> 16) & 0xffff).astype(np.int64) & 0xf
+dt_clk = r[:, 6].astype(np.float64) - r[:, 5].astype(np.float64)
+dt_rt = (r[:, 9].astype(np.float64) - r[:, 8].astype(np.float64)) / 100e6          # s_memrealtime: 100 MHz
+st_rt = (r[:, 8].astype(np.float64) - r[:, 8].min()) / 100e6 * 1e6
+print(f'in-kernel clock {np.median(dt_clk / dt_rt) / 1e9:.3f} GHz (median over waves; p10 '
+      f'{np.percentile(dt_clk / dt_rt, 10) / 1e9:.3f}, p90 {np.percentile(dt_clk / dt_rt, 90) / 1e9:.3f}); wave lifetime '
+      f'{np.median(dt_rt) * 1e3:.4f} ms median, {dt_rt.max() * 1e3:.4f} max; start spread {st_rt.max():.1f} us')
+lt = dt_rt * 1e3
+print('wave lifetime ms percentiles p10/p50/p90/p99/max', ' '.join(f'{np.percentile(lt, q):.4f}' for q in (10, 50, 90, 99, 100)))
+xc = ((r[:, 7] >> 16) & 0xffff).astype(np.int64) & 0xf
+print('per-XCD median / max lifetime ms', ' '.join(f'{np.median(lt[xc == x]):.4f}/{lt[xc == x].max():.4f}' for x in range(8)))
+print('per-XCD clock GHz', ' '.join(f'{np.median((dt_clk / dt_rt)[xc == x]) / 1e9:.3f}' for x in range(8)))
 print('simd histogram', np.bincount(simd, minlength=4).tolist(), 'xcc histogram', np.bincount(xcc, minlength=8).tolist())
