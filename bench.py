@@ -216,8 +216,11 @@ def roofline(device, res, cbase, dtype, N=32):
     gbps = byts / (ms * 1e-3) / 1e9
     tflops = flops / (ms * 1e-3) / 1e12
     ring = C == 64 and os.environ.get('SG2_C64_RING', '49') != '0'
+    ring32 = C == 32 and os.environ.get('SG2_C32_RING', '1') != '0'
     kname = ('conv3x3_c64r_kernel (LDS-DMA halo ring, weights in registers)' if ring else
-             'conv3x3_c64p_kernel (persistent, weights in LDS)') if C == 64 else 'conv3x3_halo_kernel'
+             'conv3x3_c64p_kernel (persistent, weights in LDS)') if C == 64 else (
+        'conv3x3_c32r_kernel (LDS-DMA halo ring, 32 x 8 tiles, weights in registers)' if ring32 else
+        'conv3x3_halo_kernel')
     out = {'kernel': f'{kname} ({key}: modulation + demod/noise/bias/lrelu/clamp epilogue)'}
     if ai < ridge:
         out.update({'bound': 'hbm', 'achieved': round(gbps, 1), 'peak': HBM_PEAK, 'unit': 'GB/s',
@@ -225,7 +228,7 @@ def roofline(device, res, cbase, dtype, N=32):
     else:
         out.update({'bound': 'mfma', 'achieved': round(tflops, 2), 'peak': MFMA_PEAK_FP16, 'unit': 'TFLOP/s',
                     'frac': round(tflops / MFMA_PEAK_FP16, 4)})
-    traffic, traffic_x2 = _measured_traffic(key, kname.split()[0] if C == 64 else 'conv3x3_halo_kernel')
+    traffic, traffic_x2 = _measured_traffic(key, kname.split()[0])
     out.update({'traffic': traffic, 'traffic_fetch_x2_rule': traffic_x2, 'ms_per_launch': round(ms, 4),
                 'algorithmic_flops_per_launch': flops, 'algorithmic_hbm_bytes_per_launch': byts,
                 'arithmetic_intensity': round(ai, 1), 'ridge': round(ridge, 1),

@@ -1374,6 +1374,270 @@ int launch_c64r_form(const Conv3Args& a, hipStream_t s, int form) {
     return launch_c64r_raw<T, SI, EPI, 8, 2>(a, s, tiles, num_cus(), band);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Ring form of the 32 -> 32 channel layer (the 1024^2 layers of the cbase-32768 networks, BASELINE C5), round 5.
+// The C = 64 ring above in 64-byte positions: a pixel line is 32 channels (64 B), so one 1 KiB LDS-DMA
+// wave-instruction brings 16 halo positions (4 lanes a position) and one 16-byte output store per lane and
+// fragment writes 16 consecutive whole pixels (1 KiB contiguous).  The generic halo kernel ran this layer with half
+// of every output-channel tile idle (64-wide tiles of 32 channels) at 0.17 of HBM.
+//   * tile 32 x 8 pixels, 4 waves, wave w: rows 2w, 2w+1 (4 fragments of 16 pixels) x all 32 output channels;
+//     per tap 4 ds_read_b128 (pixels) feed 8 MFMAs, weights (2 A fragments a tap, one 32-channel chunk: 72 VGPRs)
+//     in registers, re-modulated when the run crosses into a new sample;
+//   * halo slot: 10 rows x 40 positions of 64 B (34 used a row; the pitch keeps position mod 4 a function of the lane
+//     and the tap column: per-lane base + immediate reads), XOR-swizzled as swz64 on the DMA source address;
+//     25 DMA pieces a tile (16 consecutive positions each, rows crossed per lane), 2-slot ring, two workgroups per
+//     CU; the pieces' per-lane halo offsets and border classes are computed once, a tile adds its base and masks
+//     the border lanes (out-of-range loads read zeros);
+//   * epilogue ring (noise 8 x 32 and demod 32 of a tile in one 1 KiB DMA) and the epilogue math of the C = 64 form.
+constexpr int Q_TW = 32, Q_TH = 8, Q_PITCH = 40, Q_HPOS = (Q_TH + 2) * Q_PITCH;   // 400 positions
+constexpr int Q_SLOT = Q_HPOS * 64;                                                // 25,600 B
+constexpr int Q_PIECES = Q_HPOS / 16;                                              // 25
+constexpr int Q_DMA = 7;                                                           // per wave: 28 slots >= 25 + 1
+constexpr int Q_NEPI = 4, Q_EPI = 1024;
+constexpr size_t Q_LDS = 2 * (size_t)Q_SLOT + Q_NEPI * Q_EPI + 32 * 4;
+
+template <typename T, bool SI, bool EPI, bool RAW>
+__global__ __launch_bounds__(256, 2) void conv3x3_c32r_kernel(Conv3Args a, int tiles_total, int band) {
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    constexpr int NF = 4;
+    constexpr int S = (RAW ? 2 : 1) * NF;             // buffer stores per wave and tile
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    char* epil = smem_raw + 2 * Q_SLOT;
+    float* blds = (float*)(epil + Q_NEPI * Q_EPI);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l16 = lane & 15, q = lane >> 4;
+    const int t_begin = (int)((int64_t)blockIdx.x * tiles_total / gridDim.x);
+    const int t_end = (int)((int64_t)(blockIdx.x + 1) * tiles_total / gridDim.x);
+    if (t_begin >= t_end) return;
+    auto pack_tile = [&](int t) -> int {
+        const int tiles_x = a.W / Q_TW, per_n = tiles_x * (a.H / Q_TH), per_band = band * tiles_x;
+        const int n = t / per_n, r = t - n * per_n, b = r / per_band, rb = r - b * per_band, col = rb / band;
+        return (n << 20) | ((b * band + rb - col * band) << 10) | col;
+    };
+    const int tinfo0 = t_begin + lane < t_end ? pack_tile(t_begin + lane) : 0;
+    const int tinfo1 = t_begin + 64 + lane < t_end ? pack_tile(t_begin + 64 + lane) : 0;
+    auto tile_of = [&](int t, int& n, int& ty, int& tx) {
+        const int j = t - t_begin;
+        const int v = j < 64 ? __builtin_amdgcn_readlane(tinfo0, j) : __builtin_amdgcn_readlane(tinfo1, j - 64);
+        n = (int)((unsigned)v >> 20);
+        ty = ((v >> 10) & 1023) * Q_TH;
+        tx = (v & 1023) * Q_TW;
+    };
+    const int xbytes = __builtin_amdgcn_readfirstlane(a.N * a.H * a.W * 32 * (int)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(a.x, xbytes);
+    const __amdgpu_buffer_rsrc_t rwb = make_rsrc(a.w, 32 * 9 * 32 * (int)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rsc = make_rsrc(a.in_scale, SI ? __builtin_amdgcn_readfirstlane(a.N * 32 * 4) : 0);
+    const __amdgpu_buffer_rsrc_t ryb = make_rsrc(a.y, xbytes);
+    const __amdgpu_buffer_rsrc_t ryr = make_rsrc(a.y_raw, RAW ? xbytes : 0);
+
+    // ---- weights: 2 x 9 A fragments (rows: output channels p_chan(16 jj + m), cols: the 32 input channels) ----
+    vec8 wf[2][9];
+    auto load_weights = [&](int n) {
+        float4 s4[2];
+        if (SI) {
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) s4[hh] = buf_load16<float4>(rsc, (n * 32 + q * 8 + hh * 4) * 4);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int o = p_chan(16 * jj + l16);
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                vec8 v = buf_load16<vec8>(rwb, ((o * 9 + tap) * 32 + q * 8) * (int)sizeof(T));
+                if (SI) {
+                    const float4 x0 = s4[0], x1 = s4[1];
+                    const vec8 sv = vec8{(T)x0.x, (T)x0.y, (T)x0.z, (T)x0.w, (T)x1.x, (T)x1.y, (T)x1.z, (T)x1.w};
+                    if constexpr (std::is_same<T, f16_t>::value) {
+                        v = v * sv;                    // round(w * round(s)), as the C = 64 ring
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] = (T)((float)v[e] * (float)sv[e]);
+                    }
+                }
+                wf[jj][tap] = v;
+            }
+        }
+    };
+    int cur_n;
+    {
+        int ty, tx;
+        tile_of(t_begin, cur_n, ty, tx);
+    }
+    load_weights(cur_n);
+    if (tid < 32) blds[tid] = (EPI && a.bias) ? (float)(T)a.bias[tid] * a.gain : 0.f;
+
+    // ---- DMA geometry: wave w issues pieces i = u * 4 + w (u < Q_DMA); piece i < 25: halo positions 16 i + lane / 4
+    // (4 lanes a position), i = 25 + ...: the epilogue table ----
+    const bool has_noise = EPI && a.noise != nullptr, has_d = EPI && a.out_scale != nullptr;
+    const char* epi_src0 = has_noise ? (const char*)a.noise : (has_d ? (const char*)a.out_scale : (const char*)a.x);
+    const char* epi_src1 = has_d ? (const char*)a.out_scale : epi_src0;
+    int hoff[Q_DMA], hcls[Q_DMA];                     // per piece: this lane's halo offset (bytes) and border class
+#pragma unroll
+    for (int u = 0; u < Q_DMA; ++u) {
+        const int i = u * 4 + wave;
+        const int p = 16 * i + (lane >> 2);
+        const int hy = p / Q_PITCH, hx = p - hy * Q_PITCH;
+        const int j = (lane & 3) ^ ((p >> 1) & 2);    // swz64 on the source side (lane-linear destination)
+        hoff[u] = (hy * a.W + hx) * 64 + j * 16;
+        hcls[u] = (hy == 0 ? 1 : 0) | (hy == Q_TH + 1 ? 2 : 0) | (hx == 0 ? 4 : 0) | (hx == Q_TW + 1 ? 8 : 0) |
+                  (hx >= Q_TW + 2 ? 16 : 0) | (i >= Q_PIECES ? 16 : 0);
+    }
+    // epilogue table: lanes 0-31 the tile's noise (row lane / 4, 16-byte piece lane % 4 of the row's 64 B), lanes
+    // 32-63 the sample's 32 demodulation scales (128 B; lanes 40-63 repeat 32-39)
+    const int elane = lane < 32 ? (has_noise ? ((lane >> 2) * a.W * (int)sizeof(T) + (lane & 3) * 16) : 0)
+                                : ((lane - 32) & 7) * 16;
+    auto issue = [&](int t, int slot, int eslot) {
+        int n, ty, tx;
+        tile_of(t, n, ty, tx);
+        const int tbase = ((n * a.H + ty - 1) * a.W + tx - 1) * 64;
+        const int flags = (ty == 0 ? 1 : 0) | (ty + Q_TH == a.H ? 2 : 0) | (tx == 0 ? 4 : 0) | (tx + Q_TW == a.W ? 8 : 0) | 16;
+        char* sb = smem_raw + slot * Q_SLOT;
+#pragma unroll
+        for (int u = 0; u < Q_DMA; ++u) {
+            const int i = u * 4 + wave;               // wave-uniform
+            if (i < Q_PIECES) {
+                const int off = (hcls[u] & flags) ? -1 : tbase + hoff[u];
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rxb, (lds_ptr_t)(sb + i * 1024), 16, off, 0, 0, 0);
+            } else if (i == Q_PIECES || u == Q_DMA - 1) {   // (the last round: every wave past the halo loads the
+                // table -- duplicates write the same bytes -- so each wave issues Q_DMA instructions a tile)
+                const char* nb = has_noise ? epi_src0 + (int64_t)((n * a.H + ty) * a.W + tx) * (int)sizeof(T) : epi_src0;
+                const char* db = has_d ? epi_src1 + n * 128 : epi_src1;
+                const char* src = (lane < 32 ? nb : db) + elane;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                 (lds_ptr_t)(epil + eslot * Q_EPI), 16, 0, 0);
+            }
+        }
+    };
+
+    // B fragment i at tap (ky, kx): position (2 wave + (i >> 1) + ky) * 40 + (i & 1) * 16 + l16 + kx, piece q
+    int boff[3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+        const int x = l16 + kx;
+        boff[kx] = (2 * wave * Q_PITCH + x) * 64 + ((q ^ ((x >> 1) & 2)) << 4);
+    }
+    const float lr_alpha = (EPI && a.act == 1) ? a.alpha : 1.f;
+    const float clampv = (EPI && a.clamp >= 0.f) ? a.clamp : __builtin_inff();
+    const float ngain = a.noise_gain * a.gain;
+    const int ch0 = 8 * q;                            // this lane's 8 output channels
+
+    auto epi_table = [&](int eslot, float (&bb)[8], float (&dd)[8], float (&nz)[NF]) {
+        if (!EPI) return;
+        const unsigned et = lds_addr(epil + eslot * Q_EPI);
+        float4 b0, b1, d0, d1;
+        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
+                     "ds_read_b128 %2, %5 offset:512\n\tds_read_b128 %3, %5 offset:528\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(b0), "=&v"(b1), "=&v"(d0), "=&v"(d1)
+                     : "v"(lds_addr(blds + ch0)), "v"(et + ch0 * 4));
+        const float bq[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        const float dq[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            bb[e] = bq[e];
+            dd[e] = has_d ? dq[e] * a.gain : a.gain;
+        }
+        // pixel (2 wave + (i >> 1)) * 32 + (i & 1) * 16 + l16: byte 32 i from na
+        const unsigned na = et + (2 * wave * Q_TW + l16) * (unsigned)sizeof(T);
+        unsigned r0, r1, r2, r3;
+        asm volatile("ds_read_u16 %0, %4\n\tds_read_u16 %1, %4 offset:32\n\tds_read_u16 %2, %4 offset:64\n\t"
+                     "ds_read_u16 %3, %4 offset:96\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3) : "v"(na));
+        const unsigned rr[4] = {r0, r1, r2, r3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nz[j] = has_noise ? (float)__builtin_bit_cast(T, (unsigned short)rr[j]) * ngain : 0.f;
+    };
+    auto epi_store = [&](f32x4 (&A)[NF][2], int n, int ty, int tx, const float (&bb)[8], const float (&dd)[8],
+                         const float (&nz)[NF]) {
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int r = 2 * wave + (i >> 1), px = (i & 1) * 16 + l16;
+            const int pix = (n * a.H + ty + r) * a.W + tx + px;
+            vec8 yv, rv;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float cv = A[i][e >> 2][e & 3];
+                if (RAW) rv[e] = (T)cv;
+                float v = cv;
+                if (EPI) {
+                    v = fmaf(v, dd[e], nz[i] + bb[e]);
+                    v = fmaxf(v, v * lr_alpha);
+                    v = __builtin_amdgcn_fmed3f(v, -clampv, clampv);
+                }
+                yv[e] = (T)v;
+            }
+            const int dst = (pix * 32 + ch0) * (int)sizeof(T);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, yv), ryb, dst, 0, 0);
+            if (RAW) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, rv), ryr, dst, 0, 0);
+        }
+    };
+    auto mfma_tile = [&](f32x4 (&A)[NF][2], const char* hb) {
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                v8<T> pf[NF];
+#pragma unroll
+                for (int i = 0; i < NF; ++i)
+                    pf[i] = *(const v8<T>*)(hb + boff[kx] + (((i >> 1) + ky) * Q_PITCH + (i & 1) * 16) * 64);
+                const bool first = ky == 0 && kx == 0;
+#pragma unroll
+                for (int i = 0; i < NF; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj)
+                        A[i][jj] = mma<T>(wf[jj][ky * 3 + kx], pf[i], first ? f32x4{0.f, 0.f, 0.f, 0.f} : A[i][jj]);
+            }
+    };
+
+    issue(t_begin, 0, 0);
+    wait_vm<0>();
+    __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0): the bias table
+    __builtin_amdgcn_s_barrier();
+    f32x4 acc[NF][2];
+    int k = 0;
+    for (int t = t_begin; t < t_end; ++t, ++k) {
+        const int slot = k & 1;
+        issue(min(t + 1, t_end - 1), slot ^ 1, (k + 1) % Q_NEPI);
+        int n, ty, tx;
+        tile_of(t, n, ty, tx);
+        if (SI && n != cur_n) {                       // a new sample: re-modulate the weights
+            cur_n = n;
+            load_weights(n);
+        }
+        mfma_tile(acc, smem_raw + slot * Q_SLOT);
+        float bb[8], dd[8], nz[NF];
+        epi_table(k % Q_NEPI, bb, dd, nz);
+        epi_store(acc, n, ty, tx, bb, dd, nz);
+        wait_vm<S>();                                 // tile t + 1's DMAs landed (younger: this tile's stores)
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_s_barrier();
+    }
+    wait_vm<0>();                                     // no LDS-DMA may outlive the workgroup
+}
+
+template <typename T, bool SI, bool EPI, bool RAW>
+int launch_c32r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band) {
+    auto kern = conv3x3_c32r_kernel<T, SI, EPI, RAW>;
+    static bool attr_set = false;   // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)Q_LDS);
+        attr_set = true;
+    }
+    kern<<<grid, 256, Q_LDS, s>>>(a, tiles, band);
+    return launch_status("sg2_conv3x3 (c32 ring)");
+}
+
+template <typename T, bool SI, bool EPI>
+int launch_c32r_raw(const Conv3Args& a, hipStream_t s) {
+    const int tiles = a.N * (a.H / Q_TH) * (a.W / Q_TW);
+    const int ty = a.H / Q_TH;
+    const int band = ty % 4 == 0 ? 4 : (ty % 2 == 0 ? 2 : 1);
+    const int grid = 2 * num_cus();
+    return a.y_raw ? launch_c32r<T, SI, EPI, true>(a, s, tiles, grid, band)
+                   : launch_c32r<T, SI, EPI, false>(a, s, tiles, grid, band);
+}
+
 template <typename T>
 int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     const bool si = a.in_scale != nullptr;
@@ -1390,6 +1654,23 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         return launch3<T, 32, false, false, 1, 2>(a, s);
     }
     static const bool persist = [] { const char* e = getenv("SG2_HALO_PERSIST"); return !e || atoi(e) != 0; }();
+    {
+        // the C = 32 ring (SG2_C32_RING=0: off)
+        const char* e32 = getenv("SG2_C32_RING");     // read per launch: tests switch it in one process
+        const bool ring32 = !e32 || atoi(e32) != 0;
+        const int tiles = a.H % Q_TH == 0 && a.W % Q_TW == 0 ? a.N * (a.H / Q_TH) * (a.W / Q_TW) : 0;
+        const int grid = 2 * num_cus();
+        if (ring32 && !a.dot_out && a.Cin == 32 && a.Cout == 32 && tiles >= 2 * grid && tiles <= 128 * grid &&
+            a.N < 4096 && a.H / Q_TH < 1024 && a.W / Q_TW < 1024 &&
+            (int64_t)a.N * a.H * a.W * 32 * (int64_t)sizeof(T) < 0x7fff0000ll &&
+            ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 && ((uintptr_t)a.noise % 16) == 0 &&
+            ((uintptr_t)a.out_scale % 16) == 0 && ((uintptr_t)a.in_scale % 16) == 0 && (a.W * (int)sizeof(T)) % 16 == 0 &&
+            (!epi || (a.gain > 0.f && (a.act == 0 || (a.alpha >= 0.f && a.alpha <= 1.f))))) {
+            if (si) { if (epi) return launch_c32r_raw<T, true, true>(a, s); return launch_c32r_raw<T, true, false>(a, s); }
+            if (epi) return launch_c32r_raw<T, false, true>(a, s);
+            return launch_c32r_raw<T, false, false>(a, s);
+        }
+    }
     // SG2_C64_RING: 0 off, else the ring form (launch_c64r_form: 49 default -- form 4 with the hoisted DMA issue
     // and the per-sample dynamic tail, 0.146-0.150 ms on the bench launch against 0.154-0.156 for 46 (hoisted issue
     // only) and 0.161 for 4, profiles/r05_ring_forms.txt --, 46, 4, 44, 8, 84)

@@ -348,28 +348,35 @@ def judge_f32(got, fix, floors=F32_FLOORS, factor=4.0, group_factor=3.0,
     return worst, sorted(ratios)
 
 
-def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, groups=('grad/',), check=True):
+def judge_vs_reference(got, fix, well=1e-4, tol=3e-4, factor=4.0, groups=('grad/',), check=True):
     """Direct product-vs-reference-f32 check on every tensor the reference's f32 result gets right (both its
-    norm and its sampled entries within `well` of the float64 answer): the product must then agree with the
-    reference itself to `tol` on both measures.  Gradients only: a parameter after Adam's first step (beta1 = 0) moves each entry by
+    norm and its sampled entries within `well` of the float64 answer, in its run and every re-evaluation): the
+    product must then agree with the reference itself to max(tol, (factor + 1) x R) on each measure, R the
+    reference's spread on that measure (judge_f32's R_k) -- the triangle bound of judge_f32's per-tensor
+    allowance (factor x R from float64) plus the reference's own distance from float64; measured: C4 Gmain
+    b256.torgb.affine.bias, whose reference re-evaluations spread its sampled entries by 9.7e-5 of the rms.  Gradients only: a parameter after Adam's first step (beta1 = 0) moves each entry by
     about lr * sign(g), so an entry whose gradient is zero up to rounding lands 2 lr apart in two correct
     evaluations (measured: D1/b512.conv1.bias at C4 / p = 0); the parameters are held by the flat check.
-    Returns (number of tensors checked, worst error, its key)."""
+    Returns (number of tensors checked, worst ratio to the bound, its key)."""
     truth = {k[4:]: v for k, v in fix.items() if k.startswith('f64/')}
     conds = _conditioning(fix)
     keys = sorted(set(_keys(truth, groups)) & set(_keys(got, groups)))
     n, worst, wk, fails = 0, 0.0, '', []
     for k in keys:
         rn, rs_ = _tensor_errs(fix, truth, k)
-        cn = max([0.0] + [max(_tensor_errs(c, truth, k)) for _, c in conds if k + '/norm' in c])
-        if max(rn, rs_, cn) >= well or float(fix[k + '/norm']) == 0.0:
+        for _, c in conds:
+            if k + '/norm' in c:
+                cn, cs = _tensor_errs(c, truth, k)
+                rn, rs_ = max(rn, cn), max(rs_, cs)
+        if max(rn, rs_) >= well or float(fix[k + '/norm']) == 0.0:
             continue
         n += 1
         en, es = _tensor_errs(got, fix, k)
-        if max(en, es) > worst:
-            worst, wk = max(en, es), k
-        if en > tol or es > tol:
-            fails.append(f'{k}: vs reference f32 norm {en:.3g} samples {es:.3g} > {tol}')
+        tn, ts = max(tol, (factor + 1) * rn), max(tol, (factor + 1) * rs_)
+        if max(en / tn, es / ts) > worst:
+            worst, wk = max(en / tn, es / ts), k
+        if en > tn or es > ts:
+            fails.append(f'{k}: vs reference f32 norm {en:.3g} (bound {tn:.3g}) samples {es:.3g} (bound {ts:.3g})')
     if check:
         assert not fails, f'{len(fails)} of {n} well-conditioned tensors differ from the reference: {fails[0]}'
     return n, worst, wk

@@ -1385,6 +1385,60 @@ def test_conv3x3_c64_ring(dtype, shape, form, ring, monkeypatch):
     assert rel_err(y.float()[..., edge], ref[..., edge]) < 2 * tol
 
 
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(4, 256, 256), (3, 344, 320), (2, 512, 256), (5, 104, 512)])
+@pytest.mark.parametrize('form', ['mod_epi_raw', 'mod_epi', 'mod_only', 'plain_epi', 'plain', 'epi_no_noise'])
+@pytest.mark.parametrize('ring32', ['1', '0'])
+def test_conv3x3_c32_ring(dtype, shape, form, ring32, monkeypatch):
+    """The 32 -> 32 channel ring kernel (conv3x3.hip conv3x3_c32r_kernel: 64-byte positions, 32 x 8 tiles, weights in
+    registers modulated per sample; ring32 '0': the generic halo kernel it replaces) in every layer form against
+    float64.  Shapes: bands of 4 and 1 tile rows (H / 8 = 43), runs that cross samples, every image border."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    monkeypatch.setenv('SG2_C32_RING', ring32)
+    N, H, W = shape
+    C = 32
+    wgs = 2 * torch.cuda.get_device_properties(DEV).multi_processor_count
+    assert N * (H // 8) * (W // 32) >= 2 * wgs      # the ring kernel's minimum of two tiles per workgroup
+    torch.manual_seed(19)
+    x = torch.randn(N, C, H, W)
+    w = torch.randn(C, C, 3, 3) / np.sqrt(C * 9)
+    s = torch.rand(N, C) + 0.5
+    d = torch.rand(N, C) + 0.5
+    noise = torch.randn(N, 1, H, W)
+    b = torch.randn(C) * 0.1
+    mod = form.startswith('mod')
+    epi = 'epi' in form
+    demod_noise = form.startswith('mod_epi')
+    kw = {}
+    if epi:
+        kw.update(bias=b.to(DEV), act=1, alpha=0.2, gain=np.sqrt(2), clamp=1.5)
+    if demod_noise:
+        kw.update(out_scale=d.to(DEV), noise=noise.to(DEV, dtype).reshape(N, H, W).contiguous(), noise_gain=0.3)
+    if form == 'epi_no_noise':
+        kw.update(out_scale=d.to(DEV))
+    xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    wp = cg._pack_conv(w.to(DEV, dtype))
+    y, raw = cg.conv3x3_fused(xd, wp, C, in_scale=s.to(DEV) if mod else None, want_raw=form.endswith('raw'), **kw)
+    xs = (x.to(dtype).float() * s[:, :, None, None]).to(dtype).double() if mod else x.to(dtype).double()
+    c = F.conv2d(xs, w.to(dtype).double(), padding=1)
+    ref = c
+    if epi:
+        z = c * (d[:, :, None, None] if (demod_noise or form == 'epi_no_noise') else 1)
+        if demod_noise:
+            z = z + noise.to(dtype).double() * 0.3
+        z = z + b[None, :, None, None]
+        ref = (F.leaky_relu(z, 0.2) * np.sqrt(2)).clamp(-1.5, 1.5)
+    tol = 5e-3 if dtype == torch.float16 else 2e-2
+    assert rel_err(y.float(), ref) < tol
+    if form.endswith('raw'):
+        assert rel_err(raw.float(), c) < tol
+    for n in range(N):
+        assert rel_err(y[n].float(), ref[n]) < 2 * tol, n
+    edge = torch.zeros(H, W, dtype=torch.bool)
+    edge[0], edge[-1], edge[:, 0], edge[:, -1] = True, True, True, True
+    assert rel_err(y.float()[..., edge], ref[..., edge]) < 2 * tol
+
+
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16, torch.float32])
 @pytest.mark.parametrize('C', [8, 64, 512])
 @pytest.mark.parametrize('form', ['G_dot', 'axpy', 'act', 'scale_only'])
