@@ -784,6 +784,10 @@ struct RingDyn {
     int s_per_wg;       // static tiles per workgroup (>= 2)
     int wg_per_n;       // workgroups per sample (grid = N wg_per_n)
     int nchunks;        // dynamic chunks of 2 tiles per sample after its static runs
+    // a dynamic tile's coordinates without runtime divisions: x / d = umulhi(x, m_d) for x d < 2^32
+    // (m_d = floor(2^32 / d) + 1; d >= 2), band = 1 << band_sh
+    unsigned m_pern, m_pband;
+    int band_sh;
 };
 constexpr int RQ_SLOTS = 64, RQ_MAXN = 4096;
 __device__ int g_ring_q[RQ_SLOTS * 2 * RQ_MAXN];
@@ -822,10 +826,19 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     };
     const int tinfo0 = t_begin + lane < t_end ? pack_tile(t_begin + lane) : 0;
     const int tinfo1 = t_begin + 64 + lane < t_end ? pack_tile(t_begin + 64 + lane) : 0;
+    // a dynamic tile (uniform t): the same packing by multiply-high (RingDyn), ~6 scalar instructions where the three
+    // signed divisions took ~90
+    auto pack_tile_dyn = [&](int t) -> int {
+        const int tiles_x = a.W / R_TW, per_n = tiles_x * (a.H / R_TH), per_band = tiles_x << dyn.band_sh;
+        const int n = (int)__builtin_amdgcn_readfirstlane(__umulhi((unsigned)t, dyn.m_pern)), r = t - n * per_n;
+        const int b = (int)__builtin_amdgcn_readfirstlane(__umulhi((unsigned)r, dyn.m_pband)), rb = r - b * per_band;
+        const int col = rb >> dyn.band_sh;
+        return (n << 20) | (((b << dyn.band_sh) + rb - (col << dyn.band_sh)) << 10) | col;
+    };
     auto tile_of = [&](int t, int& n, int& ty, int& tx) {
         const int j = t - t_begin;
         int v;
-        if (DYN && (unsigned)j >= (unsigned)(t_end - t_begin)) v = __builtin_amdgcn_readfirstlane(pack_tile(t));   // a dynamic tile
+        if (DYN && (unsigned)j >= (unsigned)(t_end - t_begin)) v = pack_tile_dyn(t);   // a dynamic tile
         else v = j < 64 ? __builtin_amdgcn_readlane(tinfo0, j) : __builtin_amdgcn_readlane(tinfo1, j - 64);
         n = (int)((unsigned)v >> 20);      // unsigned: a sample index >= 2048 sets bit 31
         ty = ((v >> 10) & 1023) * R_TH;
@@ -931,11 +944,9 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
     // tile), one vector add, a select on the border columns only -- where the generic issue above spends ~20
     // instructions (a runtime division, the row-validity branch and the per-lane kill logic) on each.
     const int rs_w = a.W * 128;
-    auto issue_fast = [&](int t, int slot, int eslot) {
+    auto issue_fast_at = [&](int n, int ty, int tx, int slot, int eslot) {
         if constexpr (R_TH == 4 && NW == 4) {
             if (SG2_RDIAG & 16) return;
-            int n, ty, tx;
-            tile_of(t, n, ty, tx);
             const int base0 = ((n * a.H + ty - 1) * a.W + tx - 1) * 128;     // halo row 0, column -1
             const int rowA = wave, rowB = 4 + (wave & 1);
             // an invalid row: every lane out of range (INT_MIN + < 8 KiB stays above any buffer of < 2^31 - 2^16 B)
@@ -967,8 +978,13 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
         }
     };
     auto issue_any = [&](int t, int slot, int eslot) {
-        if constexpr ((STG & 4) != 0) issue_fast(t, slot, eslot);
-        else issue(t, slot, eslot);
+        if constexpr ((STG & 4) != 0) {
+            int n, ty, tx;
+            tile_of(t, n, ty, tx);
+            issue_fast_at(n, ty, tx, slot, eslot);
+        } else {
+            issue(t, slot, eslot);
+        }
     };
 
     // MFMA B-fragment addressing: pixel fragment i of the wave at tap (ky, kx), chunk c reads position
@@ -1154,6 +1170,8 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
         int* qn = dyn.q + dyn_n;                      // this sample's grab counter
         f32x4 acc[NF][2];
         int cur = t_begin, rend = t_end, gv = 0;
+        int cn, cty, ctx;                                 // the current tile's coordinates (carried from its issue)
+        tile_of(cur, cn, cty, ctx);
         for (;; ++k) {
             int nxt;
             if (cur + 1 < rend) {
@@ -1167,9 +1185,10 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
             const bool grab = cur + 2 == rend;            // second-to-last tile of its run / chunk: grab the next chunk
             if (grab && wave == 0 && lane == 0) gv = __hip_atomic_fetch_add(qn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int slot = k % R_NSLOT;
-            issue_any(nxt >= 0 ? nxt : cur, (k + 1) % R_NSLOT, (k + 1) % R_NEPI);
-            int n, ty, tx;
-            tile_of(cur, n, ty, tx);
+            const int n = cn, ty = cty, tx = ctx;
+            if (nxt >= 0) tile_of(nxt, cn, cty, ctx);
+            if constexpr ((STG & 4) != 0) issue_fast_at(cn, cty, ctx, (k + 1) % R_NSLOT, (k + 1) % R_NEPI);
+            else issue(nxt >= 0 ? nxt : cur, (k + 1) % R_NSLOT, (k + 1) % R_NEPI);
             RING_STAMP(0);
             mfma_tile(acc, smem_raw + slot * R_SLOT);
             RING_STAMP(1);
@@ -1319,7 +1338,7 @@ int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RG::LDS);
         attr_set = true;
     }
-    RingDyn dyn{nullptr, 0, 0, 0};
+    RingDyn dyn{nullptr, 0, 0, 0, 0u, 0u, 0};
     if ((STG & 16) != 0) {
         // the caller (launch_c64r_form) checked grid % N == 0; SG2_RING_DYN: percent of a sample's tiles handed out
         // dynamically (default 12), the dynamic part a whole number of 2-tile chunks
@@ -1331,7 +1350,12 @@ int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band
         dyn.s_per_wg = sp;
         dyn.wg_per_n = gpn;
         dyn.nchunks = (per_n - gpn * sp) / 2;
-        if (!dyn.q || gpn * sp > per_n || (per_n - gpn * sp) % 2 || a.N > RQ_MAXN) {
+        const int per_band = band * (a.W / R_TW);
+        dyn.m_pern = (unsigned)((1ull << 32) / (unsigned)per_n + 1);
+        dyn.m_pband = (unsigned)((1ull << 32) / (unsigned)per_band + 1);
+        dyn.band_sh = band == 4 ? 2 : (band == 2 ? 1 : 0);
+        if (!dyn.q || gpn * sp > per_n || (per_n - gpn * sp) % 2 || a.N > RQ_MAXN || per_n < 2 || per_band < 2 ||
+            (int64_t)tiles * per_n >= (1ll << 32) || (band != 1 && band != 2 && band != 4)) {
             set_error("sg2_conv3x3 (c64 ring): dynamic tail unavailable");
             return -1;
         }
@@ -1638,6 +1662,176 @@ int launch_c32r_raw(const Conv3Args& a, hipStream_t s) {
                    : launch_c32r<T, SI, EPI, false>(a, s, tiles, grid, band);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Stride-2 / pad-0 3x3 conv of the wide discriminator down layers (conv2d_resample's down-2 plan after its FIR,
+// :94-109: the D blocks' conv1 at 128^2 .. 32^2 outputs, Cin 64 .. 256 -> Cout = 2 Cin), round 5.  The 32 x 4 halo
+// form above restages a tile's 9 x 64 x 32 weights per 128 output pixels and ran these shapes at 0.10-0.18 of the
+// MFMA peak, the generic implicit GEMM (register-staged gathers) at 0.12-0.24 (profiles/r02_s2_ab.log).  Here an
+// implicit GEMM whose operands arrive by LDS-DMA, nothing staged through registers:
+//   * workgroup tile: 256 output pixels (linear over n, oy, ox) x 128 output channels; 4 waves of 128 x 64
+//     (8 pixel fragments x 4 channel fragments: 32 MFMAs and 12 ds_read_b128 per wave and K step);
+//   * K = 9 taps x Cin in 32-channel steps, tap-minor (consecutive steps read neighbouring input pixels); per step
+//     the workgroup stages the 256 pixels' tap inputs (64 B each) and 128 weight rows into one of G_NS = 3 LDS slots
+//     by 24 wave-instructions of 1 KiB (6 per wave, issued two steps ahead, one barrier per step); the 16-byte
+//     pieces are swizzled on the source side (swz64), so fragment reads of 16 consecutive rows are conflict-free;
+//     the weight rows are loaded in p_chan order, so a lane's accumulators hold 8 consecutive output channels of
+//     one pixel (16-byte stores straight from registers);
+//   * XCD-aware order: workgroup i runs on XCD i % 8 and takes tile (i % 8) * (grid / 8) + i / 8, so neighbouring
+//     tiles -- which share input rows -- meet in one L2.
+// Epilogue in registers: demod scale, bias (rounded to T), lrelu, gain, clamp (the halo kernel's order), then the
+// residual add (the D resnet's skip: round(round(v) + residual)) with y_raw = the raw conv output or (raw_act) the
+// activated value before the add.
+constexpr int G_BM = 256, G_BN = 128, G_NS = 3;
+constexpr int G_SLOT = (G_BM + G_BN) * 64;                  // 24 KiB
+constexpr int G_DMA = (G_BM + G_BN) / 16 / 4;               // wave-instructions per wave and step (6)
+constexpr int G_ADMA = G_BM / 16 / 4;                       // of which pixel rows (4)
+constexpr size_t G_LDS = (size_t)G_NS * G_SLOT;
+
+template <typename T, bool EPI>
+__global__ __launch_bounds__(256, 2) void conv3x3_s2g_kernel(Conv3Args a, int m_tiles, int n_tiles) {
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l16 = lane & 15, q = lane >> 4;
+    const int t = (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8);
+    if (t >= m_tiles * n_tiles) return;
+    const int mt = t / n_tiles, nt = t - mt * n_tiles;
+    const int OHW = a.OH * a.OW, M = a.N * OHW;
+    const int m0 = mt * G_BM, n0 = nt * G_BN;
+    const int nk = 9 * (a.Cin / 32);
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(a.x, (int64_t)a.N * a.H * a.W * a.Cin * 2);
+    const __amdgpu_buffer_rsrc_t rwb = make_rsrc(a.w, (int64_t)a.Cout * 9 * a.Cin * 2);
+
+    // DMA lanes: instruction u of wave w fills slot rows (4 u + w) * 16 + lane / 4, piece lane % 4 (u < G_ADMA:
+    // pixel rows, else weight rows); the lane reads source piece (lane % 4) ^ ((row >> 1) & 2)
+    int dbase[G_DMA];
+#pragma unroll
+    for (int u = 0; u < G_DMA; ++u) {
+        const int r = (u * 4 + wave) * 16 + (lane >> 2);
+        const int j = (lane & 3) ^ ((r >> 1) & 2);
+        if (u < G_ADMA) {
+            const int m = m0 + r;
+            if (m < M) {
+                const int n = m / OHW, rem = m - n * OHW, oy = rem / a.OW, ox = rem - oy * a.OW;
+                dbase[u] = (((n * a.H + 2 * oy) * a.W + 2 * ox) * a.Cin + j * 8) * 2;
+            } else {
+                dbase[u] = -1;
+            }
+        } else {
+            dbase[u] = ((n0 + p_chan(r - G_BM)) * 9 * a.Cin + j * 8) * 2;
+        }
+    }
+    auto issue = [&](int step, int slot) {
+        const int tap = step % 9, c = step / 9;
+        const int ky = tap / 3, kx = tap - ky * 3;
+        const int aoff = ((ky * a.W + kx) * a.Cin + c * 32) * 2, boff = (tap * a.Cin + c * 32) * 2;
+        char* sb = smem_raw + slot * G_SLOT;
+#pragma unroll
+        for (int u = 0; u < G_DMA; ++u) {
+            if (u < G_ADMA) {
+                const int off = dbase[u] < 0 ? -1 : dbase[u] + aoff;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rxb, (lds_ptr_t)(sb + (u * 4 + wave) * 1024), 16, off, 0, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rwb, (lds_ptr_t)(sb + (u * 4 + wave) * 1024), 16, dbase[u] + boff,
+                                                         0, 0, 0);
+            }
+        }
+    };
+
+    const int wm = wave >> 1, wn = wave & 1;
+    const int sw = ((q ^ ((l16 >> 1) & 2)) << 4) + l16 * 64;    // a fragment row's lane offset (row base % 16 == 0)
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int st = 0; st < G_NS - 1; ++st)
+        if (st < nk) issue(st, st);
+    for (int step = 0; step < nk; ++step) {
+        if (step + G_NS - 2 < nk) wait_vm<(G_NS - 2) * G_DMA>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();                 // every wave's DMAs of this step landed; the oldest slot is free
+        if (step + G_NS - 1 < nk) issue(step + G_NS - 1, (step + G_NS - 1) % G_NS);
+        const char* sb = smem_raw + (step % G_NS) * G_SLOT + sw;
+        v8<T> wf[4], pf[8];
+#pragma unroll
+        for (int jc = 0; jc < 4; ++jc) wf[jc] = *(const v8<T>*)(sb + (G_BM + wn * 64 + jc * 16) * 64);
+#pragma unroll
+        for (int jp = 0; jp < 8; ++jp) pf[jp] = *(const v8<T>*)(sb + (wm * 128 + jp * 16) * 64);
+#pragma unroll
+        for (int jp = 0; jp < 8; ++jp)
+#pragma unroll
+            for (int jc = 0; jc < 4; ++jc) acc[jc][jp] = mma<T>(wf[jc], pf[jp], acc[jc][jp]);
+    }
+
+    // ---- epilogue: lane (l16, q) holds, per pixel fragment jp and channel pair h, channels
+    // n0 + (2 wn + h) * 32 + 8 q .. + 7 of pixel m0 + wm * 128 + 16 jp + l16 ----
+    float bsc[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int ch0 = n0 + (2 * wn + h) * 32 + 8 * q;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsc[h][e] = (EPI && a.bias) ? (float)(T)a.bias[ch0 + e] : 0.f;
+    }
+    const float alpha = (EPI && a.act == 1) ? a.alpha : 1.f;
+    const float clampv = (EPI && a.clamp >= 0.f) ? a.clamp : __builtin_inff();
+    T* y = (T*)a.y;
+    T* yr = (T*)a.y_raw;
+    const T* res = (const T*)a.residual;
+#pragma unroll
+    for (int jp = 0; jp < 8; ++jp) {
+        const int m = m0 + wm * 128 + jp * 16 + l16;
+        if (m >= M) continue;
+        const int n = m / OHW;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int ch0 = n0 + (2 * wn + h) * 32 + 8 * q;
+            const int64_t dst = (int64_t)m * a.Cout + ch0;
+            vec8 yv, rv;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float v = acc[2 * h + (e >> 2)][jp][e & 3];
+                rv[e] = (T)v;
+                if (EPI) {
+                    const float d = a.out_scale ? a.out_scale[(int64_t)n * a.Cout + ch0 + e] : 1.f;
+                    v = v * d + bsc[h][e];
+                    v = v > 0.f ? v : v * alpha;
+                    v *= a.gain;
+                    v = fminf(fmaxf(v, -clampv), clampv);
+                }
+                yv[e] = (T)v;
+            }
+            if (res) {
+                if (yr && a.raw_act) *(vec8*)(yr + dst) = yv;
+                const vec8 rr = *(const vec8*)(res + dst);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) yv[e] = (T)((float)yv[e] + (float)rr[e]);
+            }
+            *(vec8*)(y + dst) = yv;
+            if (yr && !(res && a.raw_act)) *(vec8*)(yr + dst) = rv;
+        }
+    }
+}
+
+template <typename T, bool EPI>
+int launch_s2g(const Conv3Args& a, hipStream_t s) {
+    const int M = a.N * a.OH * a.OW;
+    const int m_tiles = (M + G_BM - 1) / G_BM, n_tiles = a.Cout / G_BN;
+    const int grid = (m_tiles * n_tiles + 7) / 8 * 8;
+    auto kern = conv3x3_s2g_kernel<T, EPI>;
+    static bool attr_set = false;   // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G_LDS);
+        attr_set = true;
+    }
+    kern<<<grid, 256, G_LDS, s>>>(a, m_tiles, n_tiles);
+    return launch_status("sg2_conv3x3_s2 (s2g)");
+}
+
 template <typename T>
 int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     const bool si = a.in_scale != nullptr;
@@ -1646,7 +1840,17 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
         hipError_t e = zero_acc(a.dot_out, (size_t)a.N * a.Cout * sizeof(float), s);
         if (e != hipSuccess) { set_error("sg2_conv3x3: memset failed"); return (int)e; }
     }
-    if (stride == 2) {   // 32 x 4 output tiles, two workgroups per CU
+    if (stride == 2) {
+        // the wide down layers: the LDS-DMA implicit GEMM (SG2_S2G=0: off)
+        const char* eg = getenv("SG2_S2G");          // read per launch: tests switch it in one process
+        if ((!eg || atoi(eg) != 0) && !si && !a.noise && !a.dot_out && a.Cin % 32 == 0 && a.Cout % G_BN == 0 &&
+            a.OW >= 32 && (int64_t)a.N * a.OH * a.OW * a.Cout * 2 < 0x7fff0000ll &&
+            ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 && ((uintptr_t)a.residual % 16) == 0 &&
+            (!epi || a.gain > 0.f)) {
+            if (epi) return launch_s2g<T, true>(a, s);
+            return launch_s2g<T, false>(a, s);
+        }
+        // 32 x 4 output tiles, two workgroups per CU
         a.tiles_x = (a.OW + 31) / 32;
         a.tiles_y = (a.OH + 3) / 4;
         if (si) { if (epi) return launch3<T, 32, true, true, 1, 2>(a, s); return launch3<T, 32, true, false, 1, 2>(a, s); }

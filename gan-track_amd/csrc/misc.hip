@@ -192,14 +192,18 @@ __device__ __forceinline__ void st_any(void* p, unsigned i, int dt, float v) {
 }
 // The table travels in the kernel arguments (scalar loads through the constant cache): a workgroup finds its
 // descriptor by a binary search over block0 there, with no dependent global loads before its element loads.
-// 1024 elements per workgroup, 4 per lane, every load of a lane issued before its first store.
-constexpr int PACK_PER_LAUNCH = 64, PACK_EPT = 4;
+// Row mode (B * K <= PACK_ROW_MAX, every conv of the networks): one workgroup per output row a -- the row's
+// B x K inputs read in input order (a conv weight's [Cin][kh][kw] slab is contiguous: whole-line loads), the
+// scaled f32 values staged in LDS, then out[a][k][b] written in output order (whole-line stores).  The element
+// mode (1024 elements per workgroup, 4 per lane) gathered 9-apart elements per wave load and ran at ~0.5 TB/s
+// (222 us per phase table, profiles/r05 step breakdown).
+constexpr int PACK_PER_LAUNCH = 64, PACK_EPT = 4, PACK_ROW_MAX = 8192;
 struct PackDescK {
     void* out;
     const void* in;
     int sa, sb, sk, A, B, K, block0;
     float scale;
-    unsigned char out_dt, in_dt, flip, pad_;
+    unsigned char out_dt, in_dt, flip, rows;
 };
 struct PackTable {
     PackDescK d[PACK_PER_LAUNCH];
@@ -213,6 +217,25 @@ __global__ __launch_bounds__(256) void pack_weight_multi_kernel(const PackTable 
         if (t.d[mid].block0 <= b) lo = mid; else hi = mid - 1;
     }
     const PackDescK& d = t.d[lo];
+    if (d.rows) {
+        __shared__ float row[PACK_ROW_MAX];
+        const int a = b - d.block0, L = d.B * d.K;
+        const int64_t base = (int64_t)a * d.sa;
+        for (int i = threadIdx.x; i < L; i += 256) {
+            const int bb = i / d.K, k = i - bb * d.K;
+            float x = ld_any(d.in, base + (int64_t)bb * d.sb + k * d.sk, d.in_dt) * d.scale;
+            asm volatile("" : "+v"(x));          // (as pack_weight_kernel: the f32 product, then one rounding)
+            row[i] = x;
+        }
+        __syncthreads();
+        const unsigned ob = (unsigned)a * (unsigned)L;
+        for (int e = threadIdx.x; e < L; e += 256) {
+            const int k = e / d.B, bb = e - k * d.B;
+            const int kk = d.flip ? d.K - 1 - k : k;
+            st_any(d.out, ob + e, d.out_dt, row[bb * d.K + kk]);
+        }
+        return;
+    }
     const unsigned total = (unsigned)d.A * d.B * d.K;
     const unsigned e0 = (unsigned)(b - d.block0) * (256u * PACK_EPT) + threadIdx.x;
     float v[PACK_EPT];
@@ -489,8 +512,18 @@ extern "C" int sg2_pack_weight(void* out, int out_dtype, const void* in, int in_
     SG2_CHECK(out && in, "sg2_pack_weight: null pointer");
     SG2_CHECK(A > 0 && B > 0 && K >= 1 && K <= 9 && (int64_t)A * B * K < (1LL << 31),
               "sg2_pack_weight: unsupported shape (K <= 9, A*B*K < 2^31)");
-    const unsigned grid = (unsigned)cdiv((int64_t)A * B * K, 256);
     hipStream_t s = as_stream(stream);
+    if (B * K <= PACK_ROW_MAX && sa >= 0 && sb >= 0 && sk >= 0 && sa < (1LL << 31) && sb < (1LL << 31) && sk < (1LL << 31) &&
+        (in_dtype == SG2_F32 || in_dtype == SG2_F16 || in_dtype == SG2_BF16) &&
+        (out_dtype == SG2_F32 || out_dtype == SG2_F16 || out_dtype == SG2_BF16)) {   // the row-mode kernel
+        PackTable t{};
+        t.n = 1;
+        t.d[0] = PackDescK{out, in, (int)sa, (int)sb, (int)sk, A, B, K, 0, scale, (unsigned char)out_dtype,
+                           (unsigned char)in_dtype, (unsigned char)(flip != 0), 1};
+        pack_weight_multi_kernel<<<A, 256, 0, s>>>(t);
+        return launch_status("sg2_pack_weight");
+    }
+    const unsigned grid = (unsigned)cdiv((int64_t)A * B * K, 256);
     SG2_DISPATCH(in_dtype, Tin, SG2_DISPATCH(out_dtype, Tout,
         pack_weight_kernel<Tin, Tout><<<grid, 256, 0, s>>>((Tout*)out, (const Tin*)in, A, B, K, sa, sb, sk, flip, scale)));
     return launch_status("sg2_pack_weight");
@@ -513,9 +546,11 @@ extern "C" int sg2_pack_weight_multi(const sg2_pack_desc* descs, int n, void* st
             SG2_CHECK((d.in_dtype == SG2_F32 || d.in_dtype == SG2_F16 || d.in_dtype == SG2_BF16) &&
                       (d.out_dtype == SG2_F32 || d.out_dtype == SG2_F16 || d.out_dtype == SG2_BF16),
                       "sg2_pack_weight_multi: unsupported dtype");
+            const bool rows = d.B * d.K <= PACK_ROW_MAX;
             t.d[j] = PackDescK{d.out, d.in, (int)d.sa, (int)d.sb, (int)d.sk, d.A, d.B, d.K, blk, d.scale,
-                               (unsigned char)d.out_dtype, (unsigned char)d.in_dtype, (unsigned char)(d.flip != 0), 0};
-            blk += (int)cdiv((int64_t)d.A * d.B * d.K, 256 * PACK_EPT);
+                               (unsigned char)d.out_dtype, (unsigned char)d.in_dtype, (unsigned char)(d.flip != 0),
+                               (unsigned char)rows};
+            blk += rows ? d.A : (int)cdiv((int64_t)d.A * d.B * d.K, 256 * PACK_EPT);
         }
         pack_weight_multi_kernel<<<blk, 256, 0, s>>>(t);
         const int rc = launch_status("sg2_pack_weight_multi");

@@ -359,18 +359,23 @@ def _halo_ok(x, kh, kw, stride, pad, out_hw):
             x.dtype in (torch.float16, torch.bfloat16) and c % 8 == 0 and h >= 16 and w >= 16)
 
 
-def _halo_s2_ok(x, kh, kw, stride, pad, dot=False):
-    """The stride-2 / pad-0 form of the halo kernel (sg2_conv3x3_s2, 32x4 output tiles) for 16-bit 3x3
-    layers.  Measured against the implicit GEMM (tools/s2_ab.py, profiles/r02_s2_ab.log): it wins for
-    outputs <= 16 wide in every form (the discriminator's 32^2 / 16^2 down layers), and in the out_scale +
-    dot form (the up layers' input gradient, where the implicit GEMM's dot epilogue is slow) also for
-    inputs of <= 128 channels; wide outputs with many channels stay on the implicit GEMM."""
+def _halo_s2_ok(x, kh, kw, stride, pad, dot=False, cout=None, scaled=False):
+    """The stride-2 / pad-0 forms of sg2_conv3x3_s2 for 16-bit 3x3 layers.  The 32x4 halo tile, measured against
+    the implicit GEMM (tools/s2_ab.py, profiles/r02_s2_ab.log), wins for outputs <= 16 wide in every form (the
+    discriminator's 32^2 / 16^2 down layers), and in the out_scale + dot form (the up layers' input gradient,
+    where the implicit GEMM's dot epilogue is slow) also for inputs of <= 128 channels.  The wide down layers
+    (outputs >= 32 wide, Cin % 32 == 0, Cout % 128 == 0, no modulation / noise / dot: the D blocks' conv1, given
+    `cout`) take the LDS-DMA implicit GEMM of the same entry point (conv3x3.hip conv3x3_s2g_kernel,
+    tools/s2g_ab.py); other wide shapes stay on the generic implicit GEMM."""
     n, c, h, w = x.shape
     p = tuple(pad) if isinstance(pad, (tuple, list)) else (pad, pad)
     if not (kh == 3 and kw == 3 and stride == 2 and p == (0, 0) and x.dtype in (torch.float16, torch.bfloat16) and
             c % 8 == 0 and h >= 17 and w >= 17):
         return False
-    return (w - 3) // 2 + 1 <= 16 or (dot and c <= 128)
+    ow = (w - 3) // 2 + 1
+    if cout is not None and not dot and not scaled and c % 32 == 0 and cout % 128 == 0 and ow >= 32:
+        return True
+    return ow <= 16 or (dot and c <= 128)
 
 
 def conv3x3_fused(x, wp, cout, in_scale=None, out_scale=None, noise=None, noise_gain=0.0, bias=None, act=0,
@@ -513,7 +518,7 @@ class _Conv2d(torch.autograd.Function):
         oh, ow = out_hw
         if _halo_ok(x, kh, kw, stride, pad, out_hw):
             y = conv3x3_fused(x, _pack_conv(w), o)[0]
-        elif _halo_s2_ok(x, kh, kw, stride, pad):
+        elif _halo_s2_ok(x, kh, kw, stride, pad, cout=o):
             y = conv3x3_fused(x, _pack_conv(w), o, stride=2)[0]
         else:
             y = _conv_raw(x, _pack_conv(w), o, oh, ow, kh, kw, stride, pad, False)

@@ -85,7 +85,7 @@ class FusedConv(torch.autograd.Function):
             y, aux = _cg.conv3x3_fused(x, _cg._pack_conv(weight, dt, scale=wgain), cout, in_scale=_f32(styles), out_scale=_f32(dcoefs),
                                        noise=nz, noise_gain=1.0, bias=b32, act=act, alpha=alpha, gain=gain,
                                        clamp=clamp, want_raw=want_c)
-        elif _cg._halo_s2_ok(x, kh, kw, stride, pad):
+        elif _cg._halo_s2_ok(x, kh, kw, stride, pad, cout=cout, scaled=styles is not None or noise is not None):
             y, aux = _cg.conv3x3_fused(x, _cg._pack_conv(weight, dt, scale=wgain), cout, in_scale=_f32(styles),
                                        out_scale=_f32(dcoefs), noise=nz, noise_gain=1.0, bias=b32, act=act,
                                        alpha=alpha, gain=gain, clamp=clamp, want_raw=want_c or want_z, stride=2,

@@ -148,7 +148,7 @@ def _isolated_phases(tr, G, D, real, c, gz, gc):
 
 
 def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False, isolated=False, deterministic=True,
-                f32_exact=False, grouped_affine=True):
+                f32_exact=False, grouped_affine=True, perturb=0.0, perturb_seed=0):
     """The product's iteration on `dev`.  fp16_dtype None: all-f32 (num_fp16_res=0, the reference's CPU
     arithmetic); else the reference's GPU default num_fp16_res=4 in that 16-bit type.  isolated: every phase
     from the starting state, no optimiser step (the *_iso fixtures); returns the gradients, pl_mean and stats.
@@ -156,7 +156,10 @@ def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False, i
     the inputs, so a bound is met or missed by the code, not by a run's atomic order.  f32_exact: the f32 layers
     on the f32-input MFMA kernels (SG2_F32_EXACT=1) instead of the split-bf16 products (the other f32
     arithmetic of the library); grouped_affine False: the synthesis affine layers one GEMM each
-    (networks_stylegan2.grouped_affine), another evaluation order of the styles (diagnostics only)."""
+    (networks_stylegan2.grouped_affine), another evaluation order of the styles (diagnostics only).  perturb > 0:
+    every parameter, real image and latent multiplied by (1 +- perturb) in f32 first (seeded signs; 2^-23 moves
+    an entry by about one f32 ulp) -- a state equal within f32 rounding, i.e. another draw of the 16-bit
+    rounding pattern (diagnostics: the product's own spread, tools/nudge16.py)."""
     import sg2hip
     from torch_utils.ops import conv2d_gradfix as cg
     from training import networks_stylegan2 as nets
@@ -167,7 +170,7 @@ def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False, i
         cg.presplit = False
     try:
         with sg2hip.deterministic(deterministic, device=dev):
-            return _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated)
+            return _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated, perturb, perturb_seed)
     finally:
         if prev[0] is None:
             os.environ.pop('SG2_F32_EXACT', None)
@@ -177,10 +180,18 @@ def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False, i
         nets.grouped_affine = prev[2]
 
 
-def _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated):
+def _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated, perturb=0.0, perturb_seed=0):
     from training import networks_stylegan2 as net, augment_mi, loss as loss_mod, trainer as trainer_mod
     torch.manual_seed(0)
     G, D = _nets(net, cfg, 0 if fp16_dtype is None else 4, fp16_dtype)
+    if perturb:
+        gen = torch.Generator().manual_seed(perturb_seed)
+        with torch.no_grad():
+            for mod in (G, D):
+                for _, p in sorted(mod.named_parameters()):
+                    p.copy_(_perturb(p.float(), perturb, gen))
+        inp = dict(inp, **{k: _perturb(torch.from_numpy(np.asarray(inp[k], np.float32)), perturb, gen).numpy()
+                           for k in ('real', 'gen_z')})
     G, D = G.to(dev), D.to(dev)
     G_ema = copy.deepcopy(G).eval()
     aug = augment_mi.AugmentPipe(run_dir=None, batch_size=cfg['batch'], **CLARO_AUG).train().requires_grad_(False).to(dev)

@@ -551,7 +551,9 @@ def merge_emulated16_nudged(tag, cache_dir):
         with np.load(fn, allow_pickle=False) as f:
             z.update({f'{pre}/{k}': v for k, v in unpack(f).items()})
         n += 1
-    np.savez_compressed(path, **pack(z))
+    tmp = path + '.tmp.npz'
+    np.savez_compressed(tmp, **pack(z))
+    os.replace(tmp, path)              # (atomic: a concurrent reader sees the old or the new file)
     print(tag, n, 'nudged 16-bit emulation samples merged', flush=True)
 
 

@@ -114,7 +114,9 @@ def merge(tag):
         with np.load(fn, allow_pickle=False) as f:
             z.update({f'r32_{name}/{k}': v for k, v in unpack(f).items()})
         names.append(name)
-    np.savez_compressed(path, **pack(z))
+    tmp = path + '.tmp.npz'
+    np.savez_compressed(tmp, **pack(z))
+    os.replace(tmp, path)              # (atomic: a concurrent reader sees the old or the new file)
     print(tag, 'merged', names, flush=True)
 
 

@@ -131,14 +131,20 @@ def test_f32_phases_vs_reference(tag, arith):
 # 16-bit (num_fp16_res = 4, the reference's GPU default; f32 accumulation) against the float64 answer of the same
 # isolated phases, held to the REFERENCE's own 16-bit error: the fixtures carry the oracle's emulation of the
 # reference's fp16 GPU iteration (q16/, qbf/: make_golden.py `emu:<tag>:<dt>`, oracle.sg2_oracle.EMU16 -- every
-# tensor and gradient of a use_fp16 block rounded where the reference's is) and, at C1 / C2, the same emulation at
-# states nudged by half an f32 ulp (q16n<seed>/, qbfn<seed>/: `emu16n:`).  Each phase's two error measures -- the
-# relative error of its vector of tensor norms and of its whole flat gradient (config_parity.compare_flat) -- are
-# each held to EMU_FACTOR x the SAME measure's largest value over the emulation samples (floor ISO16_FLOOR): no
-# measure is bounded by the other.  Run in deterministic mode and with the float atomics the bench times.
+# tensor and gradient of a use_fp16 block rounded where the reference's is) and the same emulation at states nudged
+# by half an f32 ulp (q16n<seed>/, qbfn<seed>/: `emu16n:`), each another draw of the rounding pattern.  The product
+# is evaluated the same way: at the fixture state and at NUDGES states nudged by one f32 ulp
+# (config_parity.run_product perturb), so both sides are distributions.  Per phase and error measure -- the
+# relative error of the vector of tensor norms and of the whole flat gradient (config_parity.compare_flat), each
+# bounded by the SAME measure only -- the product's median is held to EMU_FACTOR x the emulation's median and the
+# product's largest draw to EMU_FACTOR x the emulation's largest (floor ISO16_FLOOR).  One draw alone is not a
+# fair statistic: the 16-bit measures are heavy-tailed (C2 bf16 Dreg norm vector, product over 7 states: median
+# 0.0028, draws 0.0014 .. 0.0165; emulation median 0.0027 -- profiles/r05_nudge16.txt).  Run in deterministic mode
+# and with the float atomics the bench times.
 EMU_FACTOR = 2.0
 ISO16_FLOOR = {'fp16': 5e-3, 'bf16': 1e-2}
 EMU_KEY = {'fp16': 'q16', 'bf16': 'qbf'}
+NUDGES = 4
 
 
 @pytest.mark.timeout(300)
@@ -146,25 +152,35 @@ EMU_KEY = {'fp16': 'q16', 'bf16': 'qbf'}
 @pytest.mark.parametrize('tag,dt', [('c1', 'fp16'), ('c1', 'bf16'), ('c2', 'fp16'), ('c2', 'bf16'), ('c4', 'fp16'),
                                     ('c5', 'bf16')])
 def test_16bit_phases(tag, dt, det):
-    cfg, inp, tape, fix = _iso(tag)
-    got, _ = cp.run_product(cfg, inp, tape, DEV, fp16_dtype=torch.float16 if dt == 'fp16' else torch.bfloat16,
-                            aug_p=cfg['aug_p'], isolated=True, deterministic=det)
+    truth = None
+    runs = []
+    for seed in range(NUDGES + 1):
+        cfg, inp, tape, fix = _iso(tag)
+        got, _ = cp.run_product(cfg, inp, tape, DEV, fp16_dtype=torch.float16 if dt == 'fp16' else torch.bfloat16,
+                                aug_p=cfg['aug_p'], isolated=True, deterministic=det,
+                                perturb=2.0 ** -23 if seed else 0.0, perturb_seed=seed)
+        if truth is None:
+            truth = _truth(fix)
+            cp.save_summary(f'{tag}_iso_{dt}_{"det" if det else "atomic"}', got)
+        runs.append(cp.compare_flat(got, truth, ISO_GROUPS))
     mode = 'det' if det else 'atomic'
-    cp.save_summary(f'{tag}_iso_{dt}_{mode}', got)
-    truth = _truth(fix)
     pres = sorted({k.split('/', 1)[0] for k in fix if k.split('/', 1)[0] == EMU_KEY[dt] or
                    (k.startswith(EMU_KEY[dt] + 'n') and '/' in k)})
     assert EMU_KEY[dt] in pres, f'train_{tag}_iso.npz has no {EMU_KEY[dt]}/ summaries (make_golden.py emu:{tag}_iso:{dt})'
-    res = cp.compare_flat(got, truth, ISO_GROUPS)
     refs = {p: cp.compare_flat({k[len(p) + 1:]: v for k, v in fix.items() if k.startswith(p + '/')}, truth, ISO_GROUPS)
             for p in pres}
-    cp.record(f'{tag}_iso_{dt}_{mode}', dict(flat=res, reference_16bit_flat=refs))
-    for g, (en, es) in res.items():
-        rn = max(r[g][0] for r in refs.values())
-        rs = max(r[g][1] for r in refs.values())
-        tn, ts = max(ISO16_FLOOR[dt], EMU_FACTOR * rn), max(ISO16_FLOOR[dt], EMU_FACTOR * rs)
-        assert en <= tn and es <= ts, (f'{g}: norm-vector err {en:.3g} (bound {tn:.3g}), flat err {es:.3g} (bound '
-                                       f'{ts:.3g}); the reference\'s emulated {dt} over {len(refs)} samples: {rn:.3g} / {rs:.3g}')
+    cp.record(f'{tag}_iso_{dt}_{mode}', dict(flat=runs[0], flat_nudged=runs[1:], reference_16bit_flat=refs))
+    fails = []
+    for g in ISO_GROUPS:
+        for j, meas in enumerate(('norm-vector', 'flat')):
+            pv = [r[g][j] for r in runs]
+            ev = [r[g][j] for r in refs.values()]
+            for stat, f in (('median', np.median), ('max', max)):
+                bound = max(ISO16_FLOOR[dt], EMU_FACTOR * float(f(ev)))
+                if float(f(pv)) > bound:
+                    fails.append(f'{g} {meas} {stat}: product {float(f(pv)):.3g} over {len(pv)} states > {bound:.3g} '
+                                 f'(emulated {dt} over {len(ev)} samples: {float(f(ev)):.3g})')
+    assert not fails, '; '.join(fails)
 
 
 class _RecordingTape(cp.Tape):

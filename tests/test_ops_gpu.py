@@ -979,10 +979,12 @@ def test_dot_hw(dtype):
 
 @pytest.mark.parametrize('src,dst', [(torch.float32, torch.float32), (torch.float32, torch.float16),
                                      (torch.float32, torch.bfloat16), (torch.float16, torch.float16)])
-@pytest.mark.parametrize('o,i,k', [(512, 512, 3), (64, 1, 1), (3, 70, 3), (45, 33, 1), (96, 40, 3), (20, 37, 2)])
+@pytest.mark.parametrize('o,i,k', [(512, 512, 3), (64, 1, 1), (3, 70, 3), (45, 33, 1), (96, 40, 3), (20, 37, 2),
+                                   (6, 1000, 3)])
 def test_pack_weight(src, dst, o, i, k):
     """sg2_pack_weight (conv2d_gradfix._pack_conv / _pack_convT, flipped taps, transposed views, ragged
-    tiles) vs the torch permute-copy it replaces: bit-exact (a layout move plus one rounding)."""
+    tiles) vs the torch permute-copy it replaces: bit-exact (a layout move plus one rounding).  Rows of B x K <=
+    8192 take the row-mode kernel (misc.hip PACK_ROW_MAX), (6, 1000, 3)'s transposed packs the element mode."""
     from torch_utils.ops import conv2d_gradfix as cg
     torch.manual_seed(7)
     w = torch.randn(o, i, k, k, device=DEV).to(src)
@@ -1153,6 +1155,50 @@ def test_conv3x3_s2(dtype, shape):
     cd = F.conv2d(x.to(dtype).double(), w.to(dtype).double(), stride=2)
     assert rel_err(y.float(), cd * d[:, :, None, None]) < tol
     assert rel_err(dot, (cd * src.double()).sum([2, 3])) < tol
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(2, 64, 129, 129, 128), (3, 128, 65, 65, 256), (1, 256, 65, 65, 512),
+                                   (2, 32, 67, 67, 128), (1, 64, 257, 257, 128), (5, 96, 71, 65, 384)])
+@pytest.mark.parametrize('s2g', ['1', '0'])
+def test_conv3x3_s2g(dtype, shape, s2g, monkeypatch):
+    """The wide stride-2 down layers on the LDS-DMA implicit GEMM (conv3x3.hip conv3x3_s2g_kernel; s2g '0': the
+    32 x 4 halo form it replaces) vs F.conv2d in float64: plain, the D block's bias + lrelu + gain + clamp with the
+    raw output, the resnet residual with the pre-residual activation, and a demodulation scale.  Shapes: several
+    output-channel tiles (Cout 256 .. 512), a ragged last pixel tile (2 x 33 x 33 pixels), Cin = 32 (one K chunk a
+    tap), non-square input."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    monkeypatch.setenv('SG2_S2G', s2g)
+    N, Cin, H, W, Cout = shape
+    OH, OW = (H - 3) // 2 + 1, (W - 3) // 2 + 1
+    assert cg._halo_s2_ok(torch.empty(N, Cin, H, W, dtype=dtype), 3, 3, 2, 0, cout=Cout)
+    torch.manual_seed(43)
+    x = torch.randn(N, Cin, H, W)
+    w = torch.randn(Cout, Cin, 3, 3) / np.sqrt(Cin * 9)
+    b = torch.randn(Cout) * 0.1
+    d = torch.rand(N, Cout) + 0.5
+    res = torch.randn(N, Cout, OH, OW)
+    xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    wp = cg._pack_conv(w.to(DEV, dtype))
+    tol = 5e-3 if dtype == torch.float16 else 2e-2
+    c = F.conv2d(x.to(dtype).double(), w.to(dtype).double(), stride=2)
+    y, _ = cg.conv3x3_fused(xd, wp, Cout, stride=2)                       # plain
+    assert y.shape == (N, Cout, OH, OW) and rel_err(y.float(), c) < tol
+    for n in range(N):
+        assert rel_err(y[n].float(), c[n]) < tol, n
+    y, raw = cg.conv3x3_fused(xd, wp, Cout, bias=b.to(DEV), act=1, alpha=0.2, gain=np.sqrt(2), clamp=1.5,
+                              want_raw=True, stride=2)
+    assert rel_err(raw.float(), c) < tol
+    assert rel_err(y.float(), (F.leaky_relu(c + b[None, :, None, None], 0.2) * np.sqrt(2)).clamp(-1.5, 1.5)) < tol
+    rd = res.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    y, za = cg.conv3x3_fused(xd, wp, Cout, bias=b.to(DEV), act=1, alpha=0.2, gain=np.sqrt(0.5), clamp=256.0,
+                             want_raw=True, stride=2, residual=rd, raw_act=True)
+    zr = F.leaky_relu(c + b[None, :, None, None], 0.2) * np.sqrt(0.5)
+    assert rel_err(za.float(), zr) < tol
+    assert torch.equal(y, (za.float() + rd.float()).to(dtype))            # round(z) + residual, rounded once more
+    y, raw = cg.conv3x3_fused(xd, wp, Cout, out_scale=d.to(DEV), want_raw=True, stride=2, residual=rd)
+    assert rel_err(raw.float(), c) < tol
+    assert rel_err(y.float(), c * d[:, :, None, None] + res.to(dtype).double()) < tol
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])

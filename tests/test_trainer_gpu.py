@@ -152,6 +152,9 @@ def test_pack_weight_multi_bitwise():
              (ws[2], 0, torch.float16, True, 0.5), (ws[3].transpose(0, 1), 0, torch.float16, False, 1.0),
              (ws[3], 1, torch.float32, True, 0.25)]
     ref = [cg._pack_raw(w, a, dt, fl, sc) for w, a, dt, fl, sc in forms]
+    for (w, a, dt, fl, sc), r in zip(forms, ref):     # the per-call pack itself against torch's expression
+        t = (w.detach().flip([2, 3]) if fl else w.detach()) * sc
+        assert torch.equal(r, t.permute(a, 2, 3, 1 - a).to(dt or w.dtype).contiguous())
     holder = {}
     for rnd in range(2):                          # first scope records the plan, the second packs up front
         with cg.pack_cache(plan=holder):

@@ -38,8 +38,16 @@ def shp(t):
 
 
 cg._conv_raw = wrap('conv', cg._conv_raw, lambda x, wp, cout, oh, ow, kh, kw, s, p, tr: shp(x) + (cout, oh, ow, kh, s, 'T' if tr else ''))
-cg.conv_fused = wrap('conv_fused', cg.conv_fused, lambda x, wp, cout, oh, ow, kh, kw, s, p, transpose=False, **k:
-                     shp(x) + (cout, oh, ow, kh, s, 'T' if transpose else '', 'dot' if k.get('dot_src') is not None else ''))
+def _fused_key(x, wp, cout, oh, ow, kh, kw, s, p, transpose=False, **k):
+    plain = all(k.get(n) is None for n in ('out_scale', 'noise', 'bias', 'residual', 'dot_src')) and \
+        k.get('act', 0) == 0 and k.get('gain', 1.0) == 1.0 and k.get('clamp', -1.0) < 0 and not k.get('aux_mode', 0)
+    be = 'up2' if plain and cg._up2_ok(x, cout, oh, ow, kh, kw, s, p, transpose) else \
+        ('generic16' if x.dtype != torch.float32 else 'generic32')
+    epi = '+'.join(n for n in ('in_scale', 'out_scale', 'bias', 'residual', 'dot_src') if k.get(n) is not None)
+    return shp(x) + (cout, oh, ow, kh, s, 'T' if transpose else '', be, epi)
+
+
+cg.conv_fused = wrap('conv_fused', cg.conv_fused, _fused_key)
 cg._wgrad_raw = wrap('wgrad', cg._wgrad_raw, lambda g, x, kh, kw, s, p, **k: shp(g) + tuple(x.shape[1:]) + (kh, s))
 cg.conv3x3_fused = wrap('conv3x3', cg.conv3x3_fused, lambda x, wp, cout, **k: shp(x) + (cout,))
 
@@ -57,5 +65,10 @@ for _ in range(16):
 torch.cuda.synchronize()
 tot = sum(v[1] for v in stats.values()) / 16
 print(f'conv calls: {sum(v[0] for v in stats.values()) / 16:.1f} per step, {tot:.2f} ms per step (synchronous)')
-for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])[:60]:
+fam = {}
+for k, v in stats.items():
+    b = k[-2] if k[0] == 'conv_fused' else k[0]
+    fam[b] = fam.get(b, 0.0) + v[1] / 16
+print('per backend (ms/step): ' + ', '.join(f'{b} {t:.2f}' for b, t in sorted(fam.items(), key=lambda kv: -kv[1])))
+for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])[:80]:
     print(f'{v[1] / 16:7.3f} ms/step {v[0] / 16:5.2f}/step {v[1] / v[0] * 1e3:8.1f} us  {k}')
