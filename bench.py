@@ -323,15 +323,29 @@ def roofline_families(device, dtype=torch.float16):
     def rnd(*shape):
         return torch.randn(shape, device=device, dtype=dtype).contiguous(memory_format=cl)
 
-    # generic implicit GEMM (conv_fwd_kernel): the D down-2 conv of the 256^2 block after its FIR (Dmain batch 64)
+    # the D down-2 conv of the 256^2 block after its FIR (Dmain batch 64) on its production route, the stride-2
+    # LDS-DMA implicit GEMM (conv3x3_s2g_kernel; the generic implicit GEMM before round 5)
     N, Ci, H, Co = 64, 64, 257, 128
     OH = (H - 3) // 2 + 1
     x = rnd(N, Ci, H, H)
     wp = cg._pack_conv((torch.randn(Co, Ci, 3, 3, device=device) / 24).to(dtype))
     b = torch.zeros(Co, device=device)
-    ms = _time_ms(lambda: cg.conv_fused(x, wp, Co, OH, OH, 3, 3, 2, (0, 0), bias=b, act=1, gain=1.41, clamp=256.0))
-    out['conv_fwd_generic'] = _roof_entry('conv_fwd_kernel (implicit GEMM)', f'D down-2 3x3 N{N} {Ci}x{H}^2 -> {Co}x{OH}^2',
-                                          ms, 2.0 * N * Co * Ci * 9 * OH * OH, (N * Ci * H * H + N * Co * OH * OH) * esz)
+    ms = _time_ms(lambda: cg.conv3x3_fused(x, wp, Co, bias=b, act=1, gain=1.41, clamp=256.0, stride=2))
+    out['d_down_s2g'] = _roof_entry('conv3x3_s2g_kernel (stride-2 LDS-DMA implicit GEMM)',
+                                    f'D down-2 3x3 N{N} {Ci}x{H}^2 -> {Co}x{OH}^2, bias + lrelu', ms,
+                                    2.0 * N * Co * Ci * 9 * OH * OH, (N * Ci * H * H + N * Co * OH * OH) * esz)
+    del x
+    # generic implicit GEMM (conv_fwd_kernel): its largest remaining launch, the 32^2 -> 65^2 up-2 transposed conv of
+    # the 64^2 synthesis block (G forward, modulated; the up-2 kernel serves 64^2 inputs and up)
+    N, Ci, H, Co = 32, 512, 32, 256
+    x = rnd(N, Ci, H, H)
+    wp = cg._pack_conv((torch.randn(Co, Ci, 3, 3, device=device) / 68).to(dtype))
+    s_ = torch.rand(N, Ci, device=device) + 0.5
+    OT = 2 * H + 1
+    ms = _time_ms(lambda: cg.conv_fused(x, wp, Co, OT, OT, 3, 3, 2, (0, 0), transpose=True, in_scale=s_))
+    out['conv_fwd_generic'] = _roof_entry('conv_fwd_kernel (implicit GEMM)',
+                                          f'up-2 transposed 3x3 N{N} {Ci}x{H}^2 -> {Co}x{OT}^2 (modulated)', ms,
+                                          2.0 * N * Co * Ci * 9 * H * H, (N * Ci * H * H + N * Co * OT * OT) * esz)
     del x
     # halo conv: the 128^2 C=128 synthesis layer (G forward, bs32)
     N, C, R = 32, 128, 128

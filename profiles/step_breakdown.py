@@ -19,7 +19,8 @@ win = [r for r in rows if t0 <= int(r['Start_Timestamp']) < t_end]
 
 
 def cat(n):
-    for key, name in [('conv3x3_c64p', 'halo conv 16-bit C=64 persistent'), ('conv3x3_c64r', 'ring conv 16-bit C=64'), ('conv3x3_halo', 'halo conv 16-bit'), ('wgrad3x3', 'halo wgrad 16-bit'),
+    for key, name in [('conv3x3_s2g', 'stride-2 GEMM 16-bit (D down)'), ('conv3x3_c32r', 'ring conv 16-bit C=32'),
+                      ('conv3x3_up2', 'up-2 conv 16-bit'), ('conv3x3_c64p', 'halo conv 16-bit C=64 persistent'), ('conv3x3_c64r', 'ring conv 16-bit C=64'), ('conv3x3_halo', 'halo conv 16-bit'), ('wgrad3x3', 'halo wgrad 16-bit'),
                       ('conv_fwd_kernel<float', 'generic conv f32'), ('conv_fwd_kernel', 'generic conv 16-bit'),
                       ('conv_wgrad_kernel<float', 'generic wgrad f32'), ('conv_wgrad_kernel', 'generic wgrad 16-bit'),
                       ('layer_bwd', 'layer_bwd'), ('bias_act', 'bias_act'), ('demod', 'demod'), ('Cijk', 'GEMM'),
@@ -44,3 +45,13 @@ tot = sum(v[0] for v in agg.values())
 print(f'{len(win) / 16:.0f} launches / step, {tot / 16e6:.1f} ms kernel time / step (step {ms} ms)')
 for k, (t, n) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
     print(f'{t / 16e6:7.2f} ms/step {n / 16:7.1f} launches/step  {k}')
+# the glue families by kernel (what "torch elementwise" and "other" are made of)
+glue = defaultdict(lambda: [0, 0])
+for r in win:
+    if cat(r['Kernel_Name']) in ('torch elementwise / reduce / copy', 'other'):
+        g = glue[r['Kernel_Name'][:110]]
+        g[0] += int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+        g[1] += 1
+print('glue kernels (torch elementwise / other), top 25:')
+for k, (t, n) in sorted(glue.items(), key=lambda kv: -kv[1][0])[:25]:
+    print(f'{t / 16e6:7.3f} ms/step {n / 16:7.1f} launches/step  {k}')

@@ -37,12 +37,17 @@ for p, r in emu.items():
 prod = []
 for seed in range(K + 1):
     cfg_, inp_, tape_, _ = cp.load_fixture(np.load(FIX))
-    got, _ = cp.run_product(cfg_, inp_, tape_, dev, fp16_dtype=torch.float16 if dt == 'fp16' else torch.bfloat16,
-                            aug_p=cfg_['aug_p'], isolated=True, perturb=2.0 ** -23 if seed else 0.0,
-                            perturb_seed=seed)
+    got, stats = cp.run_product(cfg_, inp_, tape_, dev, fp16_dtype=torch.float16 if dt == 'fp16' else torch.bfloat16,
+                                aug_p=cfg_['aug_p'], isolated=True, perturb=2.0 ** -23 if seed else 0.0,
+                                perturb_seed=seed)
     r = cp.compare_flat(got, truth, GROUPS)
     prod.append(r)
     print(row(f'prod s{seed}', r), flush=True)
+    for j, (n, v) in enumerate(stats):      # the R1 penalty per sample against float64
+        if 'r1_penalty' in n:
+            t = np.asarray(fix[f'f64/stats/{j}'], np.float64)
+            print('           r1_penalty vs f64: ' + ' '.join(f'{x:+.4f}' for x in (np.asarray(v, np.float64) / t - 1).ravel()),
+                  flush=True)
 for lab, rs in (('emu', list(emu.values())), ('prod', prod)):
     print(f'{lab:5s} median ' + '  '.join(f'{g[5:]} {np.median([r[g][0] for r in rs]):.4f}/'
                                         f'{np.median([r[g][1] for r in rs]):.4f}' for g in GROUPS))
