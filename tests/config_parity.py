@@ -184,14 +184,14 @@ def _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated, pertu
     from training import networks_stylegan2 as net, augment_mi, loss as loss_mod, trainer as trainer_mod
     torch.manual_seed(0)
     G, D = _nets(net, cfg, 0 if fp16_dtype is None else 4, fp16_dtype)
-    if perturb:
+    if perturb:     # the same signs, in the same order, as run_oracle's nudge (the state rounded to f32)
         gen = torch.Generator().manual_seed(perturb_seed)
         with torch.no_grad():
             for mod in (G, D):
                 for _, p in sorted(mod.named_parameters()):
-                    p.copy_(_perturb(p.float(), perturb, gen))
-        inp = dict(inp, **{k: _perturb(torch.from_numpy(np.asarray(inp[k], np.float32)), perturb, gen).numpy()
-                           for k in ('real', 'gen_z')})
+                    p.copy_(_perturb(p.detach().cpu().double(), perturb, gen).float())
+        inp = {k: (_perturb(torch.from_numpy(np.asarray(v, np.float64)), perturb, gen).float().numpy()
+                   if k in ('real', 'gen_z', 'z') else v) for k, v in inp.items()}
     G, D = G.to(dev), D.to(dev)
     G_ema = copy.deepcopy(G).eval()
     aug = augment_mi.AugmentPipe(run_dir=None, batch_size=cfg['batch'], **CLARO_AUG).train().requires_grad_(False).to(dev)

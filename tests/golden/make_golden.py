@@ -19,6 +19,7 @@ Outputs: tests/golden/*.npz (small, committed).
 import copy
 import zlib
 import os
+import re
 import sys
 import types
 
@@ -557,6 +558,53 @@ def merge_emulated16_nudged(tag, cache_dir):
     print(tag, n, 'nudged 16-bit emulation samples merged', flush=True)
 
 
+def gen_emulated16_perturbed(tag, dts, seed, k, cache_dir):
+    """Same-state samples for the 16-bit comparison: the fixture's state nudged by (1 +- 2^-k) (seeded signs;
+    k = 12 moves each entry by 1/16 of a bf16 ulp, so every sample redraws the 16-bit rounding pattern, which the
+    half-f32-ulp nudges of emu16n do not), the float64 answer at that state and the emulated reference's 16-bit
+    evaluation of it in each type of `dts`, saved to <cache_dir>/p<k>_<tag>_<f64|fp16|bf16>_<seed>.npz;
+    emu16pmerge folds them in as 'f64p<k>s<seed>/', 'q16p<k>s<seed>/', 'qbfp<k>s<seed>/'.  The product runs at the
+    same states (config_parity.run_product perturb: the same signs in the same order, the state rounded to f32)."""
+    import config_parity as cp
+    path = os.path.join(OUT, f'train_{tag}.npz')
+    os.makedirs(cache_dir, exist_ok=True)
+    for dt in ['f64'] + list(dts):
+        fn = os.path.join(cache_dir, f'p{k}_{tag}_{dt}_{seed}.npz')
+        if os.path.exists(fn):
+            continue
+        with np.load(path, allow_pickle=False) as f:
+            cfg, inp, tape, _ = cp.load_fixture(f)
+        out, _ = cp.run_oracle_f64(cfg, inp, tape, cfg.get('aug_p', 0.3), perturb=2.0 ** -k, perturb_seed=int(seed),
+                                   isolated=cfg.get('isolated', False),
+                                   emu16=None if dt == 'f64' else {'fp16': torch.float16, 'bf16': torch.bfloat16}[dt])
+        tmp = fn + '.tmp.npz'
+        np.savez_compressed(tmp, **pack(out))
+        os.replace(tmp, fn)
+        print(tag, dt, k, seed, 'perturbed sample written', flush=True)
+
+
+def merge_emulated16_perturbed(tag, cache_dir):
+    from golden_init import unpack
+    import glob
+    path = os.path.join(OUT, f'train_{tag}.npz')
+    with np.load(path, allow_pickle=False) as f:
+        z = unpack(f)
+    z = {kk: v for kk, v in z.items() if not re.match(r'(f64|q16|qbf)p\d+s\d+/', kk)}
+    n = 0
+    for fn in sorted(glob.glob(os.path.join(cache_dir, f'p*_{tag}_*.npz'))):
+        m = re.match(r'p(\d+)_' + re.escape(tag) + r'_(f64|fp16|bf16)_(\d+)\.npz$', os.path.basename(fn))
+        if not m:
+            continue
+        pre = {'f64': 'f64', 'fp16': 'q16', 'bf16': 'qbf'}[m.group(2)] + f'p{m.group(1)}s{m.group(3)}'
+        with np.load(fn, allow_pickle=False) as f:
+            z.update({f'{pre}/{kk}': v for kk, v in unpack(f).items()})
+        n += 1
+    tmp = path + '.tmp.npz'
+    np.savez_compressed(tmp, **pack(z))
+    os.replace(tmp, path)
+    print(tag, n, 'perturbed samples merged', flush=True)
+
+
 def gen_emulated16(tag, dt):
     """Add 'q16/...' (dt fp16) or 'qbf/...' (bf16) to train_<tag>.npz: the oracle's emulation of the reference's
     16-bit GPU evaluation of the fixture (oracle.sg2_oracle.EMU16: the num_fp16_res = 4 blocks round every tensor
@@ -637,6 +685,12 @@ if __name__ == '__main__':
         if w.startswith('emu16n:'):        # emu16n:<tag>:<fp16|bf16>:<seed>   (to $GOLD_CACHE)
             parts = w.split(':')
             gen_emulated16_nudged(parts[1], parts[2], parts[3], os.environ.get('GOLD_CACHE', '/tmp/gold'))
+        if w.startswith('emu16p:'):        # emu16p:<tag>:<fp16,bf16>:<seed>[:<k, default 12>]   (to $GOLD_CACHE)
+            parts = w.split(':')
+            gen_emulated16_perturbed(parts[1], parts[2].split(','), parts[3], int(parts[4]) if len(parts) > 4 else 12,
+                                     os.environ.get('GOLD_CACHE', '/tmp/gold'))
+        if w.startswith('emu16pmerge:'):   # emu16pmerge:<tag>
+            merge_emulated16_perturbed(w.split(':')[1], os.environ.get('GOLD_CACHE', '/tmp/gold'))
         if w.startswith('emu16nmerge:'):   # emu16nmerge:<tag>
             merge_emulated16_nudged(w.split(':')[1], os.environ.get('GOLD_CACHE', '/tmp/gold'))
         if w.startswith('emu32:'):         # emu32:<tag>:<sample k>   (to $GOLD_CACHE, default /tmp/gold)

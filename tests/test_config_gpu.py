@@ -22,6 +22,8 @@ The phase-isolated tests run the product both in the library's deterministic mod
 order reductions, so a result is a function of the code and the fixture; tests/test_deterministic_gpu.py checks two
 runs bitwise equal) and in its default atomic mode, the arithmetic bench.py times.
 """
+import re
+
 import numpy as np
 import pytest
 import torch
@@ -131,50 +133,81 @@ def test_f32_phases_vs_reference(tag, arith):
 # 16-bit (num_fp16_res = 4, the reference's GPU default; f32 accumulation) against the float64 answer of the same
 # isolated phases, held to the REFERENCE's own 16-bit error: the fixtures carry the oracle's emulation of the
 # reference's fp16 GPU iteration (q16/, qbf/: make_golden.py `emu:<tag>:<dt>`, oracle.sg2_oracle.EMU16 -- every
-# tensor and gradient of a use_fp16 block rounded where the reference's is) and the same emulation at states nudged
-# by half an f32 ulp (q16n<seed>/, qbfn<seed>/: `emu16n:`), each another draw of the rounding pattern.  The product
-# is evaluated the same way: at the fixture state and at NUDGES states nudged by one f32 ulp
-# (config_parity.run_product perturb), so both sides are distributions.  Per phase and error measure -- the
-# relative error of the vector of tensor norms and of the whole flat gradient (config_parity.compare_flat), each
-# bounded by the SAME measure only -- the product's median is held to EMU_FACTOR x the emulation's median and the
-# product's largest draw to EMU_FACTOR x the emulation's largest (floor ISO16_FLOOR).  One draw alone is not a
-# fair statistic: the 16-bit measures are heavy-tailed (C2 bf16 Dreg norm vector, product over 7 states: median
-# 0.0028, draws 0.0014 .. 0.0165; emulation median 0.0027 -- profiles/r05_nudge16.txt).  Run in deterministic mode
-# and with the float atomics the bench times.
+# tensor and gradient of a use_fp16 block rounded where the reference's is).  The 16-bit error measures are
+# heavy-tailed functions of the state (which lrelu masks and 16-bit roundings fall which way), so one draw against
+# one draw is no comparison: both sides are evaluated over a set of states and compared as distributions.
+#   * Same-state samples (C1, C2: make_golden.py `emu16p`): the fixture state and states nudged by (1 +- 2^-12)
+#     (seeded signs: 1/16 of a bf16 ulp, so every state redraws the 16-bit rounding pattern), each with its OWN
+#     float64 answer (f64p12s<seed>/) and the emulation there (q16p12s<seed>/, qbfp12s<seed>/); the product runs at
+#     the same states (config_parity.run_product perturb: the same signs in the same order, rounded to f32).
+#   * Otherwise (C4, C5, whose float64 runs are too long to repeat): the emulation at half-f32-ulp nudges of the
+#     fixture state (q16n<seed>/, qbfn<seed>/: `emu16n`) against the product at one-ulp nudges -- a weaker sample
+#     (a half-ulp nudge flips few 16-bit roundings; profiles/r05_nudge16.txt).
+# Per phase and error measure -- the relative error of the vector of tensor norms and of the whole flat gradient
+# (config_parity.compare_flat), each bounded by the SAME measure only -- the product's median over its states is
+# held to EMU_FACTOR x the emulation's median and its largest to EMU_FACTOR x the emulation's largest (floor
+# ISO16_FLOOR).  Run in deterministic mode and with the float atomics the bench times.
 EMU_FACTOR = 2.0
 ISO16_FLOOR = {'fp16': 5e-3, 'bf16': 1e-2}
 EMU_KEY = {'fp16': 'q16', 'bf16': 'qbf'}
 NUDGES = 4
 
 
-@pytest.mark.timeout(300)
+def _sub(fix, pre):
+    return {k[len(pre) + 1:]: v for k, v in fix.items() if k.startswith(pre + '/')}
+
+
+def _same_states(fix, dt):
+    """[(k, seed, truth prefix, emulation prefix)]: the fixture state and every same-state sample in the fixture."""
+    out = []
+    for p in sorted({k.split('/', 1)[0] for k in fix if re.match(r'f64p\d+s\d+/', k)}):
+        m = re.match(r'f64p(\d+)s(\d+)$', p)
+        e = f'{EMU_KEY[dt]}p{m.group(1)}s{m.group(2)}'
+        if any(k.startswith(e + '/') for k in fix):
+            out.append((int(m.group(1)), int(m.group(2)), p, e))
+    return [(0, 0, 'f64', EMU_KEY[dt])] + out if out else []
+
+
+@pytest.mark.timeout(400)
 @pytest.mark.parametrize('det', [True, False], ids=['det', 'atomic'])
 @pytest.mark.parametrize('tag,dt', [('c1', 'fp16'), ('c1', 'bf16'), ('c2', 'fp16'), ('c2', 'bf16'), ('c4', 'fp16'),
                                     ('c5', 'bf16')])
 def test_16bit_phases(tag, dt, det):
-    truth = None
-    runs = []
-    for seed in range(NUDGES + 1):
-        cfg, inp, tape, fix = _iso(tag)
-        got, _ = cp.run_product(cfg, inp, tape, DEV, fp16_dtype=torch.float16 if dt == 'fp16' else torch.bfloat16,
-                                aug_p=cfg['aug_p'], isolated=True, deterministic=det,
-                                perturb=2.0 ** -23 if seed else 0.0, perturb_seed=seed)
-        if truth is None:
-            truth = _truth(fix)
-            cp.save_summary(f'{tag}_iso_{dt}_{"det" if det else "atomic"}', got)
-        runs.append(cp.compare_flat(got, truth, ISO_GROUPS))
+    cfg, inp, tape, fix = _iso(tag)
+    assert any(k.startswith(EMU_KEY[dt] + '/') for k in fix), \
+        f'train_{tag}_iso.npz has no {EMU_KEY[dt]}/ summaries (make_golden.py emu:{tag}_iso:{dt})'
+    states = _same_states(fix, dt)
+    fp = torch.float16 if dt == 'fp16' else torch.bfloat16
+    runs, refs = [], []
+    if states:
+        for k, seed, tp, ep in states:
+            cfg, inp, tape, _ = _iso(tag)
+            got, _ = cp.run_product(cfg, inp, tape, DEV, fp16_dtype=fp, aug_p=cfg['aug_p'], isolated=True,
+                                    deterministic=det, perturb=2.0 ** -k if k else 0.0, perturb_seed=seed)
+            if not k:
+                cp.save_summary(f'{tag}_iso_{dt}_{"det" if det else "atomic"}', got)
+            truth = _sub(fix, tp)
+            runs.append(cp.compare_flat(got, truth, ISO_GROUPS))
+            refs.append(cp.compare_flat(_sub(fix, ep), truth, ISO_GROUPS))
+    else:
+        truth = _truth(fix)
+        for seed in range(NUDGES + 1):
+            cfg, inp, tape, _ = _iso(tag)
+            got, _ = cp.run_product(cfg, inp, tape, DEV, fp16_dtype=fp, aug_p=cfg['aug_p'], isolated=True,
+                                    deterministic=det, perturb=2.0 ** -23 if seed else 0.0, perturb_seed=seed)
+            if not seed:
+                cp.save_summary(f'{tag}_iso_{dt}_{"det" if det else "atomic"}', got)
+            runs.append(cp.compare_flat(got, truth, ISO_GROUPS))
+        pres = sorted({k.split('/', 1)[0] for k in fix if k.split('/', 1)[0] == EMU_KEY[dt] or
+                       re.match(EMU_KEY[dt] + r'n\d+/', k)})
+        refs = [cp.compare_flat(_sub(fix, p), truth, ISO_GROUPS) for p in pres]
     mode = 'det' if det else 'atomic'
-    pres = sorted({k.split('/', 1)[0] for k in fix if k.split('/', 1)[0] == EMU_KEY[dt] or
-                   (k.startswith(EMU_KEY[dt] + 'n') and '/' in k)})
-    assert EMU_KEY[dt] in pres, f'train_{tag}_iso.npz has no {EMU_KEY[dt]}/ summaries (make_golden.py emu:{tag}_iso:{dt})'
-    refs = {p: cp.compare_flat({k[len(p) + 1:]: v for k, v in fix.items() if k.startswith(p + '/')}, truth, ISO_GROUPS)
-            for p in pres}
-    cp.record(f'{tag}_iso_{dt}_{mode}', dict(flat=runs[0], flat_nudged=runs[1:], reference_16bit_flat=refs))
+    cp.record(f'{tag}_iso_{dt}_{mode}', dict(same_state=bool(states), product=runs, reference_16bit=refs))
     fails = []
     for g in ISO_GROUPS:
         for j, meas in enumerate(('norm-vector', 'flat')):
             pv = [r[g][j] for r in runs]
-            ev = [r[g][j] for r in refs.values()]
+            ev = [r[g][j] for r in refs]
             for stat, f in (('median', np.median), ('max', max)):
                 bound = max(ISO16_FLOOR[dt], EMU_FACTOR * float(f(ev)))
                 if float(f(pv)) > bound:

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5, call o: SQ counter passes on the stride-2 LDS-DMA GEMM (two D down shapes)
 set -o pipefail
-O=gpurun_out/r05o
+O=gpurun_out/r05p/pmc_s2g
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES"
