@@ -56,6 +56,9 @@ struct Conv3Args {
     float* det_dot;         // deterministic mode: [N, OH, OW, Cout] per-element dot products (det_sum adds them)
 };
 
+// Output channel of MFMA row P of a 64-channel tile (see the C = 64 kernels below)
+__device__ __forceinline__ int p_chan(int P) { return (P >> 5) * 32 + 8 * ((P & 15) >> 2) + 4 * ((P >> 4) & 1) + (P & 3); }
+
 template <typename T>
 using v8 = typename std::conditional<std::is_same<T, bf16_t>::value, bf16x8, f16x8>::type;
 
@@ -74,8 +77,13 @@ __device__ __forceinline__ f32x4 mma(v8<T> a, v8<T> b, f32x4 c) {
 // blocks' conv1 and the input gradient of the G up layers) on a 32 x 4 output tile: the (2 TW + 1) x
 // (2 TH + 1) input halo is stored column-deinterleaved (a halo row = its even columns, then its odd ones),
 // so a fragment read of 16 output pixels (input columns 2 apart) is 16 consecutive swizzled LDS rows.
-template <typename T, int TW, bool SCALE_IN, bool EPI, int NBUF, int S = 1>
+// DIR (round 5; S = 1, Cout % 64 == 0): the MFMA operands swapped (weights as A, pixels as B) and the weight rows
+// staged in p_chan order, so a lane's accumulators hold 8 consecutive output channels of one pixel and the epilogue
+// stores 16 bytes per lane straight from registers -- no output tile through LDS, no epilogue barrier (the dot
+// reduction: 16-lane shuffles, LDS atomics, one global atomic per channel).
+template <typename T, int TW, bool SCALE_IN, bool EPI, int NBUF, int S = 1, bool DIR = false>
 __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a) {   // NBUF = 1: two workgroups per CU
+    static_assert(!DIR || S == 1, "the direct epilogue is the stride-1 form");
     constexpr int TH = S == 1 ? 256 / TW : 4;
     constexpr int PXW = TW * TH / 4, NFR = PXW / 16;                 // pixels and 16-pixel fragments per wave
     constexpr int HW_ = S * (TW - 1) + 3, HH = S * (TH - 1) + 3, HP = HW_ * HH;   // halo pixels
@@ -122,7 +130,7 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
         const int r = idx >> 2;                    // 0 .. 9*BN-1
         const int tap = r / BN, o = r - tap * BN;
         w_ok[i] = o0 + o < a.Cout;
-        w_src[i] = (w_ok[i] ? (o0 + o) : 0) * 9 + tap;              // row index in [Cout*9]
+        w_src[i] = (w_ok[i] ? (o0 + (DIR ? p_chan(o) : o)) : 0) * 9 + tap;   // row index in [Cout*9]
         w_dst[i] = swz64(tap * BN + o, idx & 3);   // byte offset
     }
 
@@ -210,7 +218,7 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
 #pragma unroll
                 for (int i = 0; i < NFR; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j] = mma<T>(af[i], bfr[j], acc[i][j]);
+                    for (int j = 0; j < 4; ++j) acc[i][j] = DIR ? mma<T>(bfr[j], af[i], acc[i][j]) : mma<T>(af[i], bfr[j], acc[i][j]);
             }
         }
         if (NBUF == 1 && more) __syncthreads();   // everyone done reading before the overwrite
@@ -218,6 +226,89 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
         __syncthreads();
     }
 
+    if constexpr (DIR) {
+        // lane (l16, q): pixel wave PXW + 16 i + l16 of the tile, channels o0 + 32 h + 8 q + e (e = 4 jj + r)
+        float dsc[2][8], bsc[2][8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int o = o0 + 32 * h + 8 * lq + e;
+                dsc[h][e] = (EPI && a.out_scale) ? a.out_scale[(int64_t)n * a.Cout + o] : 1.f;
+                bsc[h][e] = (EPI && a.bias) ? (float)(T)a.bias[o] : 0.f;
+            }
+        typedef T vec8d __attribute__((ext_vector_type(8)));
+        const bool want_dot = a.dot_out != nullptr, atom = want_dot && !a.det_dot;
+        float* red = (float*)smem;                 // [BN] dot partial sums (the halo buffer is free after the loop)
+        if (atom) {
+            if (tid < BN) red[tid] = 0.f;
+            __syncthreads();
+        }
+        float dacc[2][8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dacc[h][e] = 0.f;
+        T* y = (T*)a.y;
+        T* yr = (T*)a.y_raw;
+        const T* dsrc = (const T*)a.dot_src;
+        const T* nz = (const T*)a.noise;
+#pragma unroll
+        for (int i = 0; i < NFR; ++i) {
+            const int m = wave * PXW + i * 16 + l16;
+            const int py = m / TW, px = m - py * TW;
+            const int oy = ty0 + py, ox = tx0 + px;
+            const bool ok = oy < a.OH && ox < a.OW;
+            const int64_t pix = ((int64_t)n * a.OH + (ok ? oy : 0)) * a.OW + (ok ? ox : 0);
+            const float nv = (EPI && nz) ? (float)nz[pix] * a.noise_gain : 0.f;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                vec8d yv, rv;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float v = acc[i][2 * h + (e >> 2)][e & 3];
+                    rv[e] = (T)v;
+                    if (EPI) {
+                        v = v * dsc[h][e] + nv + bsc[h][e];
+                        if (a.act == 1) v = v > 0.f ? v : v * a.alpha;
+                        v *= a.gain;
+                        if (a.clamp >= 0.f) v = fminf(fmaxf(v, -a.clamp), a.clamp);
+                    }
+                    yv[e] = (T)v;
+                }
+                if (!ok) continue;
+                const int64_t dst = pix * a.Cout + o0 + 32 * h + 8 * lq;
+                *(vec8d*)(y + dst) = yv;
+                if (yr) *(vec8d*)(yr + dst) = rv;
+                if (want_dot) {
+                    const vec8d sv = *(const vec8d*)(dsrc + dst);
+                    if (a.det_dot) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) a.det_dot[dst + e] = (float)rv[e] * (float)sv[e];
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) dacc[h][e] += (float)rv[e] * (float)sv[e];
+                    }
+                }
+            }
+        }
+        if (atom) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float v = dacc[h][e];
+                    v += __shfl_xor(v, 1);
+                    v += __shfl_xor(v, 2);
+                    v += __shfl_xor(v, 4);
+                    v += __shfl_xor(v, 8);
+                    if (l16 == 0) atomicAdd(&red[32 * h + 8 * lq + e], v);
+                }
+            __syncthreads();
+            if (tid < BN) atomicAdd(&a.dot_out[(int64_t)n * a.Cout + o0 + tid], red[tid]);
+        }
+        return;
+    }
     // ---- epilogue: fused math in registers, transpose through LDS, 16-byte row stores ----
     // per-lane channel parameters (n is fixed per workgroup).  (Fetching these and the noise before
     // the main loop raised register pressure past two workgroups per CU: measured slower.)
@@ -326,12 +417,12 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
     }
 }
 
-template <typename T, int TW, bool SI, bool EPI, int NBUF, int S = 1>
-int launch3(const Conv3Args& a, hipStream_t s) {
+template <typename T, int TW, bool SI, bool EPI, int NBUF, int S = 1, bool DIR = false>
+int launch3_k(const Conv3Args& a, hipStream_t s) {
     constexpr int TH = S == 1 ? 256 / TW : 4;
     size_t lds = NBUF * (size_t)((S * (TW - 1) + 3) * (S * (TH - 1) + 3) * PX + 9 * BN * PX) * sizeof(T);
-    lds = std::max(lds, (size_t)2 * TW * TH * (BN + 8) * sizeof(T) + BN * sizeof(float));   // epilogue tiles
-    auto kern = conv3x3_halo_kernel<T, TW, SI, EPI, NBUF, S>;
+    if (!DIR) lds = std::max(lds, (size_t)2 * TW * TH * (BN + 8) * sizeof(T) + BN * sizeof(float));   // epilogue tiles
+    auto kern = conv3x3_halo_kernel<T, TW, SI, EPI, NBUF, S, DIR>;
     static bool attr_set = false;   // benign race: idempotent attribute
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -340,6 +431,18 @@ int launch3(const Conv3Args& a, hipStream_t s) {
     dim3 grid(a.N * a.tiles_x * a.tiles_y, (a.Cout + BN - 1) / BN);
     kern<<<grid, 256, lds, s>>>(a);
     return launch_status("sg2_conv3x3");
+}
+
+template <typename T, int TW, bool SI, bool EPI, int NBUF, int S = 1>
+int launch3(const Conv3Args& a, hipStream_t s) {
+    if constexpr (S == 1) {
+        // the direct epilogue (SG2_HALO_DIRECT=0: the LDS-transposed one); read per launch: tests switch it
+        const char* e = getenv("SG2_HALO_DIRECT");
+        if ((!e || atoi(e) != 0) && a.Cout % BN == 0 && ((uintptr_t)a.y % 16) == 0 && ((uintptr_t)a.y_raw % 16) == 0 &&
+            ((uintptr_t)a.dot_src % 16) == 0)
+            return launch3_k<T, TW, SI, EPI, NBUF, 1, true>(a, s);
+    }
+    return launch3_k<T, TW, SI, EPI, NBUF, S, false>(a, s);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -388,7 +491,6 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // Output channel of MFMA row m (0..15) of channel tile j (A-operand row P = 16 j + m): tiles 2jj, 2jj+1 give
 // lane group q the 8 consecutive channels 32 jj + 8 q .. +7 (rows 4q..4q+3 of each), so the epilogue stores
 // 16 bytes per lane and pixel instead of 8 (a store-issue-bound tail: MI355X_MICROARCH.md latency table).
-__device__ __forceinline__ int p_chan(int P) { return (P >> 5) * 32 + 8 * ((P & 15) >> 2) + 4 * ((P >> 4) & 1) + (P & 3); }
 __device__ __forceinline__ int swz(int pos, int q) { return pos * P_POS + ((q ^ ((pos >> 1) & 2)) << 4); }
 
 template <typename T, bool SCALE_IN, bool EPI, bool DOT>

@@ -440,6 +440,50 @@ def test_conv3x3_fused(shape, dtype):
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize('shape', [(2, 64, 20, 37, 128), (1, 256, 33, 40, 192), (3, 128, 16, 16, 64),
+                                   (2, 512, 32, 32, 512)])
+@pytest.mark.parametrize('direct', ['1', '0'])
+def test_conv3x3_halo_direct(dtype, shape, direct, monkeypatch):
+    """The halo kernel's direct epilogue (conv3x3.hip DIR: swapped MFMA operands, p_chan weight rows, 16-byte
+    stores from registers; direct '0': the LDS-transposed epilogue) against float64: the modulated layer with the
+    full epilogue and its raw output, and the dgrad form (out_scale + dot) with float atomics and in
+    deterministic mode.  Ragged tiles (20 x 37, 33 x 40), TW = 16 (16 x 16), 1..8 channel tiles."""
+    import sg2hip
+    from torch_utils.ops import conv2d_gradfix as cg
+    monkeypatch.setenv('SG2_HALO_DIRECT', direct)
+    monkeypatch.setenv('SG2_C64_RING', '0')
+    N, Cin, H, W, Cout = shape
+    torch.manual_seed(13)
+    x = torch.randn(N, Cin, H, W)
+    w = torch.randn(Cout, Cin, 3, 3) / np.sqrt(Cin * 9)
+    s = torch.rand(N, Cin) + 0.5
+    d = torch.rand(N, Cout) + 0.5
+    noise = torch.randn(N, 1, H, W)
+    b = torch.randn(Cout) * 0.1
+    xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+    wp = cg._pack_conv(w.to(DEV, dtype))
+    y, raw = cg.conv3x3_fused(xd, wp, Cout, in_scale=s.to(DEV), out_scale=d.to(DEV),
+                              noise=noise.to(DEV, dtype).reshape(N, H, W).contiguous(), noise_gain=0.3,
+                              bias=b.to(DEV), act=1, alpha=0.2, gain=np.sqrt(2), clamp=1.5, want_raw=True)
+    xs = (x.to(dtype).float() * s[:, :, None, None]).to(dtype).double()
+    c = F.conv2d(xs, w.to(dtype).double(), padding=1)
+    z = c * d[:, :, None, None] + noise.to(dtype).double() * 0.3 + b[None, :, None, None]
+    yr = (F.leaky_relu(z, 0.2) * np.sqrt(2)).clamp(-1.5, 1.5)
+    tol = 5e-3 if dtype == torch.float16 else 2e-2
+    assert rel_err(raw.float(), c) < tol and rel_err(y.float(), yr) < tol
+    for n in range(N):
+        assert rel_err(y[n].float(), yr[n]) < 2 * tol, n
+    src = torch.randn(N, Cout, H, W).to(dtype)
+    c0 = F.conv2d(x.to(dtype).double(), w.to(dtype).double(), padding=1)
+    for det in (False, True):
+        with sg2hip.deterministic(det, device=DEV):
+            y, _, dot = cg.conv3x3_fused(xd, wp, Cout, out_scale=d.to(DEV),
+                                         dot_src=src.to(DEV).contiguous(memory_format=torch.channels_last))
+        assert rel_err(y.float(), c0 * d[:, :, None, None]) < tol
+        assert rel_err(dot, (c0.to(dtype).double() * src.double()).sum([2, 3])) < tol
+
+
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
 def test_fused_synthesis_layer_matches_composed(dtype):
     """SynthesisLayer through the one-kernel path (sg2_conv3x3 + ModConvLayer backward) vs the composed
     path (x*s, conv, fma, bias_act kernels): outputs, first-order grads and the PL-style second-order
