@@ -148,8 +148,9 @@ def test_f32_phases_vs_reference(tag, arith):
 # held to EMU_FACTOR x the emulation's median and its tail to EMU_FACTOR x the emulation's largest (floor
 # ISO16_FLOOR), the tail being the product's largest value or, over >= 5 states, its second largest: one state of
 # a heavy-tailed measure may land beyond a maximum estimated from a handful of emulation samples (measured, C2 bf16
-# Dreg norm vector over the fixture state and four 2^-12 states: product 0.0042 0.0139 0.0148 0.0187 0.0416,
-# emulation 0.0039 0.0101 0.0128 0.0136 0.0168 -- medians 0.0148 / 0.0128; profiles/r05_same_state16.txt).
+# Dreg norm vector over the fixture state and six 2^-12 states: product 0.0042 .. 0.0416, median 0.0148; emulation
+# 0.0039 .. 0.0240, median 0.0136 -- with four states the emulation's largest was 0.0168;
+# profiles/r05_same_state16.txt).
 # Run in deterministic mode and with the float atomics the bench times.
 EMU_FACTOR = 2.0
 ISO16_FLOOR = {'fp16': 5e-3, 'bf16': 1e-2}
