@@ -520,6 +520,152 @@ __global__ __launch_bounds__(256) void wgrad3x3_s2_kernel(W3Args a) {
     }
 }
 
+// Pipelined form of the stride-2 kernel above (round 5).  That kernel holds a 99 KB single LDS buffer, so one
+// workgroup (one wave per SIMD, 390 registers) runs per CU and every tile ends with compute, barrier, staging
+// store, barrier: the matrix pipe idles through the store and both barriers (mfma_util 0.25, and the LDS bank
+// conflicts it shows -- 0.40 of the LDS cycles -- are not what bounds it: the swizzled layout removes them and
+// is 5 % slower, profiles/r05_pmc_wgrad.txt).  Here the g tile is 16 x 6 (96 pixels; the x region 33 x 13) and the
+// LDS holds two stages (2 x 75.6 KB): tile t's MFMAs read stage t & 1 while tile t + 1's registers are stored
+// into the other stage between its third and fourth k-step, the loads of tile t + 2 are issued right after that
+// store, and ONE barrier ends the tile.
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad3x3_s2p_kernel(W3Args a) {
+    constexpr int LD = LDP;
+    constexpr int TW = 16, TH = 6, NP = TW * TH;          // g tile (96 px, 6 k-steps of 16)
+    constexpr int XW = 2 * TW + 1, XH = 2 * TH + 1, XEV = TW + 1, HP = XW * XH;   // x region (429 px)
+    constexpr int GCH = NP * 8 / 256;                     // 3 g loads per thread
+    constexpr int XCH = (HP * 8 + 255) / 256;             // 14 x loads per thread
+    constexpr int STAGE = (NP + HP) * LD;                 // elements per stage
+    typedef T vec8 __attribute__((ext_vector_type(8)));
+    extern __shared__ __attribute__((aligned(16))) char smem_w[];
+    T* const st0 = (T*)smem_w;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wa = wave >> 1, wb = wave & 1;
+    const int a0 = blockIdx.x * BC, b0 = blockIdx.y * BC;
+    const int t_begin = blockIdx.z * a.tiles_per_block;
+    const int t_end = min(a.tiles, t_begin + a.tiles_per_block);
+    const T* __restrict__ gp = (const T*)a.g;
+    const T* __restrict__ xp = (const T*)a.x;
+    const int cc = (tid & 7) * 8;
+    const bool a_ok = a0 + cc < a.A, b_ok = b0 + cc < a.B;
+
+    vec8 rg[GCH], rx[XCH];
+    float gsc[8], xsc[8];
+    const __amdgpu_buffer_rsrc_t rgb = make_rsrc(gp, (int64_t)a.N * a.GH * a.GW * a.A * (int64_t)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rxb = make_rsrc(xp, (int64_t)a.N * a.XH * a.XW * a.B * (int64_t)sizeof(T));
+    auto gload = [&](int t) {
+        const int per = a.tiles_x * a.tiles_y;
+        const int n = t / per, r = t - n * per;
+        const int ty0 = (r / a.tiles_x) * TH, tx0 = (r % a.tiles_x) * TW;
+#pragma unroll
+        for (int i = 0; i < GCH; ++i) {
+            const int px = (tid >> 3) + i * 32;
+            const int oy = ty0 + px / TW, ox = tx0 + px % TW;
+            const bool ok = a_ok && oy < a.GH && ox < a.GW;
+            rg[i] = buf_load16<vec8>(rgb, ok ? (((n * a.GH + oy) * a.GW + ox) * a.A + a0 + cc) * (int)sizeof(T) : -1);
+        }
+#pragma unroll
+        for (int i = 0; i < XCH; ++i) {
+            const int hp = (tid >> 3) + i * 32;
+            const int iy = 2 * ty0 + hp / XW, ix = 2 * tx0 + hp % XW;
+            const bool ok = b_ok && hp < HP && iy < a.XH && ix < a.XW;
+            rx[i] = buf_load16<vec8>(rxb, ok ? (((n * a.XH + iy) * a.XW + ix) * a.B + b0 + cc) * (int)sizeof(T) : -1);
+        }
+        if (a.gscale) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gsc[j] = a.gscale[n * a.A + (a_ok ? a0 + cc + j : 0)];
+        }
+        if (a.xscale) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xsc[j] = a.xscale[n * a.B + (b_ok ? b0 + cc + j : 0)];
+        }
+    };
+    auto scale8 = [](vec8 v, const float* sc) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (T)((float)v[j] * sc[j]);
+        return v;
+    };
+    auto sstore = [&](T* gs, T* xs) {
+#pragma unroll
+        for (int i = 0; i < GCH; ++i)
+            *(vec8*)(gs + Lay<false>::off((tid >> 3) + i * 32, cc)) = a.gscale ? scale8(rg[i], gsc) : rg[i];
+#pragma unroll
+        for (int i = 0; i < XCH; ++i) {
+            const int hp = (tid >> 3) + i * 32;
+            const int hy = hp / XW, hx = hp - hy * XW;
+            const int row = hy * XW + ((hx & 1) ? XEV + (hx >> 1) : (hx >> 1));   // deinterleaved
+            if (hp < HP) *(vec8*)(xs + Lay<false>::off(row, cc)) = a.xscale ? scale8(rx[i], xsc) : rx[i];
+        }
+    };
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
+
+    auto rowk = [&](int k0) { return k0 + 8 * ((lane >> 4) >> 1); };
+    auto xrow = [&](int k0, int ky, int kx) {
+        const int pr = rowk(k0), py = pr / TW, px = pr % TW;
+        return (2 * py + ky) * XW + ((kx & 1) ? XEV : 0) + px + (kx >> 1);
+    };
+    if (t_begin < t_end) {
+        gload(t_begin);
+        sstore(st0, st0 + NP * LD);
+        if (t_begin + 1 < t_end) gload(t_begin + 1);
+        __syncthreads();
+        int k = 0;
+        for (int t = t_begin; t < t_end; ++t, ++k) {
+            T* const gs = st0 + (k & 1) * STAGE;
+            T* const xs = gs + NP * LD;
+            T* const gn = st0 + ((k + 1) & 1) * STAGE;
+            v8w<T> fa = frag32<T, false>(gs, rowk(0), wa * 32, lane), fb[9];
+#pragma unroll
+            for (int tp = 0; tp < 9; ++tp) fb[tp] = frag32<T, false>(xs, xrow(0, tp / 3, tp % 3), wb * 32, lane);
+#pragma unroll
+            for (int k0 = 0; k0 < NP; k0 += 16) {
+                const int kn = k0 + 16 < NP ? k0 + 16 : k0;
+                const v8w<T> fan = frag32<T, false>(gs, rowk(kn), wa * 32, lane);
+#pragma unroll
+                for (int tp = 0; tp < 9; ++tp) {
+                    acc[tp] = mma32<T>(fa, fb[tp], acc[tp]);
+                    fb[tp] = frag32<T, false>(xs, xrow(kn, tp / 3, tp % 3), wb * 32, lane);
+                }
+                fa = fan;
+                if (k0 == 32 && t + 1 < t_end) {       // mid-tile: stage tile t + 1, then fetch tile t + 2
+                    sstore(gn, gn + NP * LD);
+                    if (t + 2 < t_end) gload(t + 2);
+                }
+            }
+            __syncthreads();
+        }
+    }
+
+    const int b = b0 + wb * 32 + (lane & 31);
+    if (b < a.B) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int ar = a0 + wa * 32 + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+            if (ar >= a.A) continue;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) w3_add(a, ((int64_t)ar * 9 + t) * a.B + b, acc[t][j] * a.alpha);
+        }
+    }
+}
+constexpr size_t W3P_LDS = 2 * (size_t)((16 * 6) + 33 * 13) * LDP * 2;    // 151,200 B (16-bit elements)
+
+template <typename T>
+void launch_w3p(const W3Args& a, dim3 grid, hipStream_t s) {
+    auto kern = wgrad3x3_s2p_kernel<T>;
+    static bool attr_set = false;   // benign race: idempotent attribute
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)W3P_LDS);
+        attr_set = true;
+    }
+    kern<<<grid, 256, W3P_LDS, s>>>(a);
+}
+
 template <typename T, int TW, int NT>
 void launch_w3(const W3Args& a, dim3 grid, hipStream_t s) {
     static const bool swz = [] { const char* e = getenv("SG2_WGRAD_SWZ"); return e != nullptr && e[0] == '1'; }();
@@ -616,9 +762,13 @@ int wgrad3x3_run(W3Args& a, DetArena& arena, float* dw, const void* g, const voi
     a.N = N; a.GH = OH; a.GW = OW; a.XH = H; a.XW = W; a.A = A; a.B = B; a.KK = KH * KW; a.S = stride;
     static const bool s2_on = [] { const char* e = getenv("SG2_WGRAD_S2"); return !e || atoi(e) != 0; }();
     if (s2_on && stride == 2 && KH == 3 && KW == 3 && pad_y == 0 && pad_x == 0) {
-        // all nine taps in one launch (wgrad3x3_s2_kernel), 16 x 8 g tiles
+        // all nine taps in one launch: the pipelined 16 x 6 form for g grids of 64^2 and up, where it measured
+        // 1-14 % faster, the 16 x 8 wgrad3x3_s2_kernel below them, where the pipelined form was 6-7 % slower
+        // (tools/wgrad_s2p_ab.py, profiles/r05_wgrad_s2p_ab.txt); SG2_WGRAD_S2P=1 / 0 forces either
+        const char* ep = getenv("SG2_WGRAD_S2P");     // read per call: tests switch it in one process
+        const bool pipe = ep ? atoi(ep) != 0 : (OH >= 64 && OW >= 64);
         a.tiles_x = (int)cdiv(OW, 16);
-        a.tiles_y = (int)cdiv(OH, 8);
+        a.tiles_y = (int)cdiv(OH, pipe ? 6 : 8);
         a.tiles = N * a.tiles_x * a.tiles_y;
         const int cb = (int)(cdiv(A, BC) * cdiv(B, BC));
         int splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(wgrad_wgs(), cb), a.tiles / 4));
@@ -627,7 +777,10 @@ int wgrad3x3_run(W3Args& a, DetArena& arena, float* dw, const void* g, const voi
         dim3 grid((unsigned)cdiv(A, BC), (unsigned)cdiv(B, BC), (unsigned)splits);
         if (int rc = w3_det_slots(a, arena, (int)grid.z, s)) return rc;
         static const bool swz = [] { const char* e = getenv("SG2_WGRAD_SWZ"); return e != nullptr && e[0] == '1'; }();
-        if (dtype == SG2_F16) {
+        if (pipe) {
+            if (dtype == SG2_F16) launch_w3p<f16_t>(a, grid, s);
+            else launch_w3p<bf16_t>(a, grid, s);
+        } else if (dtype == SG2_F16) {
             if (swz) wgrad3x3_s2_kernel<f16_t, true><<<grid, 256, 0, s>>>(a);
             else wgrad3x3_s2_kernel<f16_t, false><<<grid, 256, 0, s>>>(a);
         } else {

@@ -858,13 +858,30 @@ def test_conv_fused_dot_and_scale(dtype, geom):
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize('case', ['conv_s2', 'convT_s2', 'conv_1x1', 'conv_s2_big'])
-def test_wgrad_halo_phases(dtype, case):
-    """Halo weight gradients: stride-2 conv (D down layers; all nine taps in one launch of
-    wgrad3x3_s2_kernel), the transposed stride-2 conv of the up layers (with the modulation on the g
-    operand) and 1x1 (phase kernel), vs autograd in f64; ragged 16 x 8 tiles, partial 64-channel blocks."""
+@pytest.mark.parametrize('case', ['conv_s2', 'convT_s2', 'conv_1x1', 'conv_s2_big', 'conv_s2_wide'])
+@pytest.mark.parametrize('s2p', ['1', '0'])
+def test_wgrad_halo_phases(dtype, case, s2p, monkeypatch):
+    """Halo weight gradients: stride-2 conv (D down layers; all nine taps in one launch: the pipelined 16 x 6
+    form wgrad3x3_s2p_kernel, s2p '0' the 16 x 8 wgrad3x3_s2_kernel), the transposed stride-2 conv of the up
+    layers (with the modulation on the g operand) and 1x1 (phase kernel), vs autograd in f64; ragged tiles,
+    partial 64-channel blocks, several tiles per workgroup (conv_s2_wide), in float-atomic and deterministic mode."""
+    import sg2hip
     from torch_utils.ops import conv2d_gradfix as cg
+    monkeypatch.setenv('SG2_WGRAD_S2P', s2p)
     torch.manual_seed(31)
+    if case == 'conv_s2_wide':
+        N, Ci, Co = 6, 64, 128
+        x = torch.randn(N, Ci, 129, 97, device=DEV)
+        w = torch.randn(Co, Ci, 3, 3, device=DEV, dtype=torch.float64, requires_grad=True)
+        y = F.conv2d(x.to(dtype).double(), w, stride=2)
+        g = torch.randn_like(y)
+        ref, = torch.autograd.grad((y * g.to(dtype).double()).sum(), [w])
+        for det in (False, True):
+            with sg2hip.deterministic(det, device=DEV):
+                dw = cg._wgrad_raw(g.to(dtype).contiguous(memory_format=torch.channels_last),
+                                   x.to(dtype).contiguous(memory_format=torch.channels_last), 3, 3, 2, (0, 0))
+            assert rel_err(dw, ref) < (2e-3 if dtype == torch.float16 else 1e-2)
+        return
     N, Ci, Co = 2, 64, 72
     if case == 'conv_s2_big':
         N, Ci, Co = 3, 136, 64
