@@ -26,7 +26,10 @@ def cat(n):
                       ('layer_bwd', 'layer_bwd'), ('bias_act', 'bias_act'), ('demod', 'demod'), ('Cijk', 'GEMM'),
                       ('conv_finalize', 'conv finalize'), ('rocclr', 'memset/copy'), ('zero_fill', 'memset/copy'), ('multi_tensor', 'optimizer'),
                       ('adam_multi', 'optimizer'), ('lerp_multi', 'optimizer'),
-                      ('pack_weight', 'weight pack'), ('infnorm', 'fp16 pre-normalisation')]:
+                      ('pack_weight', 'weight pack'), ('infnorm', 'fp16 pre-normalisation'),
+                      ('conv1x1_small', '1x1 conv toRGB / fromRGB'), ('wgrad1x1_small', '1x1 conv toRGB / fromRGB'),
+                      ('vjp_axpy', 'fused VJP pass'), ('split3', 'f32 operand split'), ('moments', 'statistics'),
+                      ('grouped', 'GEMM')]:
         if key in n:
             return name
     if 'upfirdn' in n:
