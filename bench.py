@@ -289,21 +289,22 @@ def _time_ms(fn, reps=20):
     return e0.elapsed_time(e1) / reps
 
 
-def _roof_entry(kernel, shape, ms, flops, byts):
+def _roof_entry(kernel, shape, ms, flops, byts, mfma_peak=None):
     """One family's roofline: the binding roof of the launch is min(MFMA peak, AI x HBM peak); frac = achieved rate
-    / that roof, in the roof's unit."""
+    / that roof, in the roof's unit.  mfma_peak: the compute roof in TFLOP/s when it is not the dense 16-bit one."""
+    mfma_peak = mfma_peak or MFMA_PEAK_FP16
     ai = flops / byts if byts else float('inf')
     tfl = flops / (ms * 1e-3) / 1e12
     gbps = byts / (ms * 1e-3) / 1e9
-    hbm_bound = ai * HBM_PEAK * 1e9 < MFMA_PEAK_FP16 * 1e12
+    hbm_bound = ai * HBM_PEAK * 1e9 < mfma_peak * 1e12
     e = {'kernel': kernel, 'shape': shape, 'ms_per_launch': round(ms, 4), 'algorithmic_flops_per_launch': flops,
          'algorithmic_hbm_bytes_per_launch': byts, 'arithmetic_intensity': round(ai, 1)}
     if hbm_bound:
         e.update({'bound': 'hbm', 'achieved': round(gbps, 1), 'peak': HBM_PEAK, 'unit': 'GB/s',
                   'frac': round(gbps / HBM_PEAK, 4)})
     else:
-        e.update({'bound': 'mfma', 'achieved': round(tfl, 1), 'peak': MFMA_PEAK_FP16, 'unit': 'TFLOP/s',
-                  'frac': round(tfl / MFMA_PEAK_FP16, 4)})
+        e.update({'bound': 'mfma', 'achieved': round(tfl, 1), 'peak': round(mfma_peak, 1), 'unit': 'TFLOP/s',
+                  'frac': round(tfl / mfma_peak, 4)})
     if flops:
         e['mfma_tflops'] = round(tfl, 1)
     return e
@@ -335,17 +336,33 @@ def roofline_families(device, dtype=torch.float16):
                                     f'D down-2 3x3 N{N} {Ci}x{H}^2 -> {Co}x{OH}^2, bias + lrelu', ms,
                                     2.0 * N * Co * Ci * 9 * OH * OH, (N * Ci * H * H + N * Co * OH * OH) * esz)
     del x
-    # generic implicit GEMM (conv_fwd_kernel): its largest remaining launch, the 32^2 -> 65^2 up-2 transposed conv of
-    # the 64^2 synthesis block (G forward, modulated; the up-2 kernel serves 64^2 inputs and up)
+    # up-2 transposed conv (conv3x3_up2_kernel, edge split) on the 32^2 -> 65^2 layer of the 64^2 synthesis block
+    # (G forward, modulated): the generic implicit GEMM's largest 16-bit launch until the edge split moved it
     N, Ci, H, Co = 32, 512, 32, 256
     x = rnd(N, Ci, H, H)
     wp = cg._pack_conv((torch.randn(Co, Ci, 3, 3, device=device) / 68).to(dtype))
     s_ = torch.rand(N, Ci, device=device) + 0.5
     OT = 2 * H + 1
+    assert cg._up2_ok(x, Co, OT, OT, 3, 3, 2, (0, 0), True)
     ms = _time_ms(lambda: cg.conv_fused(x, wp, Co, OT, OT, 3, 3, 2, (0, 0), transpose=True, in_scale=s_))
-    out['conv_fwd_generic'] = _roof_entry('conv_fwd_kernel (implicit GEMM)',
-                                          f'up-2 transposed 3x3 N{N} {Ci}x{H}^2 -> {Co}x{OT}^2 (modulated)', ms,
-                                          2.0 * N * Co * Ci * 9 * H * H, (N * Ci * H * H + N * Co * OT * OT) * esz)
+    out['up2_conv'] = _roof_entry('conv3x3_up2_kernel (cell tiles + edge strips)',
+                                  f'up-2 transposed 3x3 N{N} {Ci}x{H}^2 -> {Co}x{OT}^2 (modulated)', ms,
+                                  2.0 * N * Co * Ci * 9 * H * H, (N * Ci * H * H + N * Co * OT * OT) * esz)
+    del x
+    # generic implicit GEMM in f32 (conv_fwd_kernel, three-way bf16 split): its largest launch, the 16^2 C = 512
+    # synthesis layer (bs32, modulated, bias + lrelu).  The split issues six bf16 products per f32 product, so its
+    # compute roof is the dense 16-bit MFMA peak / 6 (the exact-f32 MFMA, v_mfma_f32_16x16x4_f32, peaks at 157.3)
+    N, C, R = 32, 512, 16
+    x = torch.randn(N, C, R, R, device=device).contiguous(memory_format=cl)
+    wp = cg._pack_conv(torch.randn(C, C, 3, 3, device=device) / 68)
+    s_ = torch.rand(N, C, device=device) + 0.5
+    b = torch.zeros(C, device=device)
+    ms = _time_ms(lambda: cg.conv_fused(x, wp, C, R, R, 3, 3, 1, (1, 1), in_scale=s_, out_scale=s_, bias=b, act=1,
+                                        gain=1.41, clamp=256.0))
+    out['conv_f32_split'] = _roof_entry('conv_fwd_kernel<float> (implicit GEMM, 3-way bf16 split)',
+                                        f'3x3 s1 N{N} C{C} {R}^2 f32 (modulated, bias + lrelu)', ms,
+                                        2.0 * N * C * C * 9 * R * R, 2 * N * C * R * R * 4,
+                                        mfma_peak=MFMA_PEAK_FP16 / 6)
     del x
     # halo conv: the 128^2 C=128 synthesis layer (G forward, bs32)
     N, C, R = 32, 128, 128

@@ -54,6 +54,7 @@ struct Conv3Args {
     int raw_act;            // y_raw receives the activated value before the residual add (the activation
                             // gradient's input) instead of the raw conv output
     float* det_dot;         // deterministic mode: [N, OH, OW, Cout] per-element dot products (det_sum adds them)
+    int edge_rx, edge_cy;   // up-2 edge split: per image, tiles of the last cell row / column (0: no split)
 };
 
 // Output channel of MFMA row P of a 64-channel tile (see the C = 64 kernels below)
@@ -2051,19 +2052,32 @@ constexpr int U_OS = BN + 8;                                           // epilog
 constexpr size_t U_LDS = (size_t)U_HB + U_WB;                          // 46,848 B
 static_assert((size_t)U_CELLS * U_OS * 2 <= U_LDS, "epilogue tile fits the staging buffer");
 
-template <typename T, bool SCALE_IN>
-__global__ __launch_bounds__(256, 2) void conv3x3_up2_kernel(Conv3Args a) {
-    constexpr int NH = (U_HP * 4 + 255) / 256;                // halo 16-B loads per thread (3)
-    constexpr int NW = (9 * BN * 4) / 256;                    // weight 16-B loads per thread (9)
+// Edge split (EDGE > 0): with H % 8 == W % 16 == 0 the 16 x 8 tiles cover cells 0 .. H-1 x 0 .. W-1 exactly and
+// the last cell row (i = H: output row 2H only, from input row H-1 through the ky = 2 taps) and column (j = W:
+// output column 2W, the kx = 2 taps) run as 128 x 1 (EDGE 1) and 1 x 128 (EDGE 2) strips of three taps each.  At
+// 32^2 inputs the ragged 16 x 8 tiling of 33 x 33 cells ran 15 tiles of nine taps per image; split it is 8 + 2/3.
+template <int EDGE> struct UpGeom {
+    static constexpr int TW = EDGE == 0 ? U_TW : (EDGE == 1 ? 128 : 1);       // cells per tile row
+    static constexpr int HR = EDGE == 1 ? 1 : (EDGE == 0 ? U_TH : 128) + 1;    // staged halo rows
+    static constexpr int HC = EDGE == 2 ? 1 : TW + 1;                          // staged halo columns
+    static constexpr int HP = HR * HC;
+    static constexpr int NT = EDGE == 0 ? 9 : 3;                               // taps
+    __device__ static constexpr int tap(int t) { return EDGE == 0 ? t : (EDGE == 1 ? 6 + t : 2 + 3 * t); }
+};
+static_assert(((UpGeom<1>::HP * 64 + 255) / 256) * 256 + 3 * BN * 64 <= U_LDS &&
+              ((UpGeom<2>::HP * 64 + 255) / 256) * 256 + 3 * BN * 64 <= U_LDS, "edge strips fit the staging buffer");
+
+template <typename T, bool SCALE_IN, int EDGE>
+__device__ __forceinline__ void up2_tile(const Conv3Args& a, int n, int i0, int j0, char* smem_raw) {
+    using G = UpGeom<EDGE>;
+    constexpr int NH = (G::HP * 4 + 255) / 256;               // halo 16-B loads per thread
+    constexpr int NW = (G::NT * BN * 4) / 256;                // weight 16-B loads per thread
+    constexpr int HB = ((G::HP * 64 + 255) / 256) * 256;
     typedef T vec8 __attribute__((ext_vector_type(8)));
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    char* hl = smem_raw;                                      // [153 rows] x 64 B
-    char* wl = smem_raw + U_HB;                               // [9 taps][64 rows] x 64 B
+    char* hl = smem_raw;                                      // [HP rows] x 64 B
+    char* wl = smem_raw + HB;                                 // [NT taps][64 rows] x 64 B
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int per_n = a.tiles_x * a.tiles_y;
-    const int n = blockIdx.x / per_n, tr = blockIdx.x - n * per_n;
-    const int i0 = (tr / a.tiles_x) * U_TH, j0 = (tr % a.tiles_x) * U_TW;   // first cell of the tile
     const int o0 = blockIdx.y * BN;
     const int OH = 2 * a.H + 1, OW = 2 * a.W + 1;
     const int nchunks = a.Cin / CK;
@@ -2078,14 +2092,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_up2_kernel(Conv3Args a) {
 #pragma unroll
         for (int k = 0; k < NH; ++k) {
             const int p = (tid + k * 256) >> 2;
-            const int iy = i0 - 1 + p / U_HW, ix = j0 - 1 + p % U_HW;
-            const bool ok = (p < U_HP) & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W);
+            const int iy = i0 - 1 + p / G::HC, ix = j0 - 1 + p % G::HC;
+            const bool ok = (p < G::HP) & ((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W);
             rh[k] = buf_load16<vec8>(rxb, ok ? (((n * a.H + iy) * a.W + ix) * a.Cin + c) * (int)sizeof(T) : -1);
         }
 #pragma unroll
         for (int k = 0; k < NW; ++k) {
-            const int r = (tid + k * 256) >> 2, tap = r / BN, o = r - tap * BN;
-            rw[k] = buf_load16<vec8>(rwb, o0 + o < a.Cout ? (((o0 + o) * 9 + tap) * a.Cin + c) * (int)sizeof(T) : -1);
+            const int r = (tid + k * 256) >> 2, t = r / BN, o = r - t * BN;
+            rw[k] = buf_load16<vec8>(rwb, o0 + o < a.Cout ? (((o0 + o) * 9 + G::tap(t)) * a.Cin + c) * (int)sizeof(T)
+                                                          : -1);
         }
         if (SCALE_IN) {
             const float* sc = a.in_scale + (int64_t)n * a.Cin + c;
@@ -2098,7 +2113,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_up2_kernel(Conv3Args a) {
 #pragma unroll
         for (int k = 0; k < NH; ++k) {
             const int p = (tid + k * 256) >> 2;
-            if (k * 256 + 256 > U_HP * 4 && p >= U_HP) continue;   // the ragged last round only
+            if (k * 256 + 256 > G::HP * 4 && p >= G::HP) continue;   // the ragged last round only
             vec8 v = rh[k];
             if (SCALE_IN) {   // x * s.to(x.dtype) (networks_stylegan2.py:69): s rounded first, one rounding after
 #pragma unroll
@@ -2112,7 +2127,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_up2_kernel(Conv3Args a) {
 
     const int lq = lane >> 4, l16 = lane & 15;
     const int b_lane = swz64(l16, lq);                        // + (tap * 64 + j * 16) * 64: the same swizzle
-    f32x4 acc[4][2][4];                                       // [phase (ky & 1) * 2 + (kx & 1)][cell row][co tile]
+    f32x4 acc[4][2][4];                                       // [phase (ky & 1) * 2 + (kx & 1)][cell group][co tile]
 #pragma unroll
     for (int f = 0; f < 4; ++f)
 #pragma unroll
@@ -2127,24 +2142,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_up2_kernel(Conv3Args a) {
         const bool more = ch + 1 < nchunks;
         if (more) gload(ch + 1);
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
+        for (int t = 0; t < G::NT; ++t) {
+            const int tap = G::tap(t), ky = tap / 3, kx = tap % 3, ph = (ky & 1) * 2 + (kx & 1);
+            v8<T> af[2], bfr[4];
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-                const int tap = ky * 3 + kx, ph = (ky & 1) * 2 + (kx & 1);
-                v8<T> af[2], bfr[4];
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    // cell row 2w + i reads input row (cell row + 1 - ky / 2) of the halo
-                    const int pos = (2 * wave + i + 1 - (ky >> 1)) * U_HW + l16 + 1 - (kx >> 1);
-                    af[i] = *(const v8<T>*)(hl + swz64(pos, lq));
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) bfr[j] = *(const v8<T>*)(wl + b_lane + (tap * BN + j * 16) * 64);
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[ph][i][j] = mma<T>(af[i], bfr[j], acc[ph][i][j]);
+            for (int i = 0; i < 2; ++i) {
+                // cell m = 16 (2 wave + i) + l16 of the tile reads halo row (cell row + 1 - ky / 2), column
+                // (cell column + 1 - kx / 2); the edge strips stage only the row / column their taps read
+                const int m = (2 * wave + i) * 16 + l16, cy = m / G::TW, cx = m % G::TW;
+                const int hy = EDGE == 1 ? 0 : cy + 1 - (ky >> 1), hx = EDGE == 2 ? 0 : cx + 1 - (kx >> 1);
+                af[i] = *(const v8<T>*)(hl + swz64(hy * G::HC + hx, lq));
             }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[j] = *(const v8<T>*)(wl + b_lane + (t * BN + j * 16) * 64);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[ph][i][j] = mma<T>(af[i], bfr[j], acc[ph][i][j]);
         }
         if (more) {
             __syncthreads();                                  // everyone done reading before the overwrite
@@ -2160,11 +2174,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_up2_kernel(Conv3Args a) {
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
         const int py = ph >> 1, px = ph & 1;
+        if ((EDGE == 1 && py) || (EDGE == 2 && px)) continue;  // output row 2H + 1 / column 2W + 1: none
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int m = (2 * wave + i) * U_TW + 4 * lq + r;     // cell of accumulator row 4 lq + r
+                const int m = (2 * wave + i) * 16 + 4 * lq + r;       // cell of accumulator row 4 lq + r
 #pragma unroll
                 for (int j = 0; j < 4; ++j) ot[m * U_OS + j * 16 + l16] = (T)acc[ph][i][j][r];
             }
@@ -2172,12 +2187,34 @@ __global__ __launch_bounds__(256, 2) void conv3x3_up2_kernel(Conv3Args a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {                         // 128 cells x 8 channel vectors / 256 threads
             const int m = (tid >> 3) + k * 32;
-            const int oy = 2 * (i0 + m / U_TW) + py, ox = 2 * (j0 + m % U_TW) + px;
-            if (oy < OH && ox < OW && o0 + c8 < a.Cout)
+            const int oy = 2 * (i0 + m / G::TW) + py, ox = 2 * (j0 + m % G::TW) + px;
+            // (the column strip leaves the corner cell (H, W) to the row strip)
+            if (oy < (EDGE == 2 ? 2 * a.H : OH) && ox < OW && o0 + c8 < a.Cout)
                 *(vec8*)(y + (((int64_t)n * OH + oy) * OW + ox) * a.Cout + o0 + c8) = *(const vec8*)(ot + m * U_OS + c8);
         }
         __syncthreads();
     }
+}
+
+template <typename T, bool SCALE_IN>
+__global__ __launch_bounds__(256, 2) void conv3x3_up2_kernel(Conv3Args a) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int per_n = a.tiles_x * a.tiles_y;
+    int b = blockIdx.x;
+    if (b < a.N * per_n) {
+        const int n = b / per_n, tr = b - n * per_n;
+        up2_tile<T, SCALE_IN, 0>(a, n, (tr / a.tiles_x) * U_TH, (tr % a.tiles_x) * U_TW, smem_raw);
+        return;
+    }
+    b -= a.N * per_n;
+    if (b < a.N * a.edge_rx) {                                // cells (H, 128 t ..)
+        const int n = b / a.edge_rx;
+        up2_tile<T, SCALE_IN, 1>(a, n, a.H, (b - n * a.edge_rx) * 128, smem_raw);
+        return;
+    }
+    b -= a.N * a.edge_rx;
+    const int n = b / a.edge_cy;                              // cells (128 t .., W)
+    up2_tile<T, SCALE_IN, 2>(a, n, (b - n * a.edge_cy) * 128, a.W, smem_raw);
 }
 
 template <typename T, bool SI>
@@ -2188,9 +2225,13 @@ int launch_up2(Conv3Args& a, hipStream_t s) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)U_LDS);
         attr_set = true;
     }
-    a.tiles_x = (a.W + 1 + U_TW - 1) / U_TW;
-    a.tiles_y = (a.H + 1 + U_TH - 1) / U_TH;
-    dim3 grid(a.N * a.tiles_x * a.tiles_y, (a.Cout + BN - 1) / BN);
+    const char* e = getenv("SG2_UP2_EDGE");          // read per launch: tests switch it in one process
+    const bool split = !(e && e[0] == '0') && a.H % U_TH == 0 && a.W % U_TW == 0;
+    a.tiles_x = split ? a.W / U_TW : (a.W + 1 + U_TW - 1) / U_TW;
+    a.tiles_y = split ? a.H / U_TH : (a.H + 1 + U_TH - 1) / U_TH;
+    a.edge_rx = split ? (a.W + 1 + 127) / 128 : 0;
+    a.edge_cy = split ? (a.H + 127) / 128 : 0;
+    dim3 grid(a.N * (a.tiles_x * a.tiles_y + a.edge_rx + a.edge_cy), (a.Cout + BN - 1) / BN);
     kern<<<grid, 256, U_LDS, s>>>(a);
     return launch_status("sg2_conv3x3_up2");
 }

@@ -133,15 +133,24 @@ def _split_k(x, clean):
         raise
 
 
+up2_min = int(os.environ.get('SG2_UP2_MIN', '16'))   # smallest input edge the up-2 kernel takes (edge split on)
+
+
 def _up2_ok(x, cout, oh, ow, kh, kw, stride, pad, transpose):
-    """sg2_conv3x3_up2 serves the 16-bit stride-2 transposed 3x3 convs with padding 0 (output 2H+1) from 64^2
-    inputs up; below, its 16 x 8 cell tiles are mostly empty (17 x 17 cells at 16^2) and the four-phase
-    implicit GEMM is faster (tools/up2_ab.py: 128^2 -> 257^2 C 128 -> 64: 0.168 vs 0.264 ms; 64^2 C 256 -> 128:
-    0.152 vs 0.181 ms; 32^2 C 512 -> 256: 0.163 vs 0.143 ms)."""
+    """sg2_conv3x3_up2 serves the 16-bit stride-2 transposed 3x3 convs with padding 0 (output 2H+1).  Its 16 x 8
+    cell tiles cover the (H+1) x (W+1) cells raggedly (15 tiles for 33 x 33 cells at 32^2); with H % 8 == W % 16
+    == 0 the kernel splits off the last cell row and column as three-tap strips (8 + 2/3 tile-equivalents at 32^2),
+    which is what lets it take the 16^2 and 32^2 inputs from the four-phase implicit GEMM (tools/up2_ab.py).
+    Unsplit (ragged) shapes take it from 64^2 up: 128^2 -> 257^2 C 128 -> 64: 0.168 vs 0.264 ms; 64^2 C 256 -> 128:
+    0.152 vs 0.181 ms; 32^2 C 512 -> 256: 0.163 vs 0.143 ms ragged."""
     n, cin, h, w = x.shape
-    return (transpose and stride == 2 and kh == 3 and kw == 3 and tuple(pad) == (0, 0) and oh == 2 * h + 1 and
-            ow == 2 * w + 1 and x.dtype in (torch.float16, torch.bfloat16) and cin % 32 == 0 and cout % 8 == 0 and
-            h >= 64 and w >= 64)
+    if not (transpose and stride == 2 and kh == 3 and kw == 3 and tuple(pad) == (0, 0) and oh == 2 * h + 1 and
+            ow == 2 * w + 1 and x.dtype in (torch.float16, torch.bfloat16) and cin % 32 == 0 and cout % 8 == 0):
+        return False
+    if h >= 64 and w >= 64:
+        return True
+    split = h % 8 == 0 and w % 16 == 0 and os.environ.get('SG2_UP2_EDGE', '1') != '0'
+    return split and h >= up2_min and w >= up2_min
 
 
 def _conv_up2(x, wp, cout, in_scale=None):

@@ -1145,12 +1145,15 @@ def test_pack_scale_and_wgrad_alpha(dtype):
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize('shape', [(2, 128, 65, 70, 64), (2, 64, 64, 64, 128), (1, 512, 64, 64, 512), (1, 32, 64, 96, 8)])
+@pytest.mark.parametrize('shape', [(2, 128, 65, 70, 64), (2, 64, 64, 64, 128), (1, 512, 64, 64, 512), (1, 32, 64, 96, 8),
+                                   (2, 64, 16, 16, 128), (2, 512, 32, 32, 256), (1, 64, 136, 272, 64),
+                                   (1, 32, 16, 48, 64)])
 @pytest.mark.parametrize('mod', [False, True])
-def test_conv3x3_up2(dtype, shape, mod):
+def test_conv3x3_up2(dtype, shape, mod, monkeypatch):
     """sg2_conv3x3_up2 (the stride-2 transposed 3x3 conv of the up-2 layers, output 2H+1, with the
     modulation x * s.to(x.dtype) in its staging) vs F.conv_transpose2d in float64 on the same rounded
-    operands; ragged tiles (H, W not multiples of the 8 x 16 cell tile), Cout below one 64-channel block."""
+    operands; ragged tiles (H, W not multiples of the 8 x 16 cell tile), Cout below one 64-channel block; the
+    edge split (16^2 and 32^2 inputs, several row / column strips at 136 x 272) bitwise against the ragged tiling."""
     from torch_utils.ops import conv2d_gradfix as cg
     N, Cin, H, W, Cout = shape
     torch.manual_seed(31)
@@ -1164,6 +1167,10 @@ def test_conv3x3_up2(dtype, shape, mod):
     assert y.shape == ref.shape
     tol = 5e-3 if dtype == torch.float16 else 2e-2
     assert rel_err(y.float(), ref) < tol
+    if H % 8 == 0 and W % 16 == 0:   # the edge split (last cell row / column as three-tap strips): the same sums
+        monkeypatch.setenv('SG2_UP2_EDGE', '0')
+        ys = cg._conv_up2(x, cg._pack_conv(w), Cout, in_scale=s)
+        assert torch.equal(y, ys)
 
 
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])

@@ -35,12 +35,19 @@ def generic(x, wp, cout):
 
 
 for (n, cin, h, cout) in [(32, 128, 128, 64), (32, 256, 64, 128), (32, 512, 32, 256), (32, 512, 16, 512),
+                          (64, 256, 64, 128), (64, 512, 32, 256), (64, 512, 16, 512), (64, 512, 8, 512),
                           (16, 256, 128, 128), (8, 512, 64, 256)]:
     x = torch.randn(n, cin, h, h, device=dev).half().contiguous(memory_format=torch.channels_last)
     wp = cg._pack_conv((torch.randn(cout, cin, 3, 3, device=dev) / np.sqrt(cin * 9)).half())
     flops = 2.0 * n * h * h * cin * cout * 9
     a = timeit(lambda: cg._conv_up2(x, wp, cout))
+    ys = cg._conv_up2(x, wp, cout)
+    os.environ['SG2_UP2_EDGE'] = '0'              # the ragged 16 x 8 tiling of all (H+1) x (W+1) cells
+    r = timeit(lambda: cg._conv_up2(x, wp, cout))
+    same = torch.equal(ys, cg._conv_up2(x, wp, cout))
+    os.environ['SG2_UP2_EDGE'] = '1'
     b = timeit(lambda: generic(x, wp, cout))
-    err = (cg._conv_up2(x, wp, cout).float() - generic(x, wp, cout).float()).norm() / generic(x, wp, cout).float().norm()
-    print(f'N={n} Cin={cin} {h}^2 -> {2 * h + 1}^2 Cout={cout}: up2 {a:.3f} ms ({flops / a / 1e9:.0f} TF) | generic '
-          f'{b:.3f} ms ({flops / b / 1e9:.0f} TF) | rel diff {err:.1e}', flush=True)
+    err = (ys.float() - generic(x, wp, cout).float()).norm() / generic(x, wp, cout).float().norm()
+    print(f'N={n} Cin={cin} {h}^2 -> {2 * h + 1}^2 Cout={cout}: up2 {a:.3f} ms ({flops / a / 1e9:.0f} TF) | ragged '
+          f'{r:.3f} ms (split == ragged: {same}) | generic {b:.3f} ms ({flops / b / 1e9:.0f} TF) | rel diff {err:.1e}',
+          flush=True)
