@@ -435,3 +435,32 @@ def test_snapshot_from_reference(tmp_path):
         assert not data[key].training
         assert dict(data[key].init_kwargs) == ast.literal_eval(str(ref[f'{key}/init_kwargs'])), key
     assert float(data['augment_pipe'].p) == 0.375 and n_checked > 100
+
+
+def test_metric_registry(tmp_path, capsys):
+    """metric_main_mi_multimodal (SG3/metrics/metric_main_mi_multimodal.py:27-95): registration, calc_metric's result
+    record, report_metric's JSON line in <run_dir>/metric-<modality>-<metric>.jsonl with the snapshot path relative
+    to the run directory, and unknown names refused."""
+    import json
+    import os
+    import torch
+    from metrics import metric_main_mi_multimodal as metric_main
+
+    assert {'fid50k_full', 'fid50k'} <= set(metric_main.list_valid_metrics())
+
+    @metric_main.register_metric
+    def unit_metric(opts):
+        assert opts.num_gpus == 1 and opts.dataset_kwargs.path == 'x.zip'
+        return {'unit_metric': 1.5}
+
+    assert metric_main.is_valid_metric('unit_metric') and not metric_main.is_valid_metric('nope')
+    res = metric_main.calc_metric(metric='unit_metric', dataset_kwargs={'path': 'x.zip'}, device=torch.device('cpu'))
+    assert res.results.unit_metric == 1.5 and res.metric == 'unit_metric' and res.num_gpus == 1
+    assert isinstance(res.total_time_str, str)
+    metric_main.report_metric(res, mode='CT', run_dir=str(tmp_path), snapshot_pkl=str(tmp_path / 'network-snapshot-000001.pkl'))
+    line = json.loads(open(os.path.join(tmp_path, 'metric-CT-unit_metric.jsonl')).read().strip())
+    assert line['results'] == {'unit_metric': 1.5} and line['mode'] == 'CT'
+    assert line['snapshot_pkl'] == 'network-snapshot-000001.pkl' and 'timestamp' in line
+    assert json.loads(capsys.readouterr().out.strip().splitlines()[-1]) == line
+    with pytest.raises(AssertionError):
+        metric_main.calc_metric(metric='nope')
