@@ -65,6 +65,9 @@ def parse():
                          'several GPUs (auto: on, after a capture probe of an RCCL all_reduce agrees on every rank; '
                          'otherwise the eager path, whose bucketed all_reduces overlap the backward from hooks)')
     ap.add_argument('--no-graphs', action='store_true', help='same as --graphs off')
+    ap.add_argument('--deterministic', default='on', choices=['on', 'off'],
+                    help='the training iteration\'s reductions: the library\'s fixed-order slots (on, the default: '
+                         'Trainer(deterministic=True)) or float atomics (off, an A/B mode)')
     return ap.parse_args()
 
 
@@ -136,7 +139,7 @@ def build(args, device, rank, num_gpus):
     tr = trainer_mod.Trainer(G, D, G_ema, loss, opt, dnnlib.EasyDict(opt), G_reg_interval=4, D_reg_interval=16,
                              batch_size=B, batch_gpu=args.batch_gpu, num_gpus=num_gpus, rank=rank, device=device,
                              ema_kimg=B * 10 / 32, augment_pipe=aug, ada_target=None,
-                             phase_timing=args.phase_timing)
+                             phase_timing=args.phase_timing, deterministic=args.deterministic == 'on')
     return tr
 
 
@@ -535,7 +538,7 @@ def main():
             'metric': f'imgs/sec at {args.res}^2 bs{args.batch_gpu}/GPU StyleGAN2-ADA training (+ sec/kimg)',
             'value': round(value, 3), 'unit': 'imgs/s', 'n_gpus': num_gpus, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
-            'graphs': graphs,
+            'graphs': graphs, 'deterministic': args.deterministic == 'on',
             'scaling': 'weak', 'vs_baseline': None,
             'dtype': f'{args.fp16_dtype}+fp32 ({args.fp16_dtype} at the 4 highest resolutions, fp32 below; f32 accumulate)',
             'data': 'synthetic (U(-1,1) reals resident in HBM, device-drawn z, random one-hot c; random-init weights)',

@@ -847,10 +847,17 @@ __global__ __launch_bounds__(256, S3 ? 2 : 3) void conv_fwd_kernel(ConvArgs a) {
 
 // Split-K finalize: f32 partial sums -> T with the fused epilogue.
 template <typename T>
-__global__ void conv_finalize_kernel(T* y, float* src, Epi e, int64_t n_el, int Cout, int64_t pix_per_n, int clean) {
+__global__ void conv_finalize_kernel(T* y, float* src, const float* slots, int nslots, Epi e, int64_t n_el, int Cout,
+                                     int64_t pix_per_n, int clean) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_el; i += (int64_t)gridDim.x * blockDim.x) {
-        const float c = src[i];
-        if (clean) src[i] = 0.f;                 // leave the workspace zeroed for the next split-K call
+        float c;
+        if (slots) {                             // deterministic mode: the splits' partial sums in split order
+            c = 0.f;
+            for (int k = 0; k < nslots; ++k) c += slots[(int64_t)k * n_el + i];
+        } else {
+            c = src[i];
+            if (clean) src[i] = 0.f;             // leave the workspace zeroed for the next split-K call
+        }
         float v = c;
         if (e.dot_out) {
             const int64_t pix = i / Cout;
@@ -1604,19 +1611,17 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
             splits = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(target, blocks), maxnk / 4));
         const bool split = splits > 1;
         const bool clean = workspace_clean();
-        // deterministic mode: split s writes its partial sums to slot s, det_sum adds the slots in order into a
-        // zeroed arena buffer that the finalize reads; the dot's per-element products go to det_dot
+        // deterministic mode: split s writes its partial sums to slot s (every output element of every slot: the
+        // splits cover all K steps' tiles), and the finalize adds the slots in split order; the dot's per-element
+        // products go to det_dot
         DetArena arena;
         float* det_acc = nullptr;
         float* acc_src = workspace;
         if (det_on()) {
             if (base.e.dot_out) SG2_DET_GET(base.e.det_dot, arena, total_out, "sg2_conv2d");
-            if (split) {
-                SG2_DET_GET(det_acc, arena, (int64_t)splits * total_out, "sg2_conv2d");
-                SG2_DET_GET(acc_src, arena, total_out, "sg2_conv2d");
-            }
+            if (split) SG2_DET_GET(det_acc, arena, (int64_t)splits * total_out, "sg2_conv2d");
         }
-        if (split && (!clean || det_acc)) {
+        if (split && !clean && !det_acc) {
             hipError_t e = zero_fill(acc_src, total_out * sizeof(float), s);
             if (e != hipSuccess) { set_error("sg2_conv2d: memset failed"); return (int)e; }
         }
@@ -1642,13 +1647,9 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
             else rc = launch_fwd<T, 128, 64>(a, vec, s);
         }
         if (rc == 0 && split) {
-            if (det_acc) {
-                hipError_t e = det_sum(acc_src, 0, det_acc, 0, total_out, 1, splits, total_out, arena, s);
-                if (e) { set_error("sg2_conv2d: det_sum"); return (int)e; }
-            }
             const int g = (int)std::min<int64_t>(cdiv(total_out, 256), 4096);
-            conv_finalize_kernel<T><<<g, 256, 0, s>>>((T*)y, acc_src, base.e, total_out, Cout, (int64_t)OH * OW,
-                                                      (int)(clean && !det_acc));
+            conv_finalize_kernel<T><<<g, 256, 0, s>>>((T*)y, acc_src, det_acc, det_acc ? splits : 0, base.e, total_out,
+                                                      Cout, (int64_t)OH * OW, (int)clean);
             rc = launch_status("sg2_conv2d finalize");
         }
         if (rc == 0 && base.e.det_dot) {

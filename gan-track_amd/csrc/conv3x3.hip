@@ -20,6 +20,7 @@
 #include "sg2_common.h"
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 namespace sg2 {
@@ -53,8 +54,10 @@ struct Conv3Args {
     const void* residual;   // optional [N,OH,OW,Cout] (dtype T): y = round(act(...)) + residual (the D resnet add)
     int raw_act;            // y_raw receives the activated value before the residual add (the activation
                             // gradient's input) instead of the raw conv output
-    float* det_dot;         // deterministic mode: [N, OH, OW, Cout] per-element dot products (det_sum adds them)
+    float* det_dot;         // deterministic mode: the dot's partial sums by slot (det_sum adds them per sample):
+                            // halo kernel [tile][Cout], one per 256-pixel tile; c64p [N][det_maxb][8 waves][64]
     int edge_rx, edge_cy;   // up-2 edge split: per image, tiles of the last cell row / column (0: no split)
+    int det_maxb;           // c64p, deterministic mode: workgroups that can share one sample (slot rows per sample)
 };
 
 // Output channel of MFMA row P of a 64-channel tile (see the C = 64 kernels below)
@@ -240,7 +243,8 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
             }
         typedef T vec8d __attribute__((ext_vector_type(8)));
         const bool want_dot = a.dot_out != nullptr, atom = want_dot && !a.det_dot;
-        float* red = (float*)smem;                 // [BN] dot partial sums (the halo buffer is free after the loop)
+        float* red = (float*)smem;                 // dot partial sums (the halo buffer is free after the loop):
+                                                   // [BN] (atomic mode), [4 waves][BN] (deterministic mode)
         if (atom) {
             if (tid < BN) red[tid] = 0.f;
             __syncthreads();
@@ -283,17 +287,14 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
                 if (yr) *(vec8d*)(yr + dst) = rv;
                 if (want_dot) {
                     const vec8d sv = *(const vec8d*)(dsrc + dst);
-                    if (a.det_dot) {
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) a.det_dot[dst + e] = (float)rv[e] * (float)sv[e];
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) dacc[h][e] += (float)rv[e] * (float)sv[e];
-                    }
+                    for (int e = 0; e < 8; ++e) dacc[h][e] += (float)rv[e] * (float)sv[e];
                 }
             }
         }
-        if (atom) {
+        if (want_dot) {
+            // the 16 pixel lanes of a channel group by shuffles; then the 4 waves: LDS atomics + one global atomic
+            // per channel, or (deterministic mode) wave partials added in wave order into the tile's slot
 #pragma unroll
             for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -303,10 +304,17 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
                     v += __shfl_xor(v, 2);
                     v += __shfl_xor(v, 4);
                     v += __shfl_xor(v, 8);
-                    if (l16 == 0) atomicAdd(&red[32 * h + 8 * lq + e], v);
+                    if (l16 == 0) {
+                        if (atom) atomicAdd(&red[32 * h + 8 * lq + e], v);
+                        else red[wave * BN + 32 * h + 8 * lq + e] = v;
+                    }
                 }
             __syncthreads();
-            if (tid < BN) atomicAdd(&a.dot_out[(int64_t)n * a.Cout + o0 + tid], red[tid]);
+            if (tid < BN) {
+                if (atom) atomicAdd(&a.dot_out[(int64_t)n * a.Cout + o0 + tid], red[tid]);
+                else a.det_dot[(int64_t)tile * a.Cout + o0 + tid] = ((red[tid] + red[BN + tid]) + red[2 * BN + tid]) +
+                                                                     red[3 * BN + tid];
+            }
         }
         return;
     }
@@ -388,13 +396,8 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
             if (want_dot) {
                 const vec8o sv = *(const vec8o*)(dsrc + dst);
                 const vec8o rv = *(const vec8o*)(rt + m * OS + c8);
-                if (a.det_dot) {
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) a.det_dot[dst + e] = (float)rv[e] * (float)sv[e];
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) dacc[e] += (float)rv[e] * (float)sv[e];
-                }
+                for (int e = 0; e < 8; ++e) dacc[e] += (float)rv[e] * (float)sv[e];
             }
         } else {
             for (int e = 0; e < 8 && o + e < a.Cout; ++e) {
@@ -402,11 +405,7 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
                 if (want_raw) yr[dst + e] = a.raw_act ? yo : rt[m * OS + c8 + e];
                 if (a.residual) yo = (T)((float)yo + (float)((const T*)a.residual)[dst + e]);
                 y[dst + e] = yo;
-                if (want_dot) {
-                    const float pr = (float)rt[m * OS + c8 + e] * (float)dsrc[dst + e];
-                    if (a.det_dot) a.det_dot[dst + e] = pr;
-                    else dacc[e] += pr;
-                }
+                if (want_dot) dacc[e] += (float)rt[m * OS + c8 + e] * (float)dsrc[dst + e];
             }
         }
     }
@@ -415,6 +414,19 @@ __global__ __launch_bounds__(256, 3 - NBUF) void conv3x3_halo_kernel(Conv3Args a
         for (int e = 0; e < 8; ++e) atomicAdd(&red[c8 + e], dacc[e]);
         __syncthreads();
         if (tid < BN && o0 + tid < a.Cout) atomicAdd(&a.dot_out[(int64_t)n * a.Cout + o0 + tid], red[tid]);
+    } else if (want_dot) {
+        // deterministic mode: the 32 threads of a channel octet in thread order (the tiles are free now), into the
+        // tile's slot
+        float* part = (float*)smem;                // [32][BN]
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part[(tid >> 3) * BN + c8 + e] = dacc[e];
+        __syncthreads();
+        if (tid < BN && o0 + tid < a.Cout) {
+            float v = 0.f;
+            for (int r = 0; r < 32; ++r) v += part[r * BN + tid];
+            a.det_dot[(int64_t)tile * a.Cout + o0 + tid] = v;
+        }
     }
 }
 
@@ -430,6 +442,17 @@ int launch3_k(const Conv3Args& a, hipStream_t s) {
         attr_set = true;
     }
     dim3 grid(a.N * a.tiles_x * a.tiles_y, (a.Cout + BN - 1) / BN);
+    if (a.dot_out && det_on()) {     // the dot's tile partials by slot, summed per sample in tile order
+        Conv3Args b = a;
+        DetArena arena;
+        const int tps = a.tiles_x * a.tiles_y;
+        SG2_DET_GET(b.det_dot, arena, (int64_t)grid.x * a.Cout, "sg2_conv3x3");
+        kern<<<grid, 256, lds, s>>>(b);
+        if (int rc = launch_status("sg2_conv3x3")) return rc;
+        hipError_t e = det_sum(a.dot_out, a.Cout, b.det_dot, (int64_t)tps * a.Cout, a.Cout, a.N, tps, a.Cout, arena, s);
+        if (e) { set_error("sg2_conv3x3: det_sum"); return (int)e; }
+        return 0;
+    }
     kern<<<grid, 256, lds, s>>>(a);
     return launch_status("sg2_conv3x3");
 }
@@ -751,7 +774,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64p_kernel(Conv3Args a, int t
                             v += __shfl_xor(v, 2);
                             v += __shfl_xor(v, 4);
                             v += __shfl_xor(v, 8);
-                            if (l16 == 0) atomicAdd(&a.dot_out[(int64_t)n * P_C + jj * 32 + oq8 + e], v);
+                            if (l16 == 0) {
+                                if (a.det_dot) {
+                                    // deterministic mode: this wave's slot of (sample n, workgroup offset within the
+                                    // workgroups that can cover n: blockIdx.x - first of them)
+                                    const int64_t blo = ((int64_t)(n * per_n + 1) * gridDim.x + tiles_total - 1) / tiles_total - 1;
+                                    a.det_dot[(((int64_t)n * a.det_maxb + (blockIdx.x - blo)) * 8 + wave) * P_C + jj * 32 + oq8 + e] = v;
+                                } else {
+                                    atomicAdd(&a.dot_out[(int64_t)n * P_C + jj * 32 + oq8 + e], v);
+                                }
+                            }
                             dacc[jj][e] = 0.f;
                         }
                 }
@@ -773,6 +805,33 @@ int launch_c64p(const Conv3Args& a, hipStream_t s, int tiles, int grid) {
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P_LDS);
         attr_set = true;
+    }
+    if (DOT && det_on()) {
+        // deterministic mode: slots [N][maxb][8 waves][64] (maxb: the most workgroups one sample's tiles spread
+        // over, offsets from the first that can cover it -- the kernel's formula), zeroed (a sample's later
+        // offsets may be unused), summed per sample in slot order
+        const int per_n = (a.W / P_TW) * (a.H / P_TH);
+        int maxb = 1;
+        for (int b = 0; b < grid; ++b) {
+            const int t0 = (int)((int64_t)b * tiles / grid), t1 = (int)((int64_t)(b + 1) * tiles / grid);
+            if (t0 >= t1) continue;
+            for (int n = t0 / per_n; n <= (t1 - 1) / per_n; ++n) {
+                const int64_t blo = ((int64_t)(n * per_n + 1) * grid + tiles - 1) / tiles - 1;
+                maxb = std::max(maxb, (int)(b - blo) + 1);
+            }
+        }
+        Conv3Args b = a;
+        DetArena arena;
+        const int64_t nslot = (int64_t)maxb * 8 * P_C;
+        SG2_DET_GET(b.det_dot, arena, a.N * nslot, "sg2_conv3x3 (c64 persistent)");
+        b.det_maxb = maxb;
+        hipError_t e = zero_fill(b.det_dot, a.N * nslot * sizeof(float), s);
+        if (e) { set_error("sg2_conv3x3 (c64 persistent): zero"); return (int)e; }
+        kern<<<grid, 512, P_LDS, s>>>(b, tiles);
+        if (int rc = launch_status("sg2_conv3x3 (c64 persistent)")) return rc;
+        e = det_sum(a.dot_out, P_C, b.det_dot, nslot, P_C, a.N, (int64_t)maxb * 8, P_C, arena, s);
+        if (e) { set_error("sg2_conv3x3 (c64 persistent): det_sum"); return (int)e; }
+        return 0;
     }
     kern<<<grid, 512, P_LDS, s>>>(a, tiles);
     return launch_status("sg2_conv3x3 (c64 persistent)");
@@ -1421,15 +1480,42 @@ __global__ __launch_bounds__((Ring<R_TH, WR>::NW) * 64, (Ring<R_TH, WR>::WGS_PER
 }
 
 int* ring_queue_slot() {
-    // one counter table per launch in flight (a rotating slot; each is left zero by its launch's workgroups);
-    // device globals start zeroed
-    static int* base = nullptr;
-    static int next = 0;           // (launches are issued from one host thread per stream; a race only shares a slot)
-    if (!base && hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_ring_q)) != hipSuccess) base = nullptr;
-    if (!base) return nullptr;
-    int* p = base + 2 * RQ_MAXN * (next % RQ_SLOTS);
-    ++next;
-    return p;
+    // One counter table per launch in flight: a rotating slot of g_ring_q, each left zero by its launch's
+    // workgroups (device globals start zeroed).  The symbol's address is per device, so it is looked up per device.
+    // Two launches that share a slot must not run at once: the dynamic tail relies on launches being serialized per
+    // slot -- the library's launches of one process are issued to one stream at a time (the trainer's phases, and
+    // their graph replays, run in stream order), and RQ_SLOTS launches separate two users of a slot.
+    static std::atomic<int*> base[64];
+    static std::atomic<unsigned> next{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    int* b = base[dev].load(std::memory_order_acquire);
+    if (!b) {
+        if (hipGetSymbolAddress((void**)&b, HIP_SYMBOL(g_ring_q)) != hipSuccess) return nullptr;
+        base[dev].store(b, std::memory_order_release);
+    }
+    return b + 2 * RQ_MAXN * (next.fetch_add(1, std::memory_order_relaxed) % RQ_SLOTS);
+}
+
+// The dynamic tail's plan (form 49): static tiles per workgroup, chunk count and the reciprocals of the tile
+// decode.  false when the shape cannot take it (the caller then launches the static form 46).
+// SG2_RING_DYN: percent of a sample's tiles handed out dynamically (default 12), a whole number of 2-tile chunks.
+bool ring_dyn_plan(const Conv3Args& a, int tiles, int grid, int band, RingDyn& dyn) {
+    static const int pct = [] { const char* e = getenv("SG2_RING_DYN"); return e ? std::max(0, std::min(50, atoi(e))) : 12; }();
+    if (grid % a.N || a.N > RQ_MAXN || (band != 1 && band != 2 && band != 4)) return false;
+    const int per_n = tiles / a.N, gpn = grid / a.N;
+    const int per_band = band * (a.W / R_TW);
+    if (per_n / gpn < 8 || per_n < 2 || per_band < 2 || (int64_t)tiles * per_n >= (1ll << 32)) return false;
+    int sp = std::max(2, (int)((int64_t)per_n * (100 - pct) / (100 * (int64_t)gpn)));
+    while (sp > 2 && (per_n - gpn * sp) % 2) --sp;
+    if (gpn * sp > per_n || (per_n - gpn * sp) % 2) return false;
+    dyn.s_per_wg = sp;
+    dyn.wg_per_n = gpn;
+    dyn.nchunks = (per_n - gpn * sp) / 2;
+    dyn.m_pern = (unsigned)((1ull << 32) / (unsigned)per_n + 1);
+    dyn.m_pband = (unsigned)((1ull << 32) / (unsigned)per_band + 1);
+    dyn.band_sh = band == 4 ? 2 : (band == 2 ? 1 : 0);
+    return true;
 }
 
 template <typename T, bool SI, bool EPI, bool RAW, int TH, int WR, bool PIPE, int STG>
@@ -1442,23 +1528,8 @@ int launch_c64r(const Conv3Args& a, hipStream_t s, int tiles, int grid, int band
         attr_set = true;
     }
     RingDyn dyn{nullptr, 0, 0, 0, 0u, 0u, 0};
-    if ((STG & 16) != 0) {
-        // the caller (launch_c64r_form) checked grid % N == 0; SG2_RING_DYN: percent of a sample's tiles handed out
-        // dynamically (default 12), the dynamic part a whole number of 2-tile chunks
-        static const int pct = [] { const char* e = getenv("SG2_RING_DYN"); return e ? std::max(0, std::min(50, atoi(e))) : 12; }();
-        const int per_n = tiles / a.N, gpn = grid / a.N;
-        int sp = std::max(2, (int)((int64_t)per_n * (100 - pct) / (100 * (int64_t)gpn)));
-        while (sp > 2 && (per_n - gpn * sp) % 2) --sp;
-        dyn.q = ring_queue_slot();
-        dyn.s_per_wg = sp;
-        dyn.wg_per_n = gpn;
-        dyn.nchunks = (per_n - gpn * sp) / 2;
-        const int per_band = band * (a.W / R_TW);
-        dyn.m_pern = (unsigned)((1ull << 32) / (unsigned)per_n + 1);
-        dyn.m_pband = (unsigned)((1ull << 32) / (unsigned)per_band + 1);
-        dyn.band_sh = band == 4 ? 2 : (band == 2 ? 1 : 0);
-        if (!dyn.q || gpn * sp > per_n || (per_n - gpn * sp) % 2 || a.N > RQ_MAXN || per_n < 2 || per_band < 2 ||
-            (int64_t)tiles * per_n >= (1ll << 32) || (band != 1 && band != 2 && band != 4)) {
+    if ((STG & 16) != 0) {     // the caller (launch_c64r_form) checked ring_dyn_plan
+        if (!ring_dyn_plan(a, tiles, grid, band, dyn) || !(dyn.q = ring_queue_slot())) {
             set_error("sg2_conv3x3 (c64 ring): dynamic tail unavailable");
             return -1;
         }
@@ -1489,9 +1560,11 @@ int launch_c64r_form(const Conv3Args& a, hipStream_t s, int form) {
     if (form == 44) return launch_c64r_raw<T, SI, EPI, 4, 2, false, 1>(a, s, tiles, 2 * num_cus(), band);
 
     if (form == 46) return launch_c64r_raw<T, SI, EPI, 4, 2, false, 4>(a, s, tiles, 2 * num_cus(), band);
-    if (form == 49) {     // the dynamic tail needs whole samples per workgroup group and >= 8 tiles per workgroup
-        const int grid = 2 * num_cus(), per_n = tiles / a.N;
-        if (grid % a.N == 0 && per_n / (grid / a.N) >= 8)
+    if (form == 49) {     // the dynamic tail where its plan exists (whole samples per workgroup group, >= 8 tiles
+                          // per workgroup, an even dynamic remainder ...), else the static form 46
+        const int grid = 2 * num_cus();
+        RingDyn probe{nullptr, 0, 0, 0, 0u, 0u, 0};
+        if (ring_dyn_plan(a, tiles, grid, band, probe))
             return launch_c64r_raw<T, SI, EPI, 4, 2, false, 20>(a, s, tiles, grid, band);
         return launch_c64r_raw<T, SI, EPI, 4, 2, false, 4>(a, s, tiles, grid, band);
     }
@@ -2001,7 +2074,7 @@ int dispatch(Conv3Args& a, hipStream_t s, int stride) {
     }
     // (the persistent kernel's epilogue folds the gain into the demod / noise / bias terms and evaluates lrelu
     // as max(v, alpha v): it needs gain > 0 and 0 <= alpha <= 1, the StyleGAN2 settings)
-    if (persist && !(a.dot_out && a.det_dot) && a.Cin == P_C && a.Cout == P_C && a.H % P_TH == 0 && a.W % P_TW == 0 &&
+    if (persist && a.Cin == P_C && a.Cout == P_C && a.H % P_TH == 0 && a.W % P_TW == 0 &&
         (!epi || (a.gain > 0.f && (a.act == 0 || (a.alpha >= 0.f && a.alpha <= 1.f))))) {
         const int tiles = a.N * (a.H / P_TH) * (a.W / P_TW);
         if (tiles >= 2 * num_cus()) {
@@ -2290,16 +2363,9 @@ int conv3x3_entry(void* y, void* y_raw, const void* x, const void* w, int dtype,
     a.OH = stride == 1 ? H : (H - 3) / 2 + 1;
     a.OW = stride == 1 ? W : (W - 3) / 2 + 1;
     hipStream_t s = as_stream(stream);
-    // deterministic mode: the dot's per-element products by slot, summed per sample in a fixed order (the
-    // persistent C = 64 kernel's wave-level atomics are bypassed: the halo kernel takes the call)
-    DetArena arena;
-    if (dot_out && det_on()) SG2_DET_GET(a.det_dot, arena, (int64_t)N * a.OH * a.OW * Cout, "sg2_conv3x3");
-    int rc = dtype == SG2_F16 ? dispatch<f16_t>(a, s, stride) : dispatch<bf16_t>(a, s, stride);
-    if (rc || !a.det_dot) return rc;
-    hipError_t e = det_sum(dot_out, Cout, a.det_dot, (int64_t)a.OH * a.OW * Cout, Cout, N, (int64_t)a.OH * a.OW, Cout,
-                           arena, s);
-    if (e) { set_error("sg2_conv3x3: det_sum"); return (int)e; }
-    return 0;
+    // deterministic mode: the kernels that take a dot (halo, persistent C = 64) write their partial sums to slots
+    // and sum them per sample in a fixed order (launch3_k, launch_c64p)
+    return dtype == SG2_F16 ? dispatch<f16_t>(a, s, stride) : dispatch<bf16_t>(a, s, stride);
 }
 }  // namespace
 }  // namespace sg2

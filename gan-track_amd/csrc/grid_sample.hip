@@ -28,19 +28,22 @@ struct Corners {
     float w00, w01, w10, w11;  // w[yy][xx]
 };
 
+// affine_grid, align_corners = False: base coordinate of pixel j at its centre, (2j + 1) / W - 1
+__device__ __forceinline__ float base_coord(int j, int W) { return (float)(2 * j + 1) / (float)W - 1.f; }
+
+__device__ __forceinline__ Corners corners_g(float gx, float gy, int Hi, int Wi);
+
+__device__ __forceinline__ Corners corners_affine(const float* t, float bx, float by, int Hi, int Wi) {
+    return corners_g(t[0] * bx + t[1] * by + t[2], t[3] * bx + t[4] * by + t[5], Hi, Wi);
+}
+
 __device__ __forceinline__ Corners corners(const GSParams& p, int n, int oy, int ox, int Hi, int Wi) {
-    float gx, gy;
-    if (p.theta) {
-        // affine_grid, align_corners = False: base coordinates at pixel centres, (2j + 1) / W - 1
-        const float* t = p.theta + n * 6;
-        const float bx = (float)(2 * ox + 1) / (float)p.Wo - 1.f, by = (float)(2 * oy + 1) / (float)p.Ho - 1.f;
-        gx = t[0] * bx + t[1] * by + t[2];
-        gy = t[3] * bx + t[4] * by + t[5];
-    } else {
-        const float* g = p.grid + (((int64_t)n * p.Ho + oy) * p.Wo + ox) * 2;
-        gx = g[0];
-        gy = g[1];
-    }
+    if (p.theta) return corners_affine(p.theta + n * 6, base_coord(ox, p.Wo), base_coord(oy, p.Ho), Hi, Wi);
+    const float* g = p.grid + (((int64_t)n * p.Ho + oy) * p.Wo + ox) * 2;
+    return corners_g(g[0], g[1], Hi, Wi);
+}
+
+__device__ __forceinline__ Corners corners_g(float gx, float gy, int Hi, int Wi) {
     const float ix = ((gx + 1.f) * Wi - 1.f) * 0.5f;
     const float iy = ((gy + 1.f) * Hi - 1.f) * 0.5f;
     Corners c;
@@ -128,39 +131,46 @@ __global__ __launch_bounds__(256) void grid_sample_bwd_gather_kernel(GSParams p)
         const int n = (int)(idx / ((int64_t)wl * hl));
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
         if (X < Wi && Y < Hi) {
-            const float* t = p.theta + n * 6;
+            float t[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) t[j] = p.theta[n * 6 + j];
             // d(ix)/d(ox) etc. and the offset, in double for the inversion only
-            const double a00 = (double)t[0] * Wi / p.Wo, a01 = (double)t[1] * Wi / p.Ho;
-            const double a10 = (double)t[3] * Hi / p.Wo, a11 = (double)t[4] * Hi / p.Ho;
+            const double rwo = 1.0 / p.Wo, rho = 1.0 / p.Ho;
+            const double a00 = (double)t[0] * Wi * rwo, a01 = (double)t[1] * Wi * rho;
+            const double a10 = (double)t[3] * Hi * rwo, a11 = (double)t[4] * Hi * rho;
             // ix at (ox, oy) = ((t0 bx + t1 by + t2 + 1) Wi - 1) / 2 with bx = (2 ox + 1) / Wo - 1
-            const double c0 = (((double)t[0] * (1.0 / p.Wo - 1.0) + (double)t[1] * (1.0 / p.Ho - 1.0) + t[2] + 1.0) * Wi - 1.0) * 0.5;
-            const double c1 = (((double)t[3] * (1.0 / p.Wo - 1.0) + (double)t[4] * (1.0 / p.Ho - 1.0) + t[5] + 1.0) * Hi - 1.0) * 0.5;
+            const double c0 = (((double)t[0] * (rwo - 1.0) + (double)t[1] * (rho - 1.0) + t[2] + 1.0) * Wi - 1.0) * 0.5;
+            const double c1 = (((double)t[3] * (rwo - 1.0) + (double)t[4] * (rho - 1.0) + t[5] + 1.0) * Hi - 1.0) * 0.5;
             const double det = a00 * a11 - a01 * a10;
             // a (near-)singular map: scan the whole output (the bounds below clamp to it)
             double oxmin = -1e30, oxmax = 1e30, oymin = -1e30, oymax = 1e30;
             if (fabs(det) > 1e-12) {
+                const double rdet = 1.0 / det;
                 oxmin = 1e30; oxmax = -1e30; oymin = 1e30; oymax = -1e30;
                 for (int cy = 0; cy < 2; ++cy)
                     for (int cx = 0; cx < 2; ++cx) {
                         const double u = (X - 1 + 2 * cx) - c0, v = (Y - 1 + 2 * cy) - c1;
-                        const double ox = (a11 * u - a01 * v) / det, oy = (-a10 * u + a00 * v) / det;
+                        const double ox = (a11 * u - a01 * v) * rdet, oy = (-a10 * u + a00 * v) * rdet;
                         oxmin = fmin(oxmin, ox); oxmax = fmax(oxmax, ox);
                         oymin = fmin(oymin, oy); oymax = fmax(oymax, oy);
                     }
             }
             // clamped in double before the int conversion (a huge or NaN bound is undefined as an int)
             auto cl = [](double v, int hi) { return v > -4.0 ? (v < hi + 4.0 ? v : hi + 4.0) : -4.0; };
-            const int ox0 = max(0, (int)floor(cl(oxmin, p.Wo)) - 2), ox1 = min(p.Wo - 1, (int)ceil(cl(oxmax, p.Wo)) + 2);
-            const int oy0 = max(0, (int)floor(cl(oymin, p.Ho)) - 2), oy1 = min(p.Ho - 1, (int)ceil(cl(oymax, p.Ho)) + 2);
-            for (int oy = oy0; oy <= oy1; ++oy)
+            // (a one-pixel margin: the float corners differ from the exact map by far less than a pixel)
+            const int ox0 = max(0, (int)floor(cl(oxmin, p.Wo)) - 1), ox1 = min(p.Wo - 1, (int)ceil(cl(oxmax, p.Wo)) + 1);
+            const int oy0 = max(0, (int)floor(cl(oymin, p.Ho)) - 1), oy1 = min(p.Ho - 1, (int)ceil(cl(oymax, p.Ho)) + 1);
+            for (int oy = oy0; oy <= oy1; ++oy) {
+                const float by = base_coord(oy, p.Ho);
                 for (int ox = ox0; ox <= ox1; ++ox) {
-                    const Corners k = corners(p, n, oy, ox, Hi, Wi);
+                    const Corners k = corners_affine(t, base_coord(ox, p.Wo), by, Hi, Wi);
                     const int dx = X - k.x0, dy = Y - k.y0;           // 0 or 1 when (X, Y) is a corner
                     if ((unsigned)dx > 1u || (unsigned)dy > 1u) continue;
                     const float w = dy ? (dx ? k.w11 : k.w10) : (dx ? k.w01 : k.w00);
                     for (int c = 0; c < p.C && c < 4; ++c)
                         acc[c] += (float)gout[n * p.os_n + c * p.os_c + (int64_t)oy * p.os_h + (int64_t)ox * p.os_w] * w;
                 }
+            }
         }
         for (int c = 0; c < p.C && c < 4; ++c) gin[n * p.is_n + c * p.is_c + (int64_t)Y * p.is_h + (int64_t)X * p.is_w] = acc[c];
     }

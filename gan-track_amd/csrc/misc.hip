@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void pack_weight_multi_kernel(const PackTable 
         const int64_t base = (int64_t)a * d.sa;
         for (int i = threadIdx.x; i < L; i += 256) {
             const int bb = i / d.K, k = i - bb * d.K;
-            float x = ld_any(d.in, base + (int64_t)bb * d.sb + k * d.sk, d.in_dt) * d.scale;
+            float x = ld_any(d.in, base + (int64_t)bb * d.sb + (int64_t)k * d.sk, d.in_dt) * d.scale;
             asm volatile("" : "+v"(x));          // (as pack_weight_kernel: the f32 product, then one rounding)
             row[i] = x;
         }
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void pack_weight_multi_kernel(const PackTable 
         const unsigned r = ec / (unsigned)d.B, bb = ec - r * d.B;
         const unsigned a = r / (unsigned)d.K, k = r - a * d.K;
         const int kk = d.flip ? d.K - 1 - (int)k : (int)k;
-        v[j] = ld_any(d.in, (int64_t)a * d.sa + (int64_t)bb * d.sb + kk * d.sk, d.in_dt) * d.scale;
+        v[j] = ld_any(d.in, (int64_t)a * d.sa + (int64_t)bb * d.sb + (int64_t)kk * d.sk, d.in_dt) * d.scale;
     }
 #pragma unroll
     for (int j = 0; j < PACK_EPT; ++j) {

@@ -60,8 +60,9 @@ class DetArena {
     float* base_;
     int64_t cap_, off_;
 };
-// out[g * go + i] += sum_{s < S} ws[g * gw + s * ss + i] for g < G, i < n: a fixed-order sum (runs of 64
-// consecutive s first, then runs of those, ...), temporaries from `arena`.
+// out[g * go + i] += sum_{s < S} ws[g * gw + s * ss + i] for g < G (<= 65535), i < n: a fixed-order sum (four
+// interleaved row sums over s, s = r mod 4 in increasing s, added in row order; det.hip), one launch.  `arena` is
+// kept for the callers' symmetry and unused.
 hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t ss, int G, int64_t S, int64_t n,
                    DetArena& arena, hipStream_t st);
 #define SG2_DET_GET(ptr, arena, n, what)                                                        \

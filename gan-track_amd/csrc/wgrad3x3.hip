@@ -744,12 +744,15 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
 }
 
 namespace {
-// det mode: allocate and zero the slot array for `slots` workgroup splits
-int w3_det_slots(W3Args& a, DetArena& arena, int slots, hipStream_t s) {
+// det mode: allocate the slot array for `slots` workgroup splits.  A launch that writes every tap of its
+// workgroup's (a, b) block (all taps in one phase) fills its slot completely; `zero` (several phase launches, each
+// writing its own taps) zeroes the array first.
+int w3_det_slots(W3Args& a, DetArena& arena, int slots, hipStream_t s, bool zero = false) {
     if (!det_on()) return 0;
     const int64_t n = (int64_t)slots * a.A * a.KK * a.B;
     SG2_DET_GET(a.det, arena, n, "sg2_conv2d_wgrad (halo)");
     a.det_slots = slots;
+    if (!zero) return 0;
     hipError_t e = zero_fill(a.det, n * sizeof(float), s);
     if (e) { set_error("sg2_conv2d_wgrad: zero"); return (int)e; }
     return 0;
@@ -838,7 +841,7 @@ int wgrad3x3_run(W3Args& a, DetArena& arena, float* dw, const void* g, const voi
         }
         return launch_status("sg2_conv2d_wgrad (halo, LDS-DMA)");
     }
-    if (int rc = w3_det_slots(a, arena, (int)grid.z, s)) return rc;
+    if (int rc = w3_det_slots(a, arena, (int)grid.z, s, stride > 1)) return rc;
     for (int py = 0; py < stride; ++py)
         for (int px = 0; px < stride; ++px) {
             int nt = 0;

@@ -128,27 +128,39 @@ def clean_workspace(on=True):
 
 
 _det_scratch = {}
+_det_retired = []
+_det_state = (0, 0)     # the registration in force: (scratch pointer, bytes); (0, 0) = float-atomic mode
+
+
+def _det_register(ptr, nbytes):
+    global _det_state
+    lib().sg2_set_deterministic(ctypes.c_void_p(ptr), ctypes.c_int64(nbytes))
+    _det_state = (ptr, nbytes)
 
 
 @contextlib.contextmanager
 def deterministic(on=True, scratch_mb=2048, device=None):
     """Bitwise-reproducible mode (sg2_set_deterministic): inside, every float accumulation the kernels would make
-    with atomics is made through slots of a device scratch buffer summed in a fixed order.  The scratch
+    with atomics is made through slots of a device scratch buffer summed in a fixed order -- the arithmetic the
+    training iteration runs by default (training/trainer.py Trainer(deterministic=True)).  on=False selects the
+    float-atomic reductions inside (an A/B mode).  The mode in force before is restored on exit.  The scratch
     (`scratch_mb` MiB, allocated once per device and kept) must not be used by two streams at once: run the calls
     inside on one stream."""
-    if not on:
-        yield
-        return
-    L = lib()
-    dev = torch.device('cuda', torch.cuda.current_device()) if device is None else torch.device(device)
-    buf = _det_scratch.get(dev)
-    if buf is None or buf.numel() * 4 < scratch_mb << 20:
-        buf = _det_scratch[dev] = torch.empty([scratch_mb << 18], dtype=torch.float32, device=dev)
-    L.sg2_set_deterministic(ctypes.c_void_p(buf.data_ptr()), ctypes.c_int64(buf.numel() * 4))
+    prev = _det_state
+    if on:
+        dev = torch.device('cuda', torch.cuda.current_device()) if device is None else torch.device(device)
+        buf = _det_scratch.get(dev)
+        if buf is None or buf.numel() * 4 < scratch_mb << 20:
+            if buf is not None:
+                _det_retired.append(buf)     # a captured graph may still write the old scratch
+            buf = _det_scratch[dev] = torch.empty([scratch_mb << 18], dtype=torch.float32, device=dev)
+        _det_register(buf.data_ptr(), buf.numel() * 4)
+    else:
+        _det_register(0, 0)
     try:
         yield
     finally:
-        L.sg2_set_deterministic(ctypes.c_void_p(0), ctypes.c_int64(0))
+        _det_register(*prev)
 
 
 @contextlib.contextmanager

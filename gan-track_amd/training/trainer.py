@@ -22,6 +22,8 @@ torch.optim.Adam arithmetic) then reads the flat buffer directly: /N, nan_to_num
 one launch.  Summation order of the all_reduce differs from the reference's single flat all_reduce only
 by fp32 rounding.
 """
+import contextlib
+
 import numpy as np
 import torch
 
@@ -183,8 +185,12 @@ class Trainer:
     def __init__(self, G, D, G_ema, loss, G_opt_kwargs, D_opt_kwargs, G_reg_interval=4, D_reg_interval=16,
                  batch_size=32, batch_gpu=32, num_gpus=1, rank=0, device=None, ema_kimg=10, ema_rampup=0.05,
                  augment_pipe=None, ada_target=None, ada_interval=4, ada_kimg=500, bucket_mb=32, overlap=True,
-                 phase_timing=False, graphs=False):
+                 phase_timing=False, graphs=False, deterministic=True):
         self.G, self.D, self.G_ema, self.loss = G, D, G_ema, loss
+        # the library's fixed-order reductions (sg2hip.deterministic) for every phase's forward and backward: the
+        # iteration is bitwise reproducible run to run, and measured faster than the float-atomic reductions on the
+        # bench workload (747 vs 740 img/s, profiles/r06e_*); False selects the float atomics (an A/B mode)
+        self.deterministic = deterministic
         self.batch_size, self.batch_gpu, self.num_gpus, self.rank = batch_size, batch_gpu, num_gpus, rank
         self.device = device
         self.ema_kimg, self.ema_rampup = ema_kimg, ema_rampup
@@ -246,7 +252,7 @@ class Trainer:
         chunks = list(zip(phase_real_img, phase_real_c, phase_gen_z, phase_gen_c))
         # the phase's weights are fixed until its optimizer step: every pack made once, all in one launch at the
         # phase start from the second run on (the plan recorded by the first, kept on the phase)
-        with conv2d_gradfix.pack_cache(plan=phase):
+        with conv2d_gradfix.pack_cache(plan=phase), self._arith():
             for ci, (real_img, real_c, gen_z, gen_c) in enumerate(chunks):
                 if ci == len(chunks) - 1:
                     passes = self.loss.backward_passes(phase.name, gen_z.shape[0] + real_img.shape[0]) \
@@ -254,6 +260,13 @@ class Trainer:
                     phase.exchange.arm(phase.name, passes)
                 self.loss.accumulate_gradients(phase=phase.name, real_img=real_img, real_c=real_c, gen_z=gen_z,
                                                gen_c=gen_c, gain=phase.interval, cur_nimg=self.cur_nimg)
+
+    def _arith(self):
+        """The reduction mode of the phase passes: deterministic (default) or float-atomic (sg2hip.deterministic)."""
+        if self.device is None or self.device.type != 'cuda':
+            return contextlib.nullcontext()
+        import sg2hip
+        return sg2hip.deterministic(self.deterministic, device=self.device)
 
     def _graph_phase(self, phase, phase_real_img, phase_real_c, phase_gen_z, phase_gen_c):
         """Replay the phase's graph (capturing it the first time): forward + backward of every micro-batch,

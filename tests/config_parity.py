@@ -170,7 +170,8 @@ def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False, i
         cg.presplit = False
     try:
         with sg2hip.deterministic(deterministic, device=dev):
-            return _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated, perturb, perturb_seed)
+            return _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated, perturb, perturb_seed,
+                                deterministic)
     finally:
         if prev[0] is None:
             os.environ.pop('SG2_F32_EXACT', None)
@@ -180,7 +181,8 @@ def run_product(cfg, inp, tape, dev, fp16_dtype=None, aug_p=0.3, graphs=False, i
         nets.grouped_affine = prev[2]
 
 
-def _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated, perturb=0.0, perturb_seed=0):
+def _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated, perturb=0.0, perturb_seed=0,
+                 deterministic=True):
     from training import networks_stylegan2 as net, augment_mi, loss as loss_mod, trainer as trainer_mod
     torch.manual_seed(0)
     G, D = _nets(net, cfg, 0 if fp16_dtype is None else 4, fp16_dtype)
@@ -200,7 +202,7 @@ def _run_product(cfg, inp, tape, dev, fp16_dtype, aug_p, graphs, isolated, pertu
                                   pl_weight=2, pl_no_weight_grad=True)
     opt = dict(class_name='torch.optim.Adam', lr=0.0025, betas=[0, 0.99], eps=1e-8)
     tr = trainer_mod.Trainer(G, D, G_ema, loss, opt, opt, batch_size=cfg['batch'], batch_gpu=cfg['batch'],
-                             num_gpus=1, rank=0, device=dev)
+                             num_gpus=1, rank=0, device=dev, deterministic=deterministic)
     out, stats = {}, []
 
     def on_grads(name, module):

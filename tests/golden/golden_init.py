@@ -81,9 +81,10 @@ def unpack(z):
     """Inverse of pack (accepts an NpzFile or a dict)."""
     d = {k: z[k] for k in z if not k.startswith('summ__')}
     if 'summ__names' in z:
-        numel = z['summ__numel']
+        # each array read once (an NpzFile decompresses the whole member on every z[key])
+        numel, norm, samples = z['summ__numel'], z['summ__norm'], z['summ__samples']
         for i, n in enumerate(z['summ__names'].tolist()):
-            d[n + '/norm'] = z['summ__norm'][i]
+            d[n + '/norm'] = norm[i]
             d[n + '/numel'] = numel[i]
-            d[n + '/samples'] = z['summ__samples'][i, :min(N_SAMPLES, int(numel[i]))]
+            d[n + '/samples'] = samples[i, :min(N_SAMPLES, int(numel[i]))]
     return d

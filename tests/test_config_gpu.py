@@ -12,15 +12,16 @@ same state, inputs and random draws):
   initial state.  f32 per gradient tensor within max(1e-4, 4 x the reference's f32 error on it, 3 x the
   reference's worst in the phase) of float64 (config_parity.judge_f32) and, where the reference's f32 is within
   1e-4, within 3e-4 of the reference's result itself -- the reference's f32 spread measured by re-running the
-  reference itself (tests/golden/make_ref_spread.py); the production arithmetic in deterministic and in atomic
-  mode and the f32-input MFMA kernels; 16-bit (num_fp16_res = 4, f32 accumulate) per phase, each error measure
+  reference itself (tests/golden/make_ref_spread.py); the production arithmetic (deterministic reductions) and
+  the f32-input MFMA kernels; 16-bit (num_fp16_res = 4, f32 accumulate) per phase, each error measure
   within 2 x the same measure of the reference's own 16-bit error (the oracle's emulation of its fp16 blocks).
 * train_<tag>.npz, C1 and C2: one full iteration (phases, lazy-reg Adam, EMA) -- the step semantics.
 * full-batch runs of C4 (bs16, fp16) and C5 (bs8, bf16): every statistic / norm finite.
 
-The phase-isolated tests run the product both in the library's deterministic mode (sg2hip.deterministic: fixed-
-order reductions, so a result is a function of the code and the fixture; tests/test_deterministic_gpu.py checks two
-runs bitwise equal) and in its default atomic mode, the arithmetic bench.py times.
+The phase-isolated tests run the product in its production arithmetic, the library's deterministic mode
+(sg2hip.deterministic, the training iteration's default: fixed-order reductions, so a result is a function of the code
+and the fixture -- tests/test_deterministic_gpu.py checks two runs bitwise equal -- and bitwise the arithmetic bench.py
+times).
 """
 import re
 
@@ -88,18 +89,20 @@ def _iso(tag):
 
 
 # The product is judged in the arithmetic the bench times and in the library's other f32 arithmetic:
-#   'det'    the production split-bf16 products (S3, conv.hip) in deterministic mode (fixed-order slot reductions);
-#   'atomic' the same kernels with their float atomics (the default, timed mode: split-K partials, weight-gradient
-#            pixel splits, dot reductions) -- its result moves with the atomics' order at f32 rounding size;
+#   'det'    the production arithmetic: the split-bf16 products (S3, conv.hip) with the library's fixed-order slot
+#            reductions -- the training iteration's default since round 6 (training/trainer.py
+#            Trainer(deterministic=True)), so the judged result is bitwise the one bench.py times, and a function of
+#            the code and the fixture alone;
 #   'exact'  the f32-input MFMA kernels (SG2_F32_EXACT=1), a diagnostic A/B switch that nothing in training or the
 #            bench selects.
-# 'det' and 'atomic' are held to the full bound on every tensor: the bounds come from the reference's own f32
-# spread (the fixture's reference run and its re-evaluations, config_parity._conditioning) and nothing else.
-# 'exact' is held to the phase-level checks (flat vector, statistics, pl_mean) and its per-tensor ratios are
-# recorded: measured r05, C4 Gmain b64.conv1.noise_strength at 4.55e-3 of float64 = 1.2 x its bound (3 x the
-# phase's worst reference spread), every other tensor of the 4 configs within bounds.
-F32_ARITH = ['det', 'atomic', 'exact']
-
+# 'det' is held to the full bound on every tensor: the bounds come from the reference's own f32 spread (the fixture's
+# reference run and its re-evaluations, config_parity._conditioning) and nothing else.  'exact' is held to the
+# phase-level checks (flat vector, statistics, pl_mean) and its per-tensor ratios are recorded.
+# The float-atomic reductions (Trainer(deterministic=False), an A/B mode since round 6) are not judged here: their
+# result moves with the atomics' order: at C4 the Gmain flat measure of four atomic runs spread over 7.6e-5 .. 1.2e-4
+# (1.5e-4 on the round-5 driver box) against one deterministic run's 6.1e-5 -- the noise-strength and weight
+# gradients are near-cancelling sums over every pixel (tools/atomic_attr.py, profiles/r06a_attr_c4.log).
+F32_ARITH = ['det', 'exact']
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize('arith', F32_ARITH)
@@ -110,8 +113,8 @@ def test_f32_phases_vs_reference(tag, arith):
     in the phase) of float64; every tensor the reference gets to 1e-4 within 3e-4 of the reference's f32 result
     itself; each phase's flat vector within max(1e-4, 3 x the reference's); statistics and pl_mean likewise."""
     cfg, inp, tape, fix = _iso(tag)
-    got, stats = cp.run_product(cfg, inp, tape, DEV, aug_p=cfg['aug_p'], isolated=True,
-                                deterministic=arith != 'atomic', f32_exact=arith == 'exact')
+    got, stats = cp.run_product(cfg, inp, tape, DEV, aug_p=cfg['aug_p'], isolated=True, deterministic=True,
+                                f32_exact=arith == 'exact')
     cp.save_summary(f'{tag}_iso_f32_{arith}', got)
     worst, ratios = cp.judge_f32(got, fix, factor=F32_FACTOR, group_factor=F32_GROUP_FACTOR, groups=('grad/',),
                                  check=False)
@@ -125,7 +128,7 @@ def test_f32_phases_vs_reference(tag, arith):
     cp.judge_stats_f32(stats, fix)
     cp.judge_pl_mean(got, fix)
     cp.judge_flat(flat, ref_flat, floor=1e-4)
-    if arith != 'exact':     # the production arithmetic, per tensor
+    if arith == 'det':       # the production arithmetic, per tensor
         cp.judge_vs_reference(got, fix, factor=F32_FACTOR)
         cp.judge_f32(got, fix, factor=F32_FACTOR, group_factor=F32_GROUP_FACTOR, groups=('grad/',))
 
@@ -151,7 +154,7 @@ def test_f32_phases_vs_reference(tag, arith):
 # Dreg norm vector over the fixture state and six 2^-12 states: product 0.0042 .. 0.0416, median 0.0148; emulation
 # 0.0039 .. 0.0240, median 0.0136 -- with four states the emulation's largest was 0.0168;
 # profiles/r05_same_state16.txt).
-# Run in deterministic mode and with the float atomics the bench times.
+# Run in the production arithmetic (deterministic reductions, the bench's).
 EMU_FACTOR = 2.0
 ISO16_FLOOR = {'fp16': 5e-3, 'bf16': 1e-2}
 EMU_KEY = {'fp16': 'q16', 'bf16': 'qbf'}
@@ -174,10 +177,9 @@ def _same_states(fix, dt):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize('det', [True, False], ids=['det', 'atomic'])
 @pytest.mark.parametrize('tag,dt', [('c1', 'fp16'), ('c1', 'bf16'), ('c2', 'fp16'), ('c2', 'bf16'), ('c4', 'fp16'),
                                     ('c5', 'bf16')])
-def test_16bit_phases(tag, dt, det):
+def test_16bit_phases(tag, dt, det=True):
     cfg, inp, tape, fix = _iso(tag)
     assert any(k.startswith(EMU_KEY[dt] + '/') for k in fix), \
         f'train_{tag}_iso.npz has no {EMU_KEY[dt]}/ summaries (make_golden.py emu:{tag}_iso:{dt})'

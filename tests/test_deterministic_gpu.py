@@ -51,8 +51,9 @@ def test_det_layer_bwd(dtype, shape):
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize('shape', [(2, 64, 20, 33, 96), (9, 64, 128, 256, 64), (2, 512, 16, 16, 512)])
 def test_det_conv3x3_dot_and_wgrad(dtype, shape):
-    """16-bit 3x3: the dot epilogue (generic halo kernel; the persistent C = 64 shape, whose wave atomics the
-    deterministic mode routes to the halo kernel) and the LDS-DMA weight gradient, plain and scaled."""
+    """16-bit 3x3: the dot epilogue (generic halo kernel: per-tile slots; the persistent C = 64 shape, 9 samples
+    over 256 workgroups so runs cross samples: per-(sample, workgroup, wave) slots) and the LDS-DMA weight
+    gradient, plain and scaled."""
     from torch_utils.ops import conv2d_gradfix as cg
     N, Cin, H, W, Cout = shape
     g = torch.Generator().manual_seed(4)
