@@ -8,6 +8,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, 'gan-track_amd'), ROOT]
 from torch_utils.ops import conv2d_gradfix as cg  # noqa: E402
+import sg2hip  # noqa: E402
 
 dev = torch.device('cuda', 0)
 CL = torch.channels_last
@@ -30,8 +31,11 @@ for (n, c, h) in [(32, 64, 256), (32, 128, 128), (32, 256, 64), (32, 512, 32)]:
     dy, y, cc = mk(), mk(), mk()
     d = torch.rand(n, c, device=dev) + 0.5
     for with_c in (True, False):
-        fn = lambda: cg.layer_bwd(dy, y, cc if with_c else None, d, act=1, gain=1.41, clamp=256.0,
-                                  want_dd=with_c, want_dnoise=with_c)
-        t = timeit(fn)
-        nbytes = dy.numel() * 2 * (4 if with_c else 3)
-        print(f'N={n} C={c} {h}^2 c={with_c}: {t * 1e3:.1f} us, {nbytes / t / 1e9:.2f} TB/s', flush=True)
+        for det in (False, True):
+            fn = lambda: cg.layer_bwd(dy, y, cc if with_c else None, d, act=1, gain=1.41, clamp=256.0,
+                                      want_db=True, want_dd=with_c, want_dnoise=with_c)
+            with sg2hip.deterministic(det):
+                t = timeit(fn)
+            nbytes = dy.numel() * 2 * (4 if with_c else 3)
+            print(f'form={os.environ.get("SG2_LB_FORM", "0")} N={n} C={c} {h}^2 c={with_c} det={det}: {t * 1e3:.1f} us, '
+                  f'{nbytes / t / 1e9:.2f} TB/s', flush=True)
