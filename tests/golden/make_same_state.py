@@ -7,7 +7,9 @@ evaluations, as make_golden.py's emu16p step makes them):
 
 Each seed writes $GOLD_CACHE/p<k>_<tag>_{f64,<dt>}_<seed>.npz (make_golden.py gen_emulated16_perturbed's format);
 --merge folds every cached sample of <tag> into tests/golden/train_<tag>.npz as 'f64p<k>s<seed>/' and
-'q16p<k>s<seed>/' / 'qbfp<k>s<seed>/' (make_golden.py merge_emulated16_perturbed)."""
+'q16p<k>s<seed>/' / 'qbfp<k>s<seed>/' (make_golden.py merge_emulated16_perturbed), keeping the fixture's other
+samples.  A state whose float64 answer the fixture already holds is not re-evaluated (C2's fp16 samples reuse the
+float64 answers made with its bf16 ones)."""
 import os
 import re
 import sys
@@ -29,7 +31,11 @@ def gen(tag, dt, seed, k):
         if os.path.exists(fn):
             continue
         with np.load(os.path.join(OUT, f'train_{tag}.npz'), allow_pickle=False) as f:
-            cfg, inp, tape, _ = cp.load_fixture(f)
+            cfg, inp, tape, fix = cp.load_fixture(f)
+        pre = {'f64': 'f64', 'fp16': 'q16', 'bf16': 'qbf'}[d] + f'p{k}s{seed}/'
+        if any(kk.startswith(pre) for kk in fix):
+            print(tag, d, k, seed, 'already in the fixture', flush=True)
+            continue
         out, _ = cp.run_oracle_f64(cfg, inp, tape, cfg.get('aug_p', 0.3), perturb=2.0 ** -k, perturb_seed=int(seed),
                                    isolated=cfg.get('isolated', False),
                                    emu16=None if d == 'f64' else {'fp16': torch.float16, 'bf16': torch.bfloat16}[d])
@@ -44,13 +50,13 @@ def merge(tag):
     path = os.path.join(OUT, f'train_{tag}.npz')
     with np.load(path, allow_pickle=False) as f:
         z = unpack(f)
-    z = {kk: v for kk, v in z.items() if not re.match(r'(f64|q16|qbf)p\d+s\d+/', kk)}
     n = 0
     for fn in sorted(glob.glob(os.path.join(CACHE, f'p*_{tag}_*.npz'))):
         m = re.match(r'p(\d+)_' + re.escape(tag) + r'_(f64|fp16|bf16)_(\d+)\.npz$', os.path.basename(fn))
         if not m:
             continue
         pre = {'f64': 'f64', 'fp16': 'q16', 'bf16': 'qbf'}[m.group(2)] + f'p{m.group(1)}s{m.group(3)}'
+        z = {kk: v for kk, v in z.items() if not kk.startswith(pre + '/')}      # (a cached sample replaces its own)
         with np.load(fn, allow_pickle=False) as f:
             z.update({f'{pre}/{kk}': v for kk, v in unpack(f).items()})
         n += 1
