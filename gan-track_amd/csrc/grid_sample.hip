@@ -61,15 +61,15 @@ __device__ __forceinline__ Corners corners_g(float gx, float gy, int Hi, int Wi)
 
 template <typename T>
 __global__ __launch_bounds__(256) void grid_sample_fwd_kernel(GSParams p) {
-    const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
+    const unsigned total = (unsigned)p.N * p.Ho * p.Wo;       // (host-checked < 2^31: 32-bit index math)
     const T* in = (const T*)p.in;
     T* out = (T*)p.out;
     const int Hi = p.dyn_hw ? p.dyn_hw[0] : p.Hi, Wi = p.dyn_hw ? p.dyn_hw[1] : p.Wi;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int ox = (int)(idx % p.Wo);
-        const int oy = (int)((idx / p.Wo) % p.Ho);
-        const int n = (int)(idx / ((int64_t)p.Wo * p.Ho));
+    for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+        const unsigned r = idx / (unsigned)p.Wo;
+        const int ox = (int)(idx - r * (unsigned)p.Wo);
+        const int n = (int)(r / (unsigned)p.Ho);
+        const int oy = (int)(r - (unsigned)n * (unsigned)p.Ho);
         const Corners k = corners(p, n, oy, ox, Hi, Wi);
         const bool vx0 = k.x0 >= 0 && k.x0 < Wi, vx1 = k.x0 + 1 >= 0 && k.x0 + 1 < Wi;
         const bool vy0 = k.y0 >= 0 && k.y0 < Hi, vy1 = k.y0 + 1 >= 0 && k.y0 + 1 < Hi;
@@ -87,15 +87,15 @@ __global__ __launch_bounds__(256) void grid_sample_fwd_kernel(GSParams p) {
 
 template <typename T>
 __global__ __launch_bounds__(256) void grid_sample_bwd_kernel(GSParams p) {
-    const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
+    const unsigned total = (unsigned)p.N * p.Ho * p.Wo;
     const T* gout = (const T*)p.in;   // gradient w.r.t. output (layout os_*)
     float* gin = (float*)p.out;       // gradient w.r.t. input  (layout is_*)
     const int Hi = p.dyn_hw ? p.dyn_hw[0] : p.Hi, Wi = p.dyn_hw ? p.dyn_hw[1] : p.Wi;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int ox = (int)(idx % p.Wo);
-        const int oy = (int)((idx / p.Wo) % p.Ho);
-        const int n = (int)(idx / ((int64_t)p.Wo * p.Ho));
+    for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+        const unsigned r = idx / (unsigned)p.Wo;
+        const int ox = (int)(idx - r * (unsigned)p.Wo);
+        const int n = (int)(r / (unsigned)p.Ho);
+        const int oy = (int)(r - (unsigned)n * (unsigned)p.Ho);
         const Corners k = corners(p, n, oy, ox, Hi, Wi);
         const bool vx0 = k.x0 >= 0 && k.x0 < Wi, vx1 = k.x0 + 1 >= 0 && k.x0 + 1 < Wi;
         const bool vy0 = k.y0 >= 0 && k.y0 < Hi, vy1 = k.y0 + 1 >= 0 && k.y0 + 1 < Hi;
@@ -121,14 +121,14 @@ template <typename T>
 __global__ __launch_bounds__(256) void grid_sample_bwd_gather_kernel(GSParams p) {
     const int Hi = p.dyn_hw ? p.dyn_hw[0] : p.Hi, Wi = p.dyn_hw ? p.dyn_hw[1] : p.Wi;
     const int hl = p.dyn_hw ? min(p.Hi, Hi + 96) : p.Hi, wl = p.dyn_hw ? min(p.Wi, Wi + 96) : p.Wi;
-    const int64_t total = (int64_t)p.N * hl * wl;
+    const unsigned total = (unsigned)p.N * hl * wl;
     const T* gout = (const T*)p.in;
     float* gin = (float*)p.out;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int X = (int)(idx % wl);
-        const int Y = (int)((idx / wl) % hl);
-        const int n = (int)(idx / ((int64_t)wl * hl));
+    for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+        const unsigned r = idx / (unsigned)wl;
+        const int X = (int)(idx - r * (unsigned)wl);
+        const int n = (int)(r / (unsigned)hl);
+        const int Y = (int)(r - (unsigned)n * (unsigned)hl);
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
         if (X < Wi && Y < Hi) {
             float t[6];
@@ -262,6 +262,7 @@ int gs_fwd(void* out, const void* in, const float* grid, const float* theta, int
     if (fill(p, in_size, in_stride, out_size, out_stride)) return -1;
     const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
     if (total == 0 || p.C == 0) return 0;
+    SG2_CHECK(total < INT32_MAX && (int64_t)p.N * p.Hi * p.Wi < INT32_MAX, "sg2_grid_sample_fwd: too many pixels");
     const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 32);
     SG2_DISPATCH(dtype, T, { grid_sample_fwd_kernel<T><<<g, 256, 0, as_stream(stream)>>>(p); });
     return launch_status("sg2_grid_sample_fwd");
@@ -291,6 +292,7 @@ int gs_bwd(float* gin, const void* gout, const float* grid, const float* theta, 
     }
     const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
     if (total == 0 || p.C == 0) return 0;
+    SG2_CHECK(total < INT32_MAX && (int64_t)p.N * p.Hi * p.Wi < INT32_MAX, "sg2_grid_sample_bwd: too many pixels");
     if (det_on() && theta) {
         SG2_CHECK(p.C <= 4, "sg2_affine_grid_sample_bwd: deterministic mode supports C <= 4");
         const int64_t tot_in = (int64_t)p.N * p.Hi * p.Wi;

@@ -1499,6 +1499,14 @@ def test_conv3x3_c64_ring(dtype, shape, form, ring, monkeypatch):
     assert rel_err(y.float()[..., edge], ref[..., edge]) < 2 * tol
 
 
+@pytest.mark.parametrize('form', ['mod_epi_raw', 'plain'])
+def test_conv3x3_c64_ring_no_dynamic_tail(form, monkeypatch):
+    """The default ring form (49) on a shape whose dynamic tail has no plan: 16 samples divide the
+    2 x 256 workgroups, but each sample's 27 x 11 = 297 tiles leave an odd remainder after any even number of static
+    tiles per workgroup, so the launch takes the static form 46 instead of failing."""
+    test_conv3x3_c64_ring(torch.float16, (16, 108, 352), form, '49', monkeypatch)
+
+
 @pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize('shape', [(4, 256, 256), (3, 344, 320), (2, 512, 256), (5, 104, 512)])
 @pytest.mark.parametrize('form', ['mod_epi_raw', 'mod_epi', 'mod_only', 'plain_epi', 'plain', 'epi_no_noise'])
