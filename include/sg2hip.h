@@ -179,8 +179,10 @@ void sg2_set_clean_workspace(int on);
  * by writing each contribution to a slot of the scratch and summing the slots in a fixed order, so results
  * are bitwise reproducible.  Calls made while it is on must be stream-ordered (they share the scratch); a call
  * whose partial sums do not fit returns -1 ("deterministic scratch too small").  The explicit-grid
- * sg2_grid_sample_bwd keeps its atomics (only the affine form has the gather used here).  Test / audit mode:
- * slower (extra passes over the partial sums). */
+ * sg2_grid_sample_bwd keeps its atomics (only the affine form has the gather used here).  Since round 6 this is
+ * the training iteration's default arithmetic (Trainer(deterministic=True) registers a 2 GiB scratch around every
+ * phase's forward and backward): the slot reductions (per-tile dot slots, split sums folded into the split-K
+ * finalize, one-launch det_sum) measured faster than the float atomics on the bench step. */
 void sg2_set_deterministic(void* scratch, int64_t bytes);
 
 /* Stride-2 / pad-0 form of sg2_conv3x3 (conv2d_resample.py:139-142 with down = 2: the discriminator's
