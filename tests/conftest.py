@@ -20,7 +20,7 @@ def pytest_configure(config):
 # Unit-level files first, whole-iteration files last: a failure under -x then stops the run after the kernel
 # tests have reported, not before them.
 _ORDER = ['test_capi', 'test_oracle_golden', 'test_loss_host', 'test_trainer_shell', 'test_dist_gloo', 'test_ops_gpu',
-          'test_deterministic_gpu', 'test_train_gpu', 'test_trainer_gpu', 'test_training_loop_gpu', 'test_config_gpu']
+          'test_deterministic_gpu', 'test_train_gpu', 'test_trainer_gpu', 'test_training_loop_gpu', 'test_bench_gpu', 'test_config_gpu']
 
 
 def _rank(item):
