@@ -11,6 +11,8 @@ import torch
 import dnnlib
 import sg2hip as _hip
 
+from . import staged_sum
+
 activation_funcs = {
     'linear': dnnlib.EasyDict(def_alpha=0, def_gain=1, cuda_idx=1, ref='', has_2nd_grad=False),
     'relu': dnnlib.EasyDict(def_alpha=0, def_gain=np.sqrt(2), cuda_idx=2, ref='y', has_2nd_grad=False),
@@ -83,7 +85,7 @@ def _bias_act_fn(dim, act, alpha, gain, clamp):
             if spec.has_2nd_grad and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]):
                 d_x = _launch(d_dx, b, x, y, dy, 2, dim, spec, alpha, gain, clamp)
             if spec.has_2nd_grad and ctx.needs_input_grad[2]:
-                d_b = d_x.sum([i for i in range(d_x.ndim) if i != dim])
+                d_b = staged_sum.staged_sum(d_x, [i for i in range(d_x.ndim) if i != dim])
             return d_dy, d_x, d_b, None
 
     class BiasAct(torch.autograd.Function):
@@ -109,7 +111,7 @@ def _bias_act_fn(dim, act, alpha, gain, clamp):
             if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
                 dx = dy if trivial else BiasActGrad.apply(dy, x, b, y)
             if ctx.needs_input_grad[1]:
-                db = dx.sum([i for i in range(dx.ndim) if i != dim])
+                db = staged_sum.staged_sum(dx, [i for i in range(dx.ndim) if i != dim])
             return dx, db
 
     BiasAct.Grad = BiasActGrad

@@ -4,6 +4,8 @@ Used for the demodulation + noise epilogue of the modulated convolution
 (networks_stylegan2.py:71-72)."""
 import torch
 
+from .staged_sum import staged_sum
+
 
 def fma(a, b, c):  # => a * b + c
     return _FMA.apply(a, b, c)
@@ -15,7 +17,7 @@ def _sum_to(x, shape):
     assert lead >= 0
     dims = [d for d in range(x.ndim) if x.shape[d] > 1 and (d < lead or shape[d - lead] == 1)]
     if dims:
-        x = x.sum(dim=dims, keepdim=True)
+        x = staged_sum(x, dims, keepdim=True)
     if lead:
         x = x.reshape(-1, *x.shape[lead + 1:])
     assert tuple(x.shape) == tuple(shape)

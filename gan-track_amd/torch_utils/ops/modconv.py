@@ -26,6 +26,7 @@ import torch
 
 from . import bias_act as _ba
 from . import conv2d_gradfix as _cg
+from . import staged_sum as _ss
 from . import upfirdn2d as _up
 
 _CL = torch.channels_last
@@ -57,6 +58,16 @@ def _halo(x, kh, kw, stride, pad):
 
 def _f32(t):
     return t.float().contiguous() if t is not None else None
+
+
+def _sum_hw(t):
+    """t.sum([2, 3], dtype=float32) as [N, C] without torch's split reduction (staged_sum.py)."""
+    return _ss.staged_sum(t, (2, 3), dtype=torch.float32)
+
+
+def _sum_nhw(t):
+    """t.sum([0, 2, 3], dtype=float32) (a bias gradient) without torch's split reduction (staged_sum.py)."""
+    return _ss.staged_sum(t, (0, 2, 3), dtype=torch.float32)
 
 
 def _mul(a, s):
@@ -285,7 +296,7 @@ class _LayerVJP(torch.autograd.Function):
                                          clamp=clamp, want_db=False, want_dd=want_dd, want_dnoise=False)
         else:   # narrow outputs (toRGB)
             dz = _ba.bias_act_grad(dy.to(dt), zsrc, act=_ACT[act], alpha=alpha, gain=gain, clamp=clamp)
-            dd = (dz * c).sum([2, 3], dtype=torch.float32) if want_dd else None
+            dd = _sum_hw(dz * c) if want_dd else None
             dc = _cg._nhwc(dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if d32 is not None else dz)
         dx, dxs, ds = _conv_any(dc, weight, cin, h, w, stride, pad, True, wgain, out_scale=s32,
                                 dot_src=xk if want_ds else None, want_raw=s32 is not None)
@@ -382,8 +393,8 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
                                        clamp=clamp, want_db=want_db, want_dd=want_dd, want_dnoise=want_dn, acc=lb)
     else:   # narrow outputs (toRGB): plain kernels
         dz = _ba.bias_act_grad(dy, zsrc, act=_ACT[act], alpha=alpha, gain=gain, clamp=clamp)
-        db = dz.sum([0, 2, 3], dtype=torch.float32) if want_db else None
-        dd = (dz * c).sum([2, 3], dtype=torch.float32) if want_dd else None
+        db = _sum_nhw(dz) if want_db else None
+        dd = _sum_hw(dz * c) if want_dd else None
         dn = dz.sum(1, keepdim=True, dtype=torch.float32) if want_dn else None
         dc = _cg._nhwc(dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None else dz)
     dx, ds, dw = _scaled_input_grads(dc, x, styles, weight, need[0], need[1], need[2], stride, pad, wgain,
@@ -412,7 +423,7 @@ def _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c
     # be computed and discarded, and -- being differentiable -- add their own double-backward nodes.
     param_grads = not _cg.weight_gradients_disabled
     if need[5] and bias is not None and param_grads:
-        db = dz.sum([0, 2, 3], dtype=torch.float32).to(bias.dtype)
+        db = _sum_nhw(dz).to(bias.dtype)
     if need[4] and noise is not None and param_grads:
         dnoise = dz.sum(1, keepdim=True, dtype=torch.float32).to(noise.dtype)
     s_ = styles.to(dt).reshape(n, -1, 1, 1) if styles is not None else None
@@ -548,7 +559,7 @@ class UpModConv(torch.autograd.Function):
             dz = _ba.bias_act_grad(dy, y, act='lrelu', alpha=alpha, gain=gain, clamp=clamp)
             param_grads = not _cg.weight_gradients_disabled      # see _composed_backward
             if need[5] and bias is not None and param_grads:
-                db = dz.sum([0, 2, 3], dtype=torch.float32)
+                db = _sum_nhw(dz)
             if need[4] and noise is not None and param_grads:
                 dn = dz.sum(1, keepdim=True, dtype=torch.float32)
             s_ = styles.to(dt).reshape(n, -1, 1, 1)

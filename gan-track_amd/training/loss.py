@@ -11,6 +11,7 @@ import torch
 
 from torch_utils import training_stats
 from torch_utils.ops import conv2d_gradfix
+from torch_utils.ops.staged_sum import staged_sum
 from torch_utils.ops import upfirdn2d
 from training.networks_stylegan2 import MinibatchStdLayer
 
@@ -184,8 +185,9 @@ class StyleGAN2Loss(Loss):
             img, ws = self.run_G(z[:n], c[:n])
             y = torch.randn_like(img) / np.sqrt(img.shape[2] * img.shape[3])
             with conv2d_gradfix.no_weight_gradients(self.pl_no_weight_grad):
-                jty, = torch.autograd.grad(outputs=[(img * y).sum()], inputs=[ws], create_graph=True,
-                                           only_inputs=True)
+                # staged: torch's split form of this 1M-value sum issues a memset into the phase graph (staged_sum.py)
+                jty, = torch.autograd.grad(outputs=[staged_sum(img * y, range(img.ndim))], inputs=[ws],
+                                           create_graph=True, only_inputs=True)
             lengths = jty.square().sum(2).mean(1).sqrt()
             a = self.pl_mean.lerp(lengths.mean(), self.pl_decay)
             self.pl_mean.copy_(a.detach())

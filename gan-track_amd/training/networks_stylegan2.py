@@ -25,6 +25,7 @@ from torch_utils.ops import conv2d_gradfix
 from torch_utils.ops import conv2d_resample
 from torch_utils.ops import fma
 from torch_utils.ops import modconv
+from torch_utils.ops import staged_sum
 from torch_utils.ops import upfirdn2d
 
 _CL = torch.channels_last
@@ -505,9 +506,10 @@ class SynthesisLayer(torch.nn.Module):
             styles = self.affine(w)
         noise = None
         if self.use_noise and noise_mode == 'random':
-            noise = torch.randn([x.shape[0], 1, self.resolution, self.resolution], device=x.device) * self.noise_strength
+            noise = staged_sum.scale_by_scalar(torch.randn([x.shape[0], 1, self.resolution, self.resolution],
+                                                           device=x.device), self.noise_strength)
         if self.use_noise and noise_mode == 'const':
-            noise = self.noise_const * self.noise_strength
+            noise = staged_sum.scale_by_scalar(self.noise_const, self.noise_strength)
         up_fused = self.up == 2 and modconv.supported_up(x, self.weight, self.resample_filter)
         if self.activation == 'lrelu' and (up_fused or (self.up == 1 and modconv.supported_generic(x, self.weight))):
             # one-kernel modulated conv + demod + noise + bias + lrelu + clamp (sg2_conv3x3 / sg2_conv2d_fused)
