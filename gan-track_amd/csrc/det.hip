@@ -9,6 +9,9 @@
 // second adds the chunk sums in chunk order.
 #include "sg2_common.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace sg2 {
 namespace {
 
@@ -54,6 +57,8 @@ hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t 
     const int64_t bx = cdiv(n, kLanes);
     // few outputs over a long sum (a bias or dot reduction over every pixel block): first chunks of the s range in
     // parallel into a temporary, then their sums in chunk order (both steps fixed by the shapes alone)
+    static const bool trace = getenv("SG2_DET_TRACE") != nullptr;   // diagnostics: one line per call (tools/)
+    const int64_t S0 = S;
     int64_t K = 1;
     if (bx * G < 512 && S > 16 * kRows) K = std::min<int64_t>(std::min<int64_t>(cdiv(S, 16 * kRows), 1024),
                                                               cdiv(512, bx * G));
@@ -74,6 +79,8 @@ hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t 
             S = K;
         }
     }
+    if (trace) fprintf(stderr, "DETSUM G=%d n=%lld S=%lld K=%lld\n", G, (long long)n, (long long)S0,
+                       (long long)K);
     det_sum_kernel<<<dim3((unsigned)bx, (unsigned)G, 1), 256, 0, st>>>(out, go, ws, gw, ss, S, n, S, 0, 0);
     return hipGetLastError();
 }

@@ -223,17 +223,18 @@ __global__ __launch_bounds__(256) void reflect_pad_adj_kernel(float* gx, const f
     }
 }
 
-// Zero rows < dyn_h + band and cols < dyn_w + band of the [N, C, Hi, Wi] gradient buffer (strides is_*).
+// Zero rows < dyn_h + band and cols < dyn_w + band of the [N, C, Hi, Wi] gradient buffer (strides is_*): the grid
+// strides over the region only (32-bit index math; the region of the static buffer is < 2^31 elements).
 __global__ __launch_bounds__(256) void zero_region_kernel(float* g, GSParams p, const int* dyn_hw, int band) {
     const int hl = min(p.Hi, dyn_hw[0] + band), wl = min(p.Wi, dyn_hw[1] + band);
-    const int64_t total = (int64_t)p.N * p.C * p.Hi * p.Wi;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int x = (int)(i % p.Wi);
-        const int y = (int)((i / p.Wi) % p.Hi);
-        const int64_t nc = i / ((int64_t)p.Wi * p.Hi);
-        if (y >= hl || x >= wl) continue;
-        const int c = (int)(nc % p.C), n = (int)(nc / p.C);
-        g[n * p.is_n + c * p.is_c + y * p.is_h + x * p.is_w] = 0.f;
+    const unsigned total = (unsigned)p.N * p.C * hl * wl;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const unsigned r = i / (unsigned)wl;
+        const int x = (int)(i - r * (unsigned)wl);
+        const unsigned nc = r / (unsigned)hl;
+        const int y = (int)(r - nc * (unsigned)hl);
+        const int c = (int)(nc % (unsigned)p.C), n = (int)(nc / (unsigned)p.C);
+        g[n * p.is_n + c * p.is_c + (int64_t)y * p.is_h + (int64_t)x * p.is_w] = 0.f;
     }
 }
 
@@ -278,9 +279,14 @@ int gs_bwd(float* gin, const void* gout, const float* grid, const float* theta, 
     // zero the float32 input-gradient buffer (dense over the strided extent)
     const int64_t extent = (p.N - 1) * p.is_n + (p.C - 1) * p.is_c + (p.Hi - 1) * p.is_h + (p.Wi - 1) * p.is_w + 1;
     hipStream_t s = as_stream(stream);
-    if (dyn_hw) {
+    const bool gather = det_on() && theta;
+    if (dyn_hw && gather) {
+        // the deterministic gather writes every element of the region below (its band included): no zeroing
+        SG2_CHECK(p.C <= 4, "sg2_affine_grid_sample_bwd: deterministic mode supports C <= 4");
+    } else if (dyn_hw) {
         // only the region a consumer of the dynamically sized gradient reads: the logical image plus a
         // band (upfirdn2d.hip kZeroBand and the adjoint FIR's reach)
+        SG2_CHECK((int64_t)p.N * p.C * p.Hi * p.Wi < INT32_MAX, "sg2_grid_sample_bwd: gradient buffer too large");
         const int64_t tot = (int64_t)p.N * p.C * p.Hi * p.Wi;
         const int g = (int)std::min<int64_t>(cdiv(tot, 256), 256 * 64);
         zero_region_kernel<<<g, 256, 0, s>>>(gin, p, dyn_hw, 96);
@@ -293,7 +299,7 @@ int gs_bwd(float* gin, const void* gout, const float* grid, const float* theta, 
     const int64_t total = (int64_t)p.N * p.Ho * p.Wo;
     if (total == 0 || p.C == 0) return 0;
     SG2_CHECK(total < INT32_MAX && (int64_t)p.N * p.Hi * p.Wi < INT32_MAX, "sg2_grid_sample_bwd: too many pixels");
-    if (det_on() && theta) {
+    if (gather) {
         SG2_CHECK(p.C <= 4, "sg2_affine_grid_sample_bwd: deterministic mode supports C <= 4");
         const int64_t tot_in = (int64_t)p.N * p.Hi * p.Wi;
         const int gi = (int)std::min<int64_t>(cdiv(tot_in, 256), 256 * 64);

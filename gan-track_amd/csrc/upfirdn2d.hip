@@ -114,48 +114,157 @@ __global__ __launch_bounds__(256) void upfirdn_generic(UpfParams p) {
     }
 }
 
+// Tap geometry along one axis with the up / down factors known at compile time (0: runtime, axis_taps).
+template <int UP, int DOWN>
+__device__ __forceinline__ void axis_taps_c(int o, int down, int pad0, int up, int& t0, int& i0) {
+    if (UP == 1 && DOWN != 0) { t0 = 0; i0 = o * DOWN - pad0; }
+    else if (UP == 2 && DOWN != 0) { const int z = o * DOWN - pad0; t0 = z & 1; i0 = (z + t0) >> 1; }
+    else axis_taps(o, down, pad0, up, t0, i0);
+}
+
 // One separable pass (filter along x only, or along y only; the other axis is the identity): the two
 // launches of every 1-D-filter upfirdn2d (upfirdn2d.py:190-193), e.g. the ADA pipe's 12-tap sym6
-// up/down-sampling of single-channel images.  A workgroup owns 256 consecutive outputs of one output
-// row, so all index math is 32-bit and per-row terms (the vertical tap window, the lim test) are
-// uniform; reads are coalesced along x and the horizontal pass's neighbouring taps hit L1.
-template <typename T, bool HORIZ, int KT>
+// up/down-sampling of single-channel images.  The grid strides over (output row, 256-column tile) pairs
+// inside the computed extent (with a device-side lim the skipped part of the static buffer costs no
+// workgroups); the pair index is uniform, its decode 32-bit scalar math.  UP / DOWN: the pass's factors when
+// known at compile time (the ADA pipe's up-2 and down-2 passes), which turns the per-lane tap geometry into
+// shifts.  Reads are coalesced along x and the horizontal pass's neighbouring taps hit L1.
+template <typename T, bool HORIZ, int KT, int UP, int DOWN>
 __global__ __launch_bounds__(256) void upfirdn_1d(UpfParams p) {
     // KT: taps per output (ceil(F / up)), unrolled so all of a lane's loads are in flight together.
-    // The grid strides over (row, 256-column tile) pairs inside the computed extent: with a device-side
-    // lim the skipped part of the static buffer costs no workgroups.
     __shared__ float sf[64];
     const int F = HORIZ ? p.fw : p.fh;
     for (int t = threadIdx.x; t < F; t += 256) sf[t] = p.f[p.flip ? t : F - 1 - t] * p.gain;
     __syncthreads();
-    const int rows = p.lim ? min(p.OH, p.lim[0] + kZeroBand) : p.OH;
-    const int cols = p.lim ? min(p.OW, p.lim[1] + kZeroBand) : p.OW;
+    const int ly = p.lim ? p.lim[0] : p.OH, lx = p.lim ? p.lim[1] : p.OW;      // computed extent
+    const int rows = min(p.OH, ly + (p.lim ? kZeroBand : 0)), cols = min(p.OW, lx + (p.lim ? kZeroBand : 0));
     const int tiles = (cols + 255) / 256;
-    const int64_t total = (int64_t)p.N * p.C * rows * tiles;
-    for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
-        const int64_t row = b / tiles;
-        const int ox = (int)(b - row * tiles) * 256 + threadIdx.x;
-        const int oy = (int)(row % rows), nc = (int)(row / rows);
-        const int c = nc % p.C, n = nc / p.C;
+    const int total = p.N * p.C * rows * tiles;
+    const int up = HORIZ ? p.upx : p.upy, down = HORIZ ? p.downx : p.downy, L = HORIZ ? p.W : p.H;
+    for (int b = blockIdx.x; b < total; b += gridDim.x) {
+        const int row = b / tiles;
+        const int ox = (b - row * tiles) * 256 + threadIdx.x;
+        const int oy = row % rows, nc = row / rows;
         if (ox >= cols) continue;
+        const int c = nc % p.C, n = nc / p.C;
         T* yp = (T*)p.y + n * p.ys_n + c * p.ys_c + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w;
-        if (p.lim && (oy >= p.lim[0] || ox >= p.lim[1])) { *yp = (T)0.f; continue; }
+        if (oy >= ly || ox >= lx) { *yp = (T)0.f; continue; }
         const T* xb = (const T*)p.x + n * p.xs_n + c * p.xs_c;
         int t0, i0;
-        if (HORIZ) axis_taps(ox, p.downx, p.padx0, p.upx, t0, i0);
-        else axis_taps(oy, p.downy, p.pady0, p.upy, t0, i0);
-        const int up = HORIZ ? p.upx : p.upy, L = HORIZ ? p.W : p.H;
+        if (HORIZ) axis_taps_c<UP, DOWN>(ox, down, p.padx0, up, t0, i0);
+        else axis_taps_c<UP, DOWN>(oy, down, p.pady0, up, t0, i0);
         const T* xl = HORIZ ? xb + (int64_t)oy * p.xs_h : xb + (int64_t)ox * p.xs_w;
         const int64_t st = HORIZ ? p.xs_w : p.xs_h;
+        const int upk = UP ? UP : up;
         float acc = 0.f;
 #pragma unroll
         for (int k = 0; k < KT; ++k) {
-            const int t = t0 + k * up, i = i0 + k;
+            const int t = t0 + k * upk, i = i0 + k;
             const bool ok = t < F && i >= 0 && i < L;
             const float v = (float)xl[(int64_t)(ok ? i : 0) * st];
             acc += ok ? v * sf[t < F ? t : 0] : 0.f;
         }
         *yp = (T)acc;
+    }
+}
+
+// The horizontal pass with UP, DOWN in {1, 2}: a workgroup stages the input span of its 256 outputs of one row
+// (256 * DOWN / UP + KT values) in LDS with coalesced loads, then each lane reads its KT taps from LDS (the
+// global form issues KT strided loads per output: at DOWN = 2 each wave load spans twice the cache lines).
+template <typename T, int UP, int DOWN, int KT>
+__global__ __launch_bounds__(256) void upfirdn_1d_hlds(UpfParams p) {
+    constexpr int SPAN = (255 * DOWN + UP - 1) / UP + KT + 1;
+    __shared__ float sf[64];
+    __shared__ float sx[SPAN];
+    const int F = p.fw;
+    for (int t = threadIdx.x; t < F; t += 256) sf[t] = p.f[p.flip ? t : F - 1 - t] * p.gain;
+    const int ly = p.lim ? p.lim[0] : p.OH, lx = p.lim ? p.lim[1] : p.OW;      // computed extent
+    const int rows = min(p.OH, ly + (p.lim ? kZeroBand : 0)), cols = min(p.OW, lx + (p.lim ? kZeroBand : 0));
+    const int tiles = (cols + 255) / 256;
+    const int total = p.N * p.C * rows * tiles;
+    for (int b = blockIdx.x; b < total; b += gridDim.x) {
+        const int row = b / tiles;
+        const int ox0 = (b - row * tiles) * 256, ox = ox0 + threadIdx.x;
+        const int oy = row % rows, nc = row / rows;
+        const int c = nc % p.C, n = nc / p.C;
+        int tb, base;
+        axis_taps_c<UP, DOWN>(ox0, DOWN, p.padx0, UP, tb, base);                 // the span's first input
+        const T* xl = (const T*)p.x + n * p.xs_n + c * p.xs_c + (int64_t)oy * p.xs_h;
+        __syncthreads();                                                        // (the previous pair's reads)
+        for (int m = threadIdx.x; m < SPAN; m += 256) {
+            const int i = base + m;
+            sx[m] = (i >= 0 && i < p.W) ? (float)xl[(int64_t)i * p.xs_w] : 0.f;
+        }
+        __syncthreads();
+        if (ox >= cols) continue;
+        T* yp = (T*)p.y + n * p.ys_n + c * p.ys_c + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w;
+        if (oy >= ly || ox >= lx) { *yp = (T)0.f; continue; }
+        int t0, i0;
+        axis_taps_c<UP, DOWN>(ox, DOWN, p.padx0, UP, t0, i0);
+        const float* w = sx + (i0 - base);
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+            const int t = t0 + k * UP;
+            acc += t < F ? w[k] * sf[t] : 0.f;
+        }
+        *yp = (T)acc;
+    }
+}
+
+// The vertical pass with UP, DOWN in {1, 2}: a lane owns column ox and a run of R consecutive output rows.
+// The run reads SPAN input rows; each is loaded once and added to every output of the run it is a tap of
+// (tap k of output j is input row i0(j) + k; i0(j) - i0(0) and the first tap's index are uniform), in
+// increasing k per output as upfirdn_1d does: 2 loads per output instead of KT.  Grid-strided over
+// (run, column tile) pairs like upfirdn_1d.
+template <typename T, int UP, int DOWN, int KT, int R>
+__global__ __launch_bounds__(256) void upfirdn_1d_vrun(UpfParams p) {
+    constexpr int SPAN = ((R - 1) * DOWN + UP - 1) / UP + KT;
+    __shared__ float sf[64];
+    const int F = p.fh;
+    for (int t = threadIdx.x; t < F; t += 256) sf[t] = p.f[p.flip ? t : F - 1 - t] * p.gain;
+    __syncthreads();
+    const int ly = p.lim ? p.lim[0] : p.OH, lx = p.lim ? p.lim[1] : p.OW;      // computed extent
+    const int rows = min(p.OH, ly + (p.lim ? kZeroBand : 0)), cols = min(p.OW, lx + (p.lim ? kZeroBand : 0));
+    const int tiles = (cols + 255) / 256, runs = (rows + R - 1) / R;
+    const int total = p.N * p.C * runs * tiles;
+    for (int b = blockIdx.x; b < total; b += gridDim.x) {
+        const int run = b / tiles;
+        const int ox = (b - run * tiles) * 256 + threadIdx.x;
+        const int oy0 = (run % runs) * R, nc = run / runs;
+        if (ox >= cols) continue;
+        const int c = nc % p.C, n = nc / p.C;
+        const T* xb = (const T*)p.x + n * p.xs_n + c * p.xs_c + (int64_t)ox * p.xs_w;
+        T* yb = (T*)p.y + n * p.ys_n + c * p.ys_c + (int64_t)ox * p.ys_w;
+        int tj[R], dj[R], base = 0;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            int t0, i0;
+            axis_taps_c<UP, DOWN>(oy0 + j, DOWN, p.pady0, UP, t0, i0);
+            if (j == 0) base = i0;
+            tj[j] = t0;
+            dj[j] = i0 - base;
+        }
+        float acc[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc[j] = 0.f;
+#pragma unroll
+        for (int m = 0; m < SPAN; ++m) {
+            const int i = base + m;
+            const bool ok = i >= 0 && i < p.H;
+            const float v = (float)xb[(int64_t)(ok ? i : 0) * p.xs_h];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const int k = m - dj[j], t = tj[j] + k * UP;
+                if (k >= 0 && k < KT && t < F) acc[j] += ok ? v * sf[t] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const int oy = oy0 + j;
+            if (oy >= rows) break;
+            yb[(int64_t)oy * p.ys_h] = (oy >= ly || ox >= lx) ? (T)0.f : (T)acc[j];
+        }
     }
 }
 
@@ -655,15 +764,28 @@ int launch(const UpfParams& p, bool vec, hipStream_t s) {
     if (!vec && !p.epi) {
         const bool horiz = p.fh == 1 && p.upy == 1 && p.downy == 1 && p.pady0 == 0 && p.OH == p.H && p.fw <= 64;
         const bool vert = p.fw == 1 && p.upx == 1 && p.downx == 1 && p.padx0 == 0 && p.OW == p.W && p.fh <= 64;
-        const int64_t blocks = (int64_t)p.N * p.C * p.OH * cdiv(p.OW, 256);
-        const int up = horiz ? p.upx : p.upy, F = horiz ? p.fw : p.fh;
+        const int up = horiz ? p.upx : p.upy, down = horiz ? p.downx : p.downy, F = horiz ? p.fw : p.fh;
         const int kt = (F + up - 1) / up;
-        if ((horiz || vert) && kt <= 16 && (int64_t)p.N * p.C < INT32_MAX / 2) {
-            const unsigned g = (unsigned)std::min<int64_t>(blocks, 256 * 64);
-#define U1D(KT_) { if (horiz) upfirdn_1d<T, true, KT_><<<g, 256, 0, s>>>(p); \
-                   else upfirdn_1d<T, false, KT_><<<g, 256, 0, s>>>(p); }
-            if (kt <= 4) U1D(4) else if (kt <= 8) U1D(8) else U1D(16)
+        const int64_t pairs = (int64_t)p.N * p.C * p.OH * cdiv(p.OW, 256);
+        if ((horiz || vert) && kt <= 16 && pairs < INT32_MAX) {
+            const unsigned g = (unsigned)std::min<int64_t>(pairs, 256 * 64);
+            const bool ada_up = up == 2 && down == 1 && kt == 6, ada_down = up == 1 && down == 2 && kt == 12;
+            static const int vr = [] { const char* e = getenv("SG2_U1D_VRUN"); return e ? atoi(e) : 4; }();
+            static const bool hl = [] { const char* e = getenv("SG2_U1D_HLDS"); return e ? atoi(e) != 0 : true; }();
+            if (vert && vr == 4 && ada_up) upfirdn_1d_vrun<T, 2, 1, 6, 4><<<g, 256, 0, s>>>(p);
+            else if (vert && vr == 4 && ada_down) upfirdn_1d_vrun<T, 1, 2, 12, 4><<<g, 256, 0, s>>>(p);
+            else if (horiz && hl && ada_up) upfirdn_1d_hlds<T, 2, 1, 6><<<g, 256, 0, s>>>(p);
+            else if (horiz && hl && ada_down) upfirdn_1d_hlds<T, 1, 2, 12><<<g, 256, 0, s>>>(p);
+            else if (horiz && ada_up) upfirdn_1d<T, true, 6, 2, 1><<<g, 256, 0, s>>>(p);
+            else if (horiz && ada_down) upfirdn_1d<T, true, 12, 1, 2><<<g, 256, 0, s>>>(p);
+            else if (ada_up) upfirdn_1d<T, false, 6, 2, 1><<<g, 256, 0, s>>>(p);
+            else if (ada_down) upfirdn_1d<T, false, 12, 1, 2><<<g, 256, 0, s>>>(p);
+            else {
+#define U1D(KT_) { if (horiz) upfirdn_1d<T, true, KT_, 0, 0><<<g, 256, 0, s>>>(p); \
+                   else upfirdn_1d<T, false, KT_, 0, 0><<<g, 256, 0, s>>>(p); }
+                if (kt <= 4) U1D(4) else if (kt <= 8) U1D(8) else U1D(16)
 #undef U1D
+            }
             return launch_status("sg2_upfirdn2d");
         }
     }

@@ -95,6 +95,29 @@ def test_upfirdn2d_golden(name, fmt):
     assert rel_err(dx, z[f'{name}_dx']) < 1e-5
 
 
+@pytest.mark.parametrize('kw', [dict(up=2, padding=[6, 5, 6, 5]), dict(up=2, padding=[5, 4, 7, 3]),
+                                dict(down=2, padding=[-3, -2, -3, -4]), dict(down=2, padding=[2, 3, 1, 5]),
+                                dict(up=2, padding=[1, 2, 0, 3], flip_filter=True), dict(padding=[5, 6, 5, 6])])
+def test_upfirdn2d_separable_passes(kw):
+    """The 1-D passes of a separable (1-D) filter on f32 NCHW images (upfirdn_1d, and upfirdn_1d_vrun for the
+    vertical up-2 / down-2 passes of the 12-tap ADA filter: runs of 4 output rows, both pad parities), forward
+    and input gradient vs the oracle; several planes, ragged sizes (a partial last run and column tile)."""
+    from torch_utils.ops import upfirdn2d
+    torch.manual_seed(11)
+    f = torch.randn(12, dtype=torch.float64)
+    x = torch.randn(3, 2, 37, 301, dtype=torch.float64)
+    xd = x.float().to(DEV).requires_grad_(True)
+    y = upfirdn2d.upfirdn2d(xd, f.float().to(DEV), **kw)
+    r = O.upfirdn2d(x, f, **kw)
+    assert y.shape == r.shape
+    assert rel_err(y, r) < 1e-5
+    dy = torch.randn(r.shape, dtype=torch.float64)
+    dx, = torch.autograd.grad((y * dy.float().to(DEV)).sum(), [xd])
+    xr = x.clone().requires_grad_(True)
+    ref, = torch.autograd.grad((O.upfirdn2d(xr, f, **kw) * dy).sum(), [xr])
+    assert rel_err(dx, ref) < 1e-5
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
 def test_upfirdn2d_vec_path(dtype):
     """Channel-vectorised NHWC kernel on network-shaped tensors, vs the oracle in fp32."""
