@@ -7,6 +7,8 @@
 // One lane per output pixel; the four corner weights are computed once and reused across channels.
 // Backward scatters with float atomics into a float32 buffer (images are 1-3 channels, so the
 // atomic traffic is ~4 x 4 B per output pixel per channel).
+#include <cstdlib>
+
 #include "sg2_common.h"
 
 namespace sg2 {
@@ -21,6 +23,7 @@ struct GSParams {
     int64_t is_n, is_c, is_h, is_w;
     int64_t os_n, os_c, os_h, os_w;
     const int* dyn_hw;   // optional device [2]: logical input height / width (<= Hi, Wi of the buffer)
+    int gather_wide;     // deterministic gather: scan one pixel beyond the rounded-out box (SG2_GATHER_WIDE, tests)
 };
 
 struct Corners {
@@ -157,9 +160,19 @@ __global__ __launch_bounds__(256) void grid_sample_bwd_gather_kernel(GSParams p)
             }
             // clamped in double before the int conversion (a huge or NaN bound is undefined as an int)
             auto cl = [](double v, int hi) { return v > -4.0 ? (v < hi + 4.0 ? v : hi + 4.0) : -4.0; };
-            // (a one-pixel margin: the float corners differ from the exact map by far less than a pixel)
-            const int ox0 = max(0, (int)floor(cl(oxmin, p.Wo)) - 1), ox1 = min(p.Wo - 1, (int)ceil(cl(oxmax, p.Wo)) + 1);
-            const int oy0 = max(0, (int)floor(cl(oymin, p.Ho)) - 1), oy1 = min(p.Ho - 1, (int)ceil(cl(oymax, p.Ho)) + 1);
+            // The output pixels inside the exact preimage, widened by kGatherEps output pixels: the forward's float
+            // ix / iy differ from the exact map by ~1e-4 input pixels at these sizes (|ix| < 2^11, a few roundings
+            // of 2^-24), and the map's gain is >= 1/4 for any transform the pipe draws, so a pixel whose float
+            // corner is (X, Y) or its up / left neighbour lies within 1e-3 output pixels of the preimage.  (The
+            // first form scanned a whole pixel beyond the rounded-out box: 5 x 5 candidates per input pixel at a
+            // near-identity map instead of 2-3 per axis.)
+            constexpr double kGatherEps = 1.0 / 64;
+            int ox0 = max(0, (int)ceil(cl(oxmin - kGatherEps, p.Wo))), ox1 = min(p.Wo - 1, (int)floor(cl(oxmax + kGatherEps, p.Wo)));
+            int oy0 = max(0, (int)ceil(cl(oymin - kGatherEps, p.Ho))), oy1 = min(p.Ho - 1, (int)floor(cl(oymax + kGatherEps, p.Ho)));
+            if (p.gather_wide) {
+                ox0 = max(0, (int)floor(cl(oxmin, p.Wo)) - 1); ox1 = min(p.Wo - 1, (int)ceil(cl(oxmax, p.Wo)) + 1);
+                oy0 = max(0, (int)floor(cl(oymin, p.Ho)) - 1); oy1 = min(p.Ho - 1, (int)ceil(cl(oymax, p.Ho)) + 1);
+            }
             for (int oy = oy0; oy <= oy1; ++oy) {
                 const float by = base_coord(oy, p.Ho);
                 for (int ox = ox0; ox <= ox1; ++ox) {
@@ -275,6 +288,7 @@ int gs_bwd(float* gin, const void* gout, const float* grid, const float* theta, 
     SG2_CHECK(gin && gout && (grid || theta), "sg2_grid_sample_bwd: null pointer");
     GSParams p;
     p.in = gout; p.out = gin; p.grid = grid; p.theta = theta; p.dyn_hw = dyn_hw;
+    { const char* e = getenv("SG2_GATHER_WIDE"); p.gather_wide = e ? atoi(e) : 0; }
     if (fill(p, in_size, in_stride, out_size, out_stride)) return -1;
     // zero the float32 input-gradient buffer (dense over the strided extent)
     const int64_t extent = (p.N - 1) * p.is_n + (p.C - 1) * p.is_c + (p.Hi - 1) * p.is_h + (p.Wi - 1) * p.is_w + 1;

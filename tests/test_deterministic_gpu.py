@@ -176,6 +176,55 @@ def test_det_affine_grid_sample_bwd():
         assert rel_err(u, r) < 1e-5 and rel_err(w, r) < 1e-5, (rel_err(u, r), rel_err(w, r))
 
 
+@pytest.mark.parametrize('seed', [0, 1])
+def test_det_gather_matches_scatter_ada_maps(seed, monkeypatch):
+    """The gather's scan box (the exact preimage widened by 1/64 output pixel) misses no contribution: bitwise equal
+    to the gather scanning one pixel beyond the rounded-out box (SG2_GATHER_WIDE=1: the same candidates in the same
+    order plus ones that contribute nothing), and, like the atomic scatter, equal to grid_sample's float64 gradient to the rounding of the float sampling coordinates
+(2^-11 of the sum of the terms' magnitudes plus the largest |dy|), over maps drawn as the ADA pipe draws them
+    (scale 2^(0.2 N(0,1)), anisotropy, rotation, translation) plus a zoom-in to a quarter and a zoom-out by 3, at
+    the pipe's 2x-upsampled sizes in a static buffer with a dynamic extent."""
+    from torch_utils.ops import grid_sample_gradfix as gs
+    g = torch.Generator().manual_seed(100 + seed)
+    n = 12
+    s = torch.exp2(0.2 * torch.randn(n, generator=g))
+    s[:3] = torch.tensor([0.25, 0.4, 3.0])
+    a = torch.exp2(0.2 * torch.randn(n, generator=g))
+    r = (torch.rand(n, generator=g) - 0.5) * 0.6
+    tx, ty = torch.randn(n, generator=g) * 0.1, torch.randn(n, generator=g) * 0.1
+    c, si = torch.cos(r), torch.sin(r)
+    theta = torch.stack([torch.stack([s * a * c, -s * si, tx], 1), torch.stack([s * si, s / a * c, ty], 1)], 1)
+    x = torch.randn(n, 1, 524, 530, generator=g)
+    size = [n, 1, 512, 520]
+    dy = torch.randn(size, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    dyn = torch.tensor([500, 516], dtype=torch.int32, device=DEV)
+
+    def fn():
+        y = gs.affine_grid_sample(xd, theta.float().to(DEV), size, dyn_hw=dyn)
+        return torch.autograd.grad(y, [xd], dy.to(DEV))[0][:, :, :500, :516]
+    with sg2hip.deterministic():
+        u = fn().clone()
+        monkeypatch.setenv('SG2_GATHER_WIDE', '1')
+        wide = fn().clone()
+        monkeypatch.delenv('SG2_GATHER_WIDE')
+    assert torch.equal(u, wide), f'{int((u != wide).sum())} pixels differ from the wide scan'
+    w = fn()
+    xr = x[:, :, :500, :516].double().requires_grad_(True)
+    grid = F.affine_grid(theta.double(), size, align_corners=False)
+    ref, = torch.autograd.grad(F.grid_sample(xr, grid, align_corners=False), [xr], dy.double())
+    mag, = torch.autograd.grad(F.grid_sample(xr, grid, align_corners=False), [xr], dy.double().abs())
+    # the float sampling coordinates (|ix| up to ~10^3, a few roundings of 2^-24) move each bilinear weight by up to
+    # ~2^-12 (and, at a pixel boundary, a weight that small to the neighbouring pixel): a missed contribution of
+    # weight >= 2^-9 is caught
+    tol = 2.0 ** -11 * (mag + float(dy.abs().max()))
+    for name, got in (('gather', u), ('scatter', w)):
+        err = (got.double().cpu() - ref).abs()
+        bad = err > tol
+        assert not bool(bad.any()), (f'{name}: {int(bad.sum())} pixels off the float64 gradient, max '
+                                     f'{float(err.max()):.3g}, in samples {sorted(set(bad.nonzero()[:, 0].tolist()))}')
+
+
 def test_det_dot_hw_and_vjp_axpy():
     from torch_utils.ops import conv2d_gradfix as cg
     g = torch.Generator().manual_seed(5)
