@@ -15,7 +15,7 @@
 namespace sg2 {
 namespace {
 
-constexpr int kRows = 4, kLanes = 64, kUnroll = 8;
+constexpr int kRows = 4, kLanes = 64, kUnroll = 8, kMaxDetJobs = 4;
 
 __global__ __launch_bounds__(256) void det_sum_kernel(float* out, int64_t go, const float* ws, int64_t gw, int64_t ss,
                                                       int64_t S, int64_t n, int64_t chunk, int64_t to, int assign) {
@@ -48,17 +48,103 @@ __global__ __launch_bounds__(256) void det_sum_kernel(float* out, int64_t go, co
     }
 }
 
+// Few slots over many outputs (a weight gradient's pixel splits: S <= kVecS over millions of i): a lane owns four
+// consecutive i (16-byte loads) and adds s = 0, 1, ..., S - 1 in order.  The 4-row form leaves three of its four
+// lane rows idle at S = 1 and issues one 4-byte load per lane per slot (1.2-2.5 TB/s at S <= 4).
+constexpr int kVecS = 16;
+
+__global__ __launch_bounds__(256) void det_sum_vec4_kernel(float* out, int64_t go, const float* ws, int64_t gw,
+                                                           int64_t ss, int64_t S, int64_t n4) {
+    const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t g = blockIdx.y;
+    if (i4 >= n4) return;
+    const float4* w = (const float4*)(ws + g * gw) + i4;
+    const int64_t ss4 = ss / 4;
+    float4 acc = w[0];
+    int64_t s = 1;
+    for (; s + 7 < S; s += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = w[(s + k) * ss4];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
+    }
+    for (; s < S; ++s) {
+        const float4 v = w[s * ss4];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    float4* o = (float4*)(out + g * go) + i4;
+    float4 r = *o;
+    r.x += acc.x; r.y += acc.y; r.z += acc.z; r.w += acc.w;
+    *o = r;
+}
+
+// Several independent sums in one launch (the pairs of sums one kernel's slots feed, e.g. sg2_layer_bwd's bias and
+// demodulation gradients): workgroup b belongs to the job whose block range holds it and runs det_sum_kernel's body
+// for that job's (i block, g, chunk).
+struct DetJob {
+    float* out;
+    const float* ws;
+    int64_t go, gw, ss, S, n, chunk, to;
+    int assign, bx, G, K, begin;
+};
+struct DetJobs {
+    DetJob j[kMaxDetJobs];
+    int count;
+};
+
+__global__ __launch_bounds__(256) void det_sum_multi_kernel(DetJobs jobs) {
+    __shared__ float part[kRows][kLanes];
+    int jb = 0;
+    while (jb + 1 < jobs.count && (int)blockIdx.x >= jobs.j[jb + 1].begin) ++jb;
+    const DetJob& J = jobs.j[jb];
+    const int l = (int)blockIdx.x - J.begin;
+    const int bxi = l % J.bx, rest = l / J.bx;
+    const int64_t g = rest % J.G, z = rest / J.G;
+    const int il = threadIdx.x & (kLanes - 1), r = threadIdx.x / kLanes;
+    const int64_t i = (int64_t)bxi * kLanes + il;
+    const int64_t s0 = z * J.chunk, s1 = s0 + J.chunk < J.S ? s0 + J.chunk : J.S;
+    float acc = 0.f;
+    if (i < J.n) {
+        const float* w = J.ws + g * J.gw + i;
+        int64_t s = s0 + r;
+        for (; s + (kUnroll - 1) * kRows < s1; s += kUnroll * kRows) {
+            float v[kUnroll];
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) v[k] = w[(s + k * kRows) * J.ss];
+#pragma unroll
+            for (int k = 0; k < kUnroll; ++k) acc += v[k];
+        }
+        for (; s < s1; s += kRows) acc += w[s * J.ss];
+    }
+    part[r][il] = acc;
+    __syncthreads();
+    if (r == 0 && i < J.n) {
+        const float v = ((part[0][il] + part[1][il]) + part[2][il]) + part[3][il];
+        float* o = J.out + g * J.go + z * J.to + i;
+        if (J.assign) *o = v;
+        else *o += v;
+    }
+}
+
 }  // namespace
 
 hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t ss, int G, int64_t S, int64_t n,
                    DetArena& arena, hipStream_t st) {
     if (G <= 0 || n <= 0 || S <= 0) return hipSuccess;
     if (G > 65535) return hipErrorInvalidValue;
-    const int64_t bx = cdiv(n, kLanes);
-    // few outputs over a long sum (a bias or dot reduction over every pixel block): first chunks of the s range in
-    // parallel into a temporary, then their sums in chunk order (both steps fixed by the shapes alone)
     static const bool trace = getenv("SG2_DET_TRACE") != nullptr;   // diagnostics: one line per call (tools/)
     const int64_t S0 = S;
+    const int64_t bx = cdiv(n, kLanes);
+    if (S <= kVecS && n % 4 == 0 && go % 4 == 0 && gw % 4 == 0 && ss % 4 == 0 && (uintptr_t)out % 16 == 0 &&
+        (uintptr_t)ws % 16 == 0 && bx * G >= 512) {
+        if (trace) fprintf(stderr, "DETSUM G=%d n=%lld S=%lld K=%lld\n", G, (long long)n, (long long)S, 1LL);
+        det_sum_vec4_kernel<<<dim3((unsigned)cdiv(n / 4, 256), (unsigned)G, 1), 256, 0, st>>>(out, go, ws, gw, ss, S,
+                                                                                             n / 4);
+        return hipGetLastError();
+    }
+    // few outputs over a long sum (a bias or dot reduction over every pixel block): first chunks of the s range in
+    // parallel into a temporary, then their sums in chunk order (both steps fixed by the shapes alone)
     int64_t K = 1;
     if (bx * G < 512 && S > 16 * kRows) K = std::min<int64_t>(std::min<int64_t>(cdiv(S, 16 * kRows), 1024),
                                                               cdiv(512, bx * G));
@@ -82,6 +168,43 @@ hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t 
     if (trace) fprintf(stderr, "DETSUM G=%d n=%lld S=%lld K=%lld\n", G, (long long)n, (long long)S0,
                        (long long)K);
     det_sum_kernel<<<dim3((unsigned)bx, (unsigned)G, 1), 256, 0, st>>>(out, go, ws, gw, ss, S, n, S, 0, 0);
+    return hipGetLastError();
+}
+
+hipError_t det_sum_multi(const DetSumJob* jobs, int count, DetArena& arena, hipStream_t st) {
+    static const bool trace = getenv("SG2_DET_TRACE") != nullptr;
+    if (count <= 0) return hipSuccess;
+    if (count > kMaxDetJobs) return hipErrorInvalidValue;
+    DetJobs first{}, second{};
+    int nb1 = 0, nb2 = 0;
+    for (int q = 0; q < count; ++q) {
+        const DetSumJob& in = jobs[q];
+        if (in.G <= 0 || in.n <= 0 || in.S <= 0) continue;
+        if (in.G > 65535) return hipErrorInvalidValue;
+        const int64_t bx = cdiv(in.n, kLanes);
+        int64_t K = 1;
+        if (bx * in.G < 512 && in.S > 16 * kRows)
+            K = std::min<int64_t>(std::min<int64_t>(cdiv(in.S, 16 * kRows), 1024), cdiv(512, bx * in.G));
+        const float* ws = in.ws;
+        int64_t gw = in.gw, ss = in.ss, S = in.S;
+        if (K > 1) {
+            const int64_t chunk = cdiv(in.S, K);
+            K = cdiv(in.S, chunk);
+            float* tmp = arena.get((int64_t)in.G * K * in.n);
+            if (!tmp) { set_error("deterministic scratch too small (det_sum)"); return hipErrorOutOfMemory; }
+            DetJob& j = first.j[first.count++];
+            j = DetJob{tmp, in.ws, K * in.n, in.gw, in.ss, in.S, in.n, chunk, in.n, 1, (int)bx, in.G, (int)K, nb1};
+            nb1 += (int)(bx * in.G * K);
+            ws = tmp; gw = K * in.n; ss = in.n; S = K;
+        }
+        if (trace) fprintf(stderr, "DETSUM G=%d n=%lld S=%lld K=%lld\n", in.G, (long long)in.n, (long long)in.S,
+                           (long long)K);
+        DetJob& j = second.j[second.count++];
+        j = DetJob{in.out, ws, in.go, gw, ss, S, in.n, S, 0, 0, (int)bx, in.G, 1, nb2};
+        nb2 += (int)(bx * in.G);
+    }
+    if (first.count) det_sum_multi_kernel<<<nb1, 256, 0, st>>>(first);
+    if (second.count) det_sum_multi_kernel<<<nb2, 256, 0, st>>>(second);
     return hipGetLastError();
 }
 

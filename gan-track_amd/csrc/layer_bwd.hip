@@ -378,8 +378,11 @@ extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, cons
     int rc = launch_status("sg2_layer_bwd");
     if (rc || !det) return rc;
     hipError_t err = hipSuccess;
-    if (db) err = det_sum(db, 0, a.det_db, 0, C, 1, (int64_t)grid.x * N, C, arena, s);
-    if (!err && dd) err = det_sum(dd, 0, a.det_dd, 0, (int64_t)N * C, 1, grid.x, (int64_t)N * C, arena, s);
+    DetSumJob jobs[2];
+    int nj = 0;
+    if (db) jobs[nj++] = DetSumJob{db, 0, a.det_db, 0, C, 1, (int64_t)grid.x * N, C};
+    if (dd) jobs[nj++] = DetSumJob{dd, 0, a.det_dd, 0, (int64_t)N * C, 1, grid.x, (int64_t)N * C};
+    err = det_sum_multi(jobs, nj, arena, s);
     if (err) { set_error("sg2_layer_bwd: det_sum"); return err; }
     return 0;
 }

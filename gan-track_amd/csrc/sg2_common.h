@@ -61,10 +61,22 @@ class DetArena {
     int64_t cap_, off_;
 };
 // out[g * go + i] += sum_{s < S} ws[g * gw + s * ss + i] for g < G (<= 65535), i < n: a fixed-order sum (four
-// interleaved row sums over s, s = r mod 4 in increasing s, added in row order; det.hip), one launch.  `arena` is
-// kept for the callers' symmetry and unused.
+// interleaved row sums over s, s = r mod 4 in increasing s, added in row order; at S <= 16 over many outputs, s in
+// increasing order four outputs a lane; det.hip), one launch, or two (a chunk pass into `arena`) for few outputs
+// over many slots.
 hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t ss, int G, int64_t S, int64_t n,
                    DetArena& arena, hipStream_t st);
+// Up to four independent det_sum calls in (at most) two launches: the chunk passes of those that need one
+// together, then the final sums together; each job's order is det_sum's.
+struct DetSumJob {
+    float* out;
+    int64_t go;
+    const float* ws;
+    int64_t gw, ss;
+    int G;
+    int64_t S, n;
+};
+hipError_t det_sum_multi(const DetSumJob* jobs, int count, DetArena& arena, hipStream_t st);
 #define SG2_DET_GET(ptr, arena, n, what)                                                        \
     do {                                                                                       \
         (ptr) = (arena).get(n);                                                                \
