@@ -774,6 +774,8 @@ int launch(const UpfParams& p, bool vec, hipStream_t s) {
             static const bool hl = [] { const char* e = getenv("SG2_U1D_HLDS"); return e ? atoi(e) != 0 : true; }();
             if (vert && vr == 4 && ada_up) upfirdn_1d_vrun<T, 2, 1, 6, 4><<<g, 256, 0, s>>>(p);
             else if (vert && vr == 4 && ada_down) upfirdn_1d_vrun<T, 1, 2, 12, 4><<<g, 256, 0, s>>>(p);
+            else if (vert && vr == 8 && ada_up) upfirdn_1d_vrun<T, 2, 1, 6, 8><<<g, 256, 0, s>>>(p);
+            else if (vert && vr == 8 && ada_down) upfirdn_1d_vrun<T, 1, 2, 12, 8><<<g, 256, 0, s>>>(p);
             else if (horiz && hl && ada_up) upfirdn_1d_hlds<T, 2, 1, 6><<<g, 256, 0, s>>>(p);
             else if (horiz && hl && ada_down) upfirdn_1d_hlds<T, 1, 2, 12><<<g, 256, 0, s>>>(p);
             else if (horiz && ada_up) upfirdn_1d<T, true, 6, 2, 1><<<g, 256, 0, s>>>(p);

@@ -1,7 +1,7 @@
 """The ADA pipe of the bench configuration alone (GPU diagnostic): 256^2 1-ch, batch 32, p = 0.2, forward +
 backward of the geometric stage, 40 iterations; prints the device time per kernel per iteration and, for one
 draw, the dynamic extents the 1-D FIR passes compute (lims) next to their static buffers.
-    python tools/ada_micro.py [iters]"""
+    python tools/ada_micro.py [iters] [det]     (det: the deterministic reductions, the training default)"""
 import collections
 import os
 import sys
@@ -18,6 +18,9 @@ DEV = torch.device('cuda', 0)
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 40
+    if len(sys.argv) > 2 and sys.argv[2] == 'det':
+        import sg2hip
+        sg2hip.deterministic(True, device=DEV).__enter__()     # for the whole run
     torch.manual_seed(0)
     aug = augment_mi.AugmentPipe(run_dir=None, batch_size=32, xflip=1, xint=1, scale=1, rotate=1, aniso=1, xfrac=1,
                                  xint_max=0.05, rotate_max=3 / 360, xfrac_std=0.05, scale_std=0.05,
