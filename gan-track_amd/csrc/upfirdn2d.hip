@@ -177,7 +177,11 @@ __global__ __launch_bounds__(256) void upfirdn_1d_hlds(UpfParams p) {
     __shared__ float sf[64];
     __shared__ float sx[SPAN];
     const int F = p.fw;
-    for (int t = threadIdx.x; t < F; t += 256) sf[t] = p.f[p.flip ? t : F - 1 - t] * p.gain;
+    for (int t = threadIdx.x; t < KT * UP; t += 256) sf[t] = t < F ? p.f[p.flip ? t : F - 1 - t] * p.gain : 0.f;
+    __syncthreads();
+    float fr[KT * UP];                                 // the taps in registers, zero past the filter
+#pragma unroll
+    for (int t = 0; t < KT * UP; ++t) fr[t] = t < F ? sf[t] : 0.f;
     const int ly = p.lim ? p.lim[0] : p.OH, lx = p.lim ? p.lim[1] : p.OW;      // computed extent
     const int rows = min(p.OH, ly + (p.lim ? kZeroBand : 0)), cols = min(p.OW, lx + (p.lim ? kZeroBand : 0));
     const int tiles = (cols + 255) / 256;
@@ -204,26 +208,46 @@ __global__ __launch_bounds__(256) void upfirdn_1d_hlds(UpfParams p) {
         const float* w = sx + (i0 - base);
         float acc = 0.f;
 #pragma unroll
-        for (int k = 0; k < KT; ++k) {
-            const int t = t0 + k * UP;
-            acc += t < F ? w[k] * sf[t] : 0.f;
-        }
+        for (int k = 0; k < KT; ++k)      // tap t0 + k UP: registers at UP = 1; at UP = 2 (t0 alternates between
+            acc += w[k] * (UP == 1 ? fr[k] : sf[t0 + k * UP]);   // lanes) LDS, faster than a per-tap select
+
         *yp = (T)acc;
     }
 }
 
 // The vertical pass with UP, DOWN in {1, 2}: a lane owns column ox and a run of R consecutive output rows.
-// The run reads SPAN input rows; each is loaded once and added to every output of the run it is a tap of
-// (tap k of output j is input row i0(j) + k; i0(j) - i0(0) and the first tap's index are uniform), in
-// increasing k per output as upfirdn_1d does: 2 loads per output instead of KT.  Grid-strided over
-// (run, column tile) pairs like upfirdn_1d.
+// The run reads SPAN input rows; each is loaded once and feeds every output of the run it is a tap of, with the
+// (input row, output, tap) pattern fixed at compile time: output j reads rows dj + k with tap tj + k UP, where
+// (dj, tj) depend only on the parity P of the run's first z = oy0 DOWN - pad0 (VRunPat; at UP = 2 an even R keeps P
+// the same for every run of a launch).  So the taps stay in registers and every tap is one FMA -- the
+// first form tested each (row, output) pair with a uniform branch and an LDS read of its tap (77 branches, LDS
+// latency on the FMA chain).  Per output, taps are added in increasing k, as upfirdn_1d does.
+template <int UP, int DOWN, int P>
+struct VRunPat {
+    static constexpr int dj(int j) { return UP == 1 ? j * DOWN : (P == 0 ? (j + 1) / 2 : j / 2); }
+    static constexpr int tj(int j) { return UP == 1 ? 0 : (P == 0 ? (j & 1) : 1 - (j & 1)); }
+};
+
+template <int UP, int DOWN, int KT, int R, int SPAN, int P>
+__device__ __forceinline__ void vrun_acc(const float (&win)[SPAN], const float (&fr)[KT * UP], float (&acc)[R]) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+#pragma unroll
+        for (int k = 0; k < KT; ++k) acc[j] += win[VRunPat<UP, DOWN, P>::dj(j) + k] * fr[VRunPat<UP, DOWN, P>::tj(j) + k * UP];
+    }
+}
+
 template <typename T, int UP, int DOWN, int KT, int R>
 __global__ __launch_bounds__(256) void upfirdn_1d_vrun(UpfParams p) {
+    static_assert(UP == 1 || R % 2 == 0, "even runs keep the phase fixed");
     constexpr int SPAN = ((R - 1) * DOWN + UP - 1) / UP + KT;
     __shared__ float sf[64];
     const int F = p.fh;
     for (int t = threadIdx.x; t < F; t += 256) sf[t] = p.f[p.flip ? t : F - 1 - t] * p.gain;
     __syncthreads();
+    float fr[KT * UP];                                 // the taps in registers, zero past the filter
+#pragma unroll
+    for (int t = 0; t < KT * UP; ++t) fr[t] = t < F ? sf[t] : 0.f;
     const int ly = p.lim ? p.lim[0] : p.OH, lx = p.lim ? p.lim[1] : p.OW;      // computed extent
     const int rows = min(p.OH, ly + (p.lim ? kZeroBand : 0)), cols = min(p.OW, lx + (p.lim ? kZeroBand : 0));
     const int tiles = (cols + 255) / 256, runs = (rows + R - 1) / R;
@@ -236,29 +260,22 @@ __global__ __launch_bounds__(256) void upfirdn_1d_vrun(UpfParams p) {
         const int c = nc % p.C, n = nc / p.C;
         const T* xb = (const T*)p.x + n * p.xs_n + c * p.xs_c + (int64_t)ox * p.xs_w;
         T* yb = (T*)p.y + n * p.ys_n + c * p.ys_c + (int64_t)ox * p.ys_w;
-        int tj[R], dj[R], base = 0;
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            int t0, i0;
-            axis_taps_c<UP, DOWN>(oy0 + j, DOWN, p.pady0, UP, t0, i0);
-            if (j == 0) base = i0;
-            tj[j] = t0;
-            dj[j] = i0 - base;
-        }
-        float acc[R];
-#pragma unroll
-        for (int j = 0; j < R; ++j) acc[j] = 0.f;
+        const int z0 = oy0 * DOWN - p.pady0;
+        const int ph = UP == 2 ? (z0 & 1) : 0;
+        const int base = UP == 2 ? (z0 + ph) >> 1 : z0;              // input row of output 0's tap 0
+        float win[SPAN];
 #pragma unroll
         for (int m = 0; m < SPAN; ++m) {
             const int i = base + m;
             const bool ok = i >= 0 && i < p.H;
             const float v = (float)xb[(int64_t)(ok ? i : 0) * p.xs_h];
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                const int k = m - dj[j], t = tj[j] + k * UP;
-                if (k >= 0 && k < KT && t < F) acc[j] += ok ? v * sf[t] : 0.f;
-            }
+            win[m] = ok ? v : 0.f;
         }
+        float acc[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc[j] = 0.f;
+        if (ph) vrun_acc<UP, DOWN, KT, R, SPAN, 1>(win, fr, acc);
+        else vrun_acc<UP, DOWN, KT, R, SPAN, 0>(win, fr, acc);
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             const int oy = oy0 + j;

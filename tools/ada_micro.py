@@ -20,7 +20,9 @@ def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 40
     if len(sys.argv) > 2 and sys.argv[2] == 'det':
         import sg2hip
-        sg2hip.deterministic(True, device=DEV).__enter__()     # for the whole run
+        global _DET
+        _DET = sg2hip.deterministic(True, device=DEV)            # kept referenced: for the whole run
+        _DET.__enter__()
     torch.manual_seed(0)
     aug = augment_mi.AugmentPipe(run_dir=None, batch_size=32, xflip=1, xint=1, scale=1, rotate=1, aniso=1, xfrac=1,
                                  xint_max=0.05, rotate_max=3 / 360, xfrac_std=0.05, scale_std=0.05,
@@ -48,6 +50,12 @@ def main():
         y = aug(x)
         y.backward(g)
     torch.cuda.synchronize()
+    if os.environ.get('ADA_NOPROF'):               # under rocprofv3 (counter passes): the iterations only
+        for _ in range(iters):
+            y = aug(x)
+            y.backward(g)
+        torch.cuda.synchronize()
+        return
     with profile(activities=[ProfilerActivity.CUDA]) as prof:
         for _ in range(iters):
             y = aug(x)
