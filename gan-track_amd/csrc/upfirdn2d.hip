@@ -171,11 +171,14 @@ __global__ __launch_bounds__(256) void upfirdn_1d(UpfParams p) {
 // The horizontal pass with UP, DOWN in {1, 2}: a workgroup stages the input span of its 256 outputs of one row
 // (256 * DOWN / UP + KT values) in LDS with coalesced loads, then each lane reads its KT taps from LDS (the
 // global form issues KT strided loads per output: at DOWN = 2 each wave load spans twice the cache lines).
-template <typename T, int UP, int DOWN, int KT>
+template <typename T, int UP, int DOWN, int KT, int TWD = 256>
 __global__ __launch_bounds__(256) void upfirdn_1d_hlds(UpfParams p) {
-    constexpr int SPAN = (255 * DOWN + UP - 1) / UP + KT + 1;
+    // TWD: outputs per row segment; a workgroup takes 256 / TWD consecutive rows of one (n, c) plane (narrow
+    // outputs, e.g. the 313-wide down-2 pass, idle fewer lanes in 128-wide segments)
+    constexpr int ROWS = 256 / TWD;
+    constexpr int SPAN = ((TWD - 1) * DOWN + UP - 1) / UP + KT + 1;
     __shared__ float sf[64];
-    __shared__ float sx[SPAN];
+    __shared__ float sx[ROWS][SPAN];
     const int F = p.fw;
     for (int t = threadIdx.x; t < KT * UP; t += 256) sf[t] = t < F ? p.f[p.flip ? t : F - 1 - t] * p.gain : 0.f;
     __syncthreads();
@@ -184,33 +187,35 @@ __global__ __launch_bounds__(256) void upfirdn_1d_hlds(UpfParams p) {
     for (int t = 0; t < KT * UP; ++t) fr[t] = t < F ? sf[t] : 0.f;
     const int ly = p.lim ? p.lim[0] : p.OH, lx = p.lim ? p.lim[1] : p.OW;      // computed extent
     const int rows = min(p.OH, ly + (p.lim ? kZeroBand : 0)), cols = min(p.OW, lx + (p.lim ? kZeroBand : 0));
-    const int tiles = (cols + 255) / 256;
-    const int total = p.N * p.C * rows * tiles;
+    const int tiles = (cols + TWD - 1) / TWD, rgroups = (rows + ROWS - 1) / ROWS;
+    const int total = p.N * p.C * rgroups * tiles;
+    const int rr = threadIdx.x / TWD, col = threadIdx.x % TWD;
     for (int b = blockIdx.x; b < total; b += gridDim.x) {
-        const int row = b / tiles;
-        const int ox0 = (b - row * tiles) * 256, ox = ox0 + threadIdx.x;
-        const int oy = row % rows, nc = row / rows;
+        const int rg = b / tiles;
+        const int ox0 = (b - rg * tiles) * TWD, ox = ox0 + col;
+        const int oy0 = (rg % rgroups) * ROWS, nc = rg / rgroups;
         const int c = nc % p.C, n = nc / p.C;
         int tb, base;
         axis_taps_c<UP, DOWN>(ox0, DOWN, p.padx0, UP, tb, base);                 // the span's first input
-        const T* xl = (const T*)p.x + n * p.xs_n + c * p.xs_c + (int64_t)oy * p.xs_h;
+        const T* xp = (const T*)p.x + n * p.xs_n + c * p.xs_c;
         __syncthreads();                                                        // (the previous pair's reads)
-        for (int m = threadIdx.x; m < SPAN; m += 256) {
-            const int i = base + m;
-            sx[m] = (i >= 0 && i < p.W) ? (float)xl[(int64_t)i * p.xs_w] : 0.f;
+        for (int e = threadIdx.x; e < ROWS * SPAN; e += 256) {
+            const int r = e / SPAN, m = e - r * SPAN;
+            const int i = base + m, y = oy0 + r;
+            sx[r][m] = (i >= 0 && i < p.W && y < rows) ? (float)xp[(int64_t)y * p.xs_h + (int64_t)i * p.xs_w] : 0.f;
         }
         __syncthreads();
-        if (ox >= cols) continue;
+        const int oy = oy0 + rr;
+        if (ox >= cols || oy >= rows) continue;
         T* yp = (T*)p.y + n * p.ys_n + c * p.ys_c + (int64_t)oy * p.ys_h + (int64_t)ox * p.ys_w;
         if (oy >= ly || ox >= lx) { *yp = (T)0.f; continue; }
         int t0, i0;
         axis_taps_c<UP, DOWN>(ox, DOWN, p.padx0, UP, t0, i0);
-        const float* w = sx + (i0 - base);
+        const float* w = &sx[rr][i0 - base];
         float acc = 0.f;
 #pragma unroll
         for (int k = 0; k < KT; ++k)      // tap t0 + k UP: registers at UP = 1; at UP = 2 (t0 alternates between
             acc += w[k] * (UP == 1 ? fr[k] : sf[t0 + k * UP]);   // lanes) LDS, faster than a per-tap select
-
         *yp = (T)acc;
     }
 }
@@ -789,10 +794,13 @@ int launch(const UpfParams& p, bool vec, hipStream_t s) {
             const bool ada_up = up == 2 && down == 1 && kt == 6, ada_down = up == 1 && down == 2 && kt == 12;
             static const int vr = [] { const char* e = getenv("SG2_U1D_VRUN"); return e ? atoi(e) : 4; }();
             static const bool hl = [] { const char* e = getenv("SG2_U1D_HLDS"); return e ? atoi(e) != 0 : true; }();
+            static const int htw = [] { const char* e = getenv("SG2_U1D_HTW"); return e ? atoi(e) : 128; }();
             if (vert && vr == 4 && ada_up) upfirdn_1d_vrun<T, 2, 1, 6, 4><<<g, 256, 0, s>>>(p);
             else if (vert && vr == 4 && ada_down) upfirdn_1d_vrun<T, 1, 2, 12, 4><<<g, 256, 0, s>>>(p);
             else if (vert && vr == 8 && ada_up) upfirdn_1d_vrun<T, 2, 1, 6, 8><<<g, 256, 0, s>>>(p);
             else if (vert && vr == 8 && ada_down) upfirdn_1d_vrun<T, 1, 2, 12, 8><<<g, 256, 0, s>>>(p);
+            else if (horiz && hl && ada_up && htw == 128) upfirdn_1d_hlds<T, 2, 1, 6, 128><<<g, 256, 0, s>>>(p);
+            else if (horiz && hl && ada_down && htw == 128) upfirdn_1d_hlds<T, 1, 2, 12, 128><<<g, 256, 0, s>>>(p);
             else if (horiz && hl && ada_up) upfirdn_1d_hlds<T, 2, 1, 6><<<g, 256, 0, s>>>(p);
             else if (horiz && hl && ada_down) upfirdn_1d_hlds<T, 1, 2, 12><<<g, 256, 0, s>>>(p);
             else if (horiz && ada_up) upfirdn_1d<T, true, 6, 2, 1><<<g, 256, 0, s>>>(p);
