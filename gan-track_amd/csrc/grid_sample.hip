@@ -197,17 +197,20 @@ __device__ __forceinline__ int reflect1(int k, int L) { return k < 0 ? -k : (k >
 
 __global__ __launch_bounds__(256) void reflect_pad_kernel(float* y, const float* x, const int* m, int N, int C, int H,
                                                           int W, int Hs, int Ws) {
+    // the grid strides over the region a consumer reads only (the padded image plus 64 rows / columns of zeros,
+    // upfirdn2d.hip UpfParams::lim), with 32-bit index math (the host checks N C Hs Ws < 2^31)
     const int mx0 = m[0], my0 = m[1], mx1 = m[2], my1 = m[3];
     const int Hd = H + my0 + my1, Wd = W + mx0 + mx1;
-    const int64_t total = (int64_t)N * C * Hs * Ws;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int px = (int)(i % Ws);
-        const int py = (int)((i / Ws) % Hs);
-        const int64_t nc = i / ((int64_t)Ws * Hs);
-        if (py >= Hd + 64 || px >= Wd + 64) continue;      // never read (upfirdn2d.hip UpfParams::lim)
+    const int hl = min(Hs, Hd + 64), wl = min(Ws, Wd + 64);
+    const unsigned total = (unsigned)N * C * hl * wl;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const unsigned r = i / (unsigned)wl;
+        const int px = (int)(i - r * (unsigned)wl);
+        const unsigned nc = r / (unsigned)hl;
+        const int py = (int)(r - nc * (unsigned)hl);
         float v = 0.f;
-        if (py < Hd && px < Wd) v = x[(nc * H + reflect1(py - my0, H)) * W + reflect1(px - mx0, W)];
-        y[i] = v;
+        if (py < Hd && px < Wd) v = x[((int64_t)nc * H + reflect1(py - my0, H)) * W + reflect1(px - mx0, W)];
+        y[((int64_t)nc * Hs + py) * Ws + px] = v;
     }
 }
 
@@ -359,6 +362,7 @@ extern "C" int sg2_reflect_pad_dyn(float* y, const float* x, const int* margins,
               "sg2_reflect_pad_dyn: the static buffer must hold the largest padded image (3H-2 x 3W-2)");
     const int64_t total = adjoint ? (int64_t)N * C * H * W : (int64_t)N * C * Hs * Ws;
     if (total == 0) return 0;
+    SG2_CHECK(adjoint || total < INT32_MAX, "sg2_reflect_pad_dyn: static buffer too large");
     const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 64);
     if (adjoint) reflect_pad_adj_kernel<<<g, 256, 0, as_stream(stream)>>>(y, x, margins, N, C, H, W, Hs, Ws);
     else reflect_pad_kernel<<<g, 256, 0, as_stream(stream)>>>(y, x, margins, N, C, H, W, Hs, Ws);
