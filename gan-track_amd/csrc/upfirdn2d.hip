@@ -790,7 +790,8 @@ int launch(const UpfParams& p, bool vec, hipStream_t s) {
         const int kt = (F + up - 1) / up;
         const int64_t pairs = (int64_t)p.N * p.C * p.OH * cdiv(p.OW, 256);
         if ((horiz || vert) && kt <= 16 && pairs < INT32_MAX) {
-            const unsigned g = (unsigned)std::min<int64_t>(pairs, 256 * 64);
+            static const int gmax = [] { const char* e = getenv("SG2_U1D_GRID"); return e ? atoi(e) : 4096; }();   // 16 a CU (r06aj A/B)
+            const unsigned g = (unsigned)std::min<int64_t>(pairs, gmax);
             const bool ada_up = up == 2 && down == 1 && kt == 6, ada_down = up == 1 && down == 2 && kt == 12;
             static const int vr = [] { const char* e = getenv("SG2_U1D_VRUN"); return e ? atoi(e) : 4; }();
             static const bool hl = [] { const char* e = getenv("SG2_U1D_HLDS"); return e ? atoi(e) != 0 : true; }();
