@@ -319,7 +319,8 @@ int gs_bwd(float* gin, const void* gout, const float* grid, const float* theta, 
     if (gather) {
         SG2_CHECK(p.C <= 4, "sg2_affine_grid_sample_bwd: deterministic mode supports C <= 4");
         const int64_t tot_in = (int64_t)p.N * p.Hi * p.Wi;
-        const int gi = (int)std::min<int64_t>(cdiv(tot_in, 256), 256 * 64);
+        static const int gmax = [] { const char* e = getenv("SG2_GATHER_GRID"); return e ? atoi(e) : 256 * 64; }();
+        const int gi = (int)std::min<int64_t>(cdiv(tot_in, 256), gmax);
         SG2_DISPATCH(dtype, T, { grid_sample_bwd_gather_kernel<T><<<gi, 256, 0, s>>>(p); });
         return launch_status("sg2_affine_grid_sample_bwd (deterministic gather)");
     }
@@ -363,7 +364,8 @@ extern "C" int sg2_reflect_pad_dyn(float* y, const float* x, const int* margins,
     const int64_t total = adjoint ? (int64_t)N * C * H * W : (int64_t)N * C * Hs * Ws;
     if (total == 0) return 0;
     SG2_CHECK(adjoint || total < INT32_MAX, "sg2_reflect_pad_dyn: static buffer too large");
-    const int g = (int)std::min<int64_t>(cdiv(total, 256), 256 * 64);
+    static const int gmax = [] { const char* e = getenv("SG2_PAD_GRID"); return e ? atoi(e) : 256 * 64; }();
+    const int g = (int)std::min<int64_t>(cdiv(total, 256), gmax);
     if (adjoint) reflect_pad_adj_kernel<<<g, 256, 0, as_stream(stream)>>>(y, x, margins, N, C, H, W, Hs, Ws);
     else reflect_pad_kernel<<<g, 256, 0, as_stream(stream)>>>(y, x, margins, N, C, H, W, Hs, Ws);
     return launch_status("sg2_reflect_pad_dyn");
