@@ -34,6 +34,7 @@ enabled = True         # switch for A/B tests against the composed (unfused) pat
 prezero = os.environ.get('SG2_PREZERO', '1') != '0'   # one zero fill per layer backward (A/B switch)
 fast_backward = True   # first-order backward through the fused kernels (A/B switch)
 fused_vjp = os.environ.get('SG2_FUSED_VJP', '1') != '0'   # create_graph input-gradient pass as one node (A/B)
+tap_enabled = os.environ.get('SG2_TORGB_TAP', '1') != '0'   # toRGB input gradient + next block's in one epilogue
 _ACT = {0: 'linear', 1: 'lrelu'}
 
 
@@ -112,31 +113,74 @@ class FusedConv(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, styles, weight, dcoefs, noise, bias, y, aux = ctx.saved_tensors
-        stride, pad, act, alpha, gain, clamp, has_res, wgain = ctx.cfg
         need = ctx.needs_input_grad
-        dres = dy if need[6] else None
-        zsrc = aux if has_res else y
-        c = aux if (dcoefs is not None and not has_res) else None
-        if not torch.is_grad_enabled() and fast_backward:
-            g = _fast_backward(need, dy, _cg._nhwc(x), styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act,
-                               alpha, gain, clamp, wgain)
-        elif fused_vjp and _cg.weight_gradients_disabled and not has_res and (dcoefs is None or c is not None):
-            # the path-length / R1 pass: input gradients only, as one node with fused kernels both ways
-            dx, ds, dd = _LayerVJP.apply(dy, x, styles, weight, dcoefs, zsrc, c, need[0], need[1], need[3],
-                                         stride, pad, act, alpha, gain, clamp, wgain)
-            g = (dx, ds, None, dd, None, None)
-        else:
-            g = _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha,
-                                   gain, clamp, wgain)
-        return g + (dres, None, None, None, None, None, None, None)
+        g = _fused_conv_grads(ctx, need, dy)
+        return g + (dy if need[6] else None, None, None, None, None, None, None, None)
+
+
+def _fused_conv_grads(ctx, need, dy, dx_residual=None):
+    """(dx, ds, dw, dd, dnoise, db) of a FusedConv node.  dx_residual: a gradient to add to dx (FusedConvTap: the
+    other consumer's gradient of the layer input), inside the dgrad epilogue on the first-order fast path."""
+    x, styles, weight, dcoefs, noise, bias, y, aux = ctx.saved_tensors
+    stride, pad, act, alpha, gain, clamp, has_res, wgain = ctx.cfg
+    zsrc = aux if has_res else y
+    c = aux if (dcoefs is not None and not has_res) else None
+    if not torch.is_grad_enabled() and fast_backward:
+        return _fast_backward(need, dy, _cg._nhwc(x), styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act,
+                              alpha, gain, clamp, wgain, dx_residual=dx_residual)
+    if fused_vjp and _cg.weight_gradients_disabled and not has_res and (dcoefs is None or c is not None):
+        # the path-length / R1 pass: input gradients only, as one node with fused kernels both ways
+        dx, ds, dd = _LayerVJP.apply(dy, x, styles, weight, dcoefs, zsrc, c, need[0], need[1], need[3],
+                                     stride, pad, act, alpha, gain, clamp, wgain)
+        g = (dx, ds, None, dd, None, None)
+    else:
+        g = _composed_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha,
+                               gain, clamp, wgain)
+    if dx_residual is not None and g[0] is not None:
+        # in the input's dtype first, as autograd rounds each gradient before it sums them
+        g = (g[0].to(dx_residual.dtype) + dx_residual,) + tuple(g[1:])
+    return g
+
+
+class FusedConvTap(torch.autograd.Function):
+    """FusedConv (a toRGB layer: no demodulation, noise or residual) that also passes its input through as a second
+    output -- the synthesis block's feature map, which feeds both the toRGB layer and the next block
+    (networks_stylegan2.py SynthesisBlock.forward; reference :446-455).  Autograd would add the two consumers'
+    gradients of the map in an activation-sized pass; this node receives both and, on the first-order fast path, adds
+    the pass-through gradient inside the toRGB input gradient's epilogue (the conv epilogue's residual: round(dx) +
+    g, the sum autograd forms)."""
+
+    @staticmethod
+    def forward(ctx, x, styles, weight, bias, pad, clamp):
+        y = FusedConv.forward(ctx, x, styles, weight, None, None, bias, None, 1, pad, 0, 0.2, 1.0, clamp, 1.0)
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, g_pass, dy):
+        n = ctx.needs_input_grad
+        need = (n[0], n[1], n[2], False, False, n[3], False)
+        if dy is None:
+            return g_pass, None, None, None, None, None
+        res = None
+        if g_pass is not None and n[0]:
+            res = _cg._nhwc(g_pass.to(ctx.saved_tensors[0].dtype))
+        dx, ds, dw, _, _, db = _fused_conv_grads(ctx, need, dy, dx_residual=res)
+        if dx is None and res is not None:
+            dx = res
+        return dx, ds, dw, db, None, None
+
+
+def fused_conv_tap(x, weight, styles, bias, padding, clamp):
+    """(x, fused_conv(x, weight, styles=styles, bias=bias, padding=padding, clamp=clamp)) through FusedConvTap."""
+    return FusedConvTap.apply(x, styles, weight, bias, int(padding), float(clamp if clamp is not None else -1.0))
 
 
 def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, pad, wgain=1.0, acc_ds=None,
-                        acc_dw=None):
+                        acc_dw=None, dx_residual=None):
     """Gradients of c = conv(x * s, W) given dc: dx = convT(dc, W) * s and ds = sum_hw convT(dc, W) * x in
     one dgrad launch (out_scale / dot_src epilogue), dw = the s-scaled weight gradient.  acc_ds / acc_dw:
-    zeroed f32 buffers (N*Cin / Cout*kh*kw*Cin) the reductions accumulate into (no memset per call)."""
+    zeroed f32 buffers (N*Cin / Cout*kh*kw*Cin) the reductions accumulate into (no memset per call).
+    dx_residual: added to dx in the epilogue (round(dx) + residual; FusedConvTap)."""
     n, cin, h, w = x.shape
     cout, _, kh, kw = weight.shape
     dt = x.dtype
@@ -145,7 +189,9 @@ def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, p
     want_ds = need_s and styles is not None
     dso = acc_ds.view(n, cin) if (want_ds and acc_ds is not None) else None
     if need_x or want_ds:
-        if _halo(dc, kh, kw, stride, pad):
+        if dx_residual is not None and not need_x:
+            dx_residual = None
+        if _halo(dc, kh, kw, stride, pad) and dx_residual is None:
             wT = _cg._pack_convT(weight, dt, flip=True, scale=wgain)
             if want_ds:
                 dx, _, ds = _cg.conv3x3_fused(dc, wT, cin, out_scale=s32, dot_src=x, dot_out=dso)
@@ -154,10 +200,11 @@ def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, p
         else:
             if want_ds:
                 dx, _, ds = _cg.conv_fused(dc, _cg._pack_convT(weight, dt, scale=wgain), cin, h, w, kh, kw, stride,
-                                           (pad, pad), transpose=True, out_scale=s32, dot_src=x, dot_out=dso)
+                                           (pad, pad), transpose=True, out_scale=s32, dot_src=x, dot_out=dso,
+                                           residual=dx_residual)
             else:
                 dx, _ = _cg.conv_fused(dc, _cg._pack_convT(weight, dt, scale=wgain), cin, h, w, kh, kw, stride,
-                                       (pad, pad), transpose=True, out_scale=s32)
+                                       (pad, pad), transpose=True, out_scale=s32, residual=dx_residual)
         ds = ds.to(styles.dtype) if want_ds else None
         dx = dx if need_x else None
     if need_w and not _cg.weight_gradients_disabled:
@@ -366,7 +413,7 @@ class _LayerVJP(torch.autograd.Function):
 
 
 def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, stride, pad, act, alpha, gain, clamp,
-                   wgain=1.0):
+                   wgain=1.0, dx_residual=None):
     """First order in three kernels: sg2_layer_bwd; dgrad with the *s scale (+ ds); scaled wgrad."""
     n, cin, h, w = x.shape
     cout, _, kh, kw = weight.shape
@@ -398,7 +445,7 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
         dn = dz.sum(1, keepdim=True, dtype=torch.float32) if want_dn else None
         dc = _cg._nhwc(dz * dcoefs.to(dt).reshape(n, -1, 1, 1) if dcoefs is not None else dz)
     dx, ds, dw = _scaled_input_grads(dc, x, styles, weight, need[0], need[1], need[2], stride, pad, wgain,
-                                     acc_ds=parts[2], acc_dw=parts[3])
+                                     acc_ds=parts[2], acc_dw=parts[3], dx_residual=dx_residual)
     db = db.to(bias.dtype) if db is not None else None
     dd = dd.to(dcoefs.dtype) if dd is not None else None
     dn = dn.to(noise.dtype) if dn is not None else None

@@ -561,6 +561,16 @@ class ToRGBLayer(torch.nn.Module):
         x = modulated_conv2d(x=x, weight=self.weight, styles=styles, demodulate=False, fused_modconv=fused_modconv)
         return bias_act.bias_act(x, self.bias.to(x.dtype), clamp=self.conv_clamp)
 
+    def forward_tap(self, x, w, fused_modconv=True, styles=None):
+        """(x, self(x, w)) for a feature map that also feeds the next block: its two gradients are added inside the
+        toRGB input gradient's epilogue (modconv.FusedConvTap) instead of by autograd in an activation-sized pass."""
+        if styles is None:
+            styles = self.affine(w, out_gain=self.weight_gain)
+        if modconv.tap_enabled and modconv.supported_generic(x, self.weight):
+            return modconv.fused_conv_tap(x, self.weight, styles, self.bias, self.weight.shape[-1] // 2,
+                                          self.conv_clamp)
+        return x, self.forward(x, w, fused_modconv=fused_modconv, styles=styles)
+
     def extra_repr(self):
         return f'in_channels={self.in_channels:d}, out_channels={self.out_channels:d}, w_dim={self.w_dim:d}'
 
@@ -646,7 +656,10 @@ class SynthesisBlock(torch.nn.Module):
             misc.assert_shape(img, [None, self.img_channels, self.resolution // 2, self.resolution // 2])
             img = upfirdn2d.upsample2d(img, self.resample_filter)
         if self.is_last or self.architecture == 'skip':
-            y = self.torgb(x, next(w_iter), fused_modconv=fused_modconv, styles=next(s_iter))
+            if self.is_last:
+                y = self.torgb(x, next(w_iter), fused_modconv=fused_modconv, styles=next(s_iter))
+            else:     # x feeds the next block too
+                x, y = self.torgb.forward_tap(x, next(w_iter), fused_modconv=fused_modconv, styles=next(s_iter))
             y = y.to(dtype=torch.float32, memory_format=torch.contiguous_format)
             img = img.add_(y) if img is not None else y
         assert x.dtype == dtype

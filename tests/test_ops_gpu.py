@@ -846,6 +846,53 @@ def test_fused_torgb_and_f32_layer(dtype):
                                                                     layer.affine.weight], x1, dy1, dtype)
 
 
+@pytest.mark.parametrize('fp16', [False, True])
+def test_torgb_tap_matches_autograd_sum(fp16, monkeypatch):
+    """SynthesisBlock feature maps feed both the toRGB layer and the next block: with modconv.FusedConvTap the two
+    gradients of the map are added inside the toRGB input gradient's epilogue.  A whole small generator's first-order
+    gradients (every parameter, and the latent input's) are bitwise those of autograd's own add (tap off), and the
+    create_graph pass (the path-length shape: input gradients, then a second backward) matches to the rounding of
+    a different summation order."""
+    from training import networks_stylegan2 as net
+    from torch_utils.ops import modconv
+    torch.manual_seed(31)
+    G = net.Generator(z_dim=32, c_dim=0, w_dim=32, img_resolution=64, img_channels=1, channel_base=2048,
+                      channel_max=64, num_fp16_res=4 if fp16 else 0, conv_clamp=256,
+                      mapping_kwargs=dict(num_layers=2)).to(DEV)
+    z = torch.randn(4, 32, device=DEV)
+    dy = torch.randn(4, 1, 64, 64, device=DEV)
+
+    def grads(tap, second=False):
+        monkeypatch.setattr(modconv, 'tap_enabled', tap)
+        ws = G.mapping(z, None).detach().requires_grad_(True)
+        img = G.synthesis(ws, noise_mode='const')
+        if not second:
+            gs = torch.autograd.grad((img * dy).sum(), [ws] + list(G.parameters()), allow_unused=True)
+        else:
+            g, = torch.autograd.grad((img * dy).sum(), [ws], create_graph=True)
+            gs = torch.autograd.grad(g.square().sum(), [ws] + list(G.synthesis.parameters()), allow_unused=True)
+        return [t for t in gs]
+    import sg2hip
+    for second in (False, True):
+        with sg2hip.deterministic():        # fixed-order reductions: the comparison is of the tap alone
+            a, b = grads(True, second), grads(False, second)
+        for i, (u, v) in enumerate(zip(a, b)):
+            assert (u is None) == (v is None), i
+            if u is not None and not second:
+                assert torch.equal(u, v), (i, float((u - v).abs().max()))
+        if second:
+            # the tap changes the order autograd runs the first pass's nodes in, so tensors with three or more
+            # gradient contributions sum them in another order: the second pass differs by that rounding (the
+            # deterministic baseline against itself is bitwise; tools/tap_diag.py) -- per tensor up to 3e-4 at 16
+            # bits, more on the near-cancelling scalar noise-strength sums; judged on the whole flat gradient
+            fa = torch.cat([u.float().flatten() for u in a if u is not None])
+            fb = torch.cat([v.float().flatten() for v in b if v is not None])
+            ok = torch.isfinite(fb)
+            assert torch.equal(torch.isfinite(fa), ok)          # (a 16-bit second order can overflow: both alike)
+            rel = float((fa[ok] - fb[ok]).norm() / fb[ok].norm())
+            assert rel < (1e-3 if fp16 else 1e-5), rel
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float16])
 @pytest.mark.parametrize('geom', [(3, 2, 0, True), (3, 2, 0, False), (3, 1, 1, False), (1, 1, 0, False),
                                   (1, 1, 0, True, 1, 64, 67, 61), (1, 1, 0, True, 3, 128, 9, 7),
