@@ -930,6 +930,7 @@ int launch_fwd(ConvArgs& a, bool vec, hipStream_t s) {
 // ------------------------------------------------------------------------------------ wgrad
 
 struct WgradArgs {
+    int oikk;            // sg2_conv2d_wgrad_oikk: the final slot sum writes dw as [A][B][KH][KW]
     const void* g;   // [N, OH, OW, A]
     const void* x;   // [N, H, W, B]
     float* dw;       // [A][KK][B]
@@ -1440,7 +1441,8 @@ int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
     }
     int rc = launch_status("sg2_conv2d_wgrad");
     if (rc || !a.det) return rc;
-    hipError_t e = det_sum(a.dw, 0, a.det, 0, nel, 1, a.splits, nel, arena, s);
+    hipError_t e = a.oikk ? det_sum_oikk(a.dw, a.det, a.splits, a.A, KK, a.B, s)
+                          : det_sum(a.dw, 0, a.det, 0, nel, 1, a.splits, nel, arena, s);
     if (e) { set_error("sg2_conv2d_wgrad: det_sum"); return (int)e; }
     return 0;
 }
@@ -1668,9 +1670,32 @@ extern "C" int sg2_conv2d(void* y, const void* x, const void* w, int dtype, int 
                             nullptr, nullptr, workspace, workspace_elems, stream);
 }
 
+namespace sg2 {
+int conv2d_wgrad_impl(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B, int H,
+                      int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* g_scale,
+                      const float* x_scale, float alpha, void* stream, int oikk);
+}
+
 extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
                                 int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* g_scale,
                                 const float* x_scale, float alpha, void* stream) {
+    return sg2::conv2d_wgrad_impl(dw, g, x, dtype, N, A, OH, OW, B, H, W, KH, KW, stride, pad_y, pad_x, g_scale,
+                                  x_scale, alpha, stream, 0);
+}
+
+extern "C" int sg2_conv2d_wgrad_oikk(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW,
+                                     int B, int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, float alpha,
+                                     void* stream) {
+    using namespace sg2;
+    SG2_CHECK(dtype == SG2_F32S3 && det_on() && B % 4 == 0,
+              "sg2_conv2d_wgrad_oikk: SG2_F32S3 operands in deterministic mode, B % 4 == 0");
+    return conv2d_wgrad_impl(dw, g, x, dtype, N, A, OH, OW, B, H, W, KH, KW, stride, pad_y, pad_x, nullptr, nullptr,
+                             alpha, stream, 1);
+}
+
+int sg2::conv2d_wgrad_impl(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
+                           int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* g_scale,
+                           const float* x_scale, float alpha, void* stream, int oikk) {
     using namespace sg2;
     SG2_CHECK(dw && g && x, "sg2_conv2d_wgrad: null pointer");
     SG2_CHECK(N > 0 && A > 0 && B > 0 && OH > 0 && OW > 0 && H > 0 && W > 0, "sg2_conv2d_wgrad: empty shape");
@@ -1693,6 +1718,7 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
     a.N = N; a.A = A; a.OH = OH; a.OW = OW; a.B = B; a.H = H; a.W = W; a.KH = KH; a.KW = KW;
     a.stride = stride; a.pady = pad_y; a.padx = pad_x; a.alpha = alpha;
     a.M = N * OH * OW;
+    a.oikk = oikk;
     if (p3) {
         a.gpl = (int64_t)N * OH * OW * A;
         a.xpl = (int64_t)N * H * W * B;

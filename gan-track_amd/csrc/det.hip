@@ -127,6 +127,37 @@ __global__ __launch_bounds__(256) void det_sum_multi_kernel(DetJobs jobs) {
     }
 }
 
+// det_sum into the parameter layout of a convolution weight gradient: the slots hold [A][KK][B] partials (the
+// kernels' K-major layout), out is [A][B][KK] (torch's [O, I, kh, kw]).  A lane owns four consecutive b of one
+// (a, tap) -- 16-byte loads, s in order -- and writes them KK floats apart.
+__global__ __launch_bounds__(256) void det_sum_oikk_kernel(float* out, const float* ws, int64_t S, int64_t nel, int KK,
+                                                           int B) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;   // 4-element group of the [A][KK][B] slot layout
+    if (q * 4 >= nel) return;
+    const float4* w = (const float4*)ws + q;
+    const int64_t nel4 = nel / 4;
+    float4 acc = w[0];
+    int64_t s = 1;
+    for (; s + 7 < S; s += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = w[(s + k) * nel4];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
+    }
+    for (; s < S; ++s) {
+        const float4 v = w[s * nel4];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    const int64_t i = q * 4;
+    const int b = (int)(i % B);
+    const int64_t at = i / B;
+    const int t = (int)(at % KK);
+    const int64_t a = at / KK;
+    float* o = out + (a * B + b) * KK + t;
+    o[0] += acc.x; o[KK] += acc.y; o[2 * KK] += acc.z; o[3 * KK] += acc.w;
+}
+
 }  // namespace
 
 hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t ss, int G, int64_t S, int64_t n,
@@ -168,6 +199,14 @@ hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t 
     if (trace) fprintf(stderr, "DETSUM G=%d n=%lld S=%lld K=%lld\n", G, (long long)n, (long long)S0,
                        (long long)K);
     det_sum_kernel<<<dim3((unsigned)bx, (unsigned)G, 1), 256, 0, st>>>(out, go, ws, gw, ss, S, n, S, 0, 0);
+    return hipGetLastError();
+}
+
+hipError_t det_sum_oikk(float* out, const float* ws, int64_t S, int A, int KK, int B, hipStream_t st) {
+    const int64_t nel = (int64_t)A * KK * B;
+    if (nel == 0 || S <= 0) return hipSuccess;
+    if (B % 4 || (uintptr_t)ws % 16) return hipErrorInvalidValue;
+    det_sum_oikk_kernel<<<(unsigned)cdiv(nel / 4, 256), 256, 0, st>>>(out, ws, S, nel, KK, B);
     return hipGetLastError();
 }
 

@@ -60,6 +60,7 @@ SIGNATURES = {
                        _vp, _vp, _vp],
     'sg2_conv3x3_up2': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp],
     'sg2_conv2d_wgrad': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _f, _vp],
+    'sg2_conv2d_wgrad_oikk': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp],
     'sg2_upfirdn2d_lim': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i,
                           _i, _f, _vp, _vp],
     'sg2_upfirdn2d_fused': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _i, _i, _i, _i, _i, _i, _i, _i, _i,
@@ -85,7 +86,7 @@ SIGNATURES = {
     'sg2_pack_weight': [_vp, _i, _vp, _i, _i, _i, _i, _i64, _i64, _i64, _i, _f, _vp],
     'sg2_pack_weight_multi': [_vp, _i, _vp],
 }
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lib = None
 
@@ -130,6 +131,11 @@ def clean_workspace(on=True):
 _det_scratch = {}
 _det_retired = []
 _det_state = (0, 0)     # the registration in force: (scratch pointer, bytes); (0, 0) = float-atomic mode
+
+
+def det_active():
+    """Whether the deterministic reductions are in force on this process (sg2_set_deterministic)."""
+    return _det_state[0] != 0
 
 
 def _det_register(ptr, nbytes):

@@ -221,16 +221,27 @@ def conv_fused(x, wp, cout, oh, ow, kh, kw, stride, pad, transpose=False, in_sca
     return (y, aux, dot) if dot_src is not None else (y, aux)
 
 
-def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None, alpha=1.0, out=None):
+def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None, alpha=1.0, out=None, param_layout=False):
     """dw[a, b, ky, kx] = alpha * sum g[n,a,oy,ox] (* g_scale[n,a]) x[n,b,oy*s+ky-p,ox*s+kx-p] (* x_scale[n,b]);
-    returns f32 [A,B,kh,kw] (NHWC-packed).  alpha: a layer's weight gain (the backward of w * gain).
-    out: a zeroed f32 buffer of A*kh*kw*B elements to accumulate into (the call skips its memset)."""
+    returns f32 [A,B,kh,kw] (NHWC-packed: a permuted view).  alpha: a layer's weight gain (the backward of w * gain).
+    out: a zeroed f32 buffer of A*kh*kw*B elements to accumulate into (the call skips its memset).
+    param_layout: where the library can (f32 layers under the deterministic reductions, sg2_conv2d_wgrad_oikk),
+    write dw contiguous in [A, B, kh, kw] -- the parameter's own layout, which autograd's gradient accumulation then
+    takes as is instead of copying a permuted view."""
     n, a, oh, ow = g.shape
     _, b, h, w = x.shape
-    dw = out.view(a, kh, kw, b) if out is not None else torch.empty([a, kh, kw, b], dtype=torch.float32, device=g.device)
     ga, xa, dt, gs, xs = g, x, _hip.dtype_code(g), g_scale, x_scale
     if _p3(g, 8) and a % 8 == 0 and b % 8 == 0 and not (kh == 1 and kw == 1 and min(a, b) <= 4):
         ga, xa, dt, gs, xs = split3(_nhwc(g), g_scale), split3(_nhwc(x), x_scale), _hip.F32S3, None, None
+        if param_layout and _hip.det_active():
+            dw = out.view(a, b, kh, kw) if out is not None else \
+                torch.empty([a, b, kh, kw], dtype=torch.float32, device=g.device)
+            with _hip.zeroed_accumulators(out is not None):
+                _hip.check(_hip.lib().sg2_conv2d_wgrad_oikk(
+                    _hip.ptr(dw), _hip.ptr(ga), _hip.ptr(xa), dt, n, a, oh, ow, b, h, w, kh, kw, stride,
+                    pad[0], pad[1], float(alpha), _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad_oikk')
+            return dw
+    dw = out.view(a, kh, kw, b) if out is not None else torch.empty([a, kh, kw, b], dtype=torch.float32, device=g.device)
     with _hip.zeroed_accumulators(out is not None):
         _hip.check(_hip.lib().sg2_conv2d_wgrad(
             _hip.ptr(dw), _hip.ptr(ga), _hip.ptr(xa), dt, n, a, oh, ow, b, h, w, kh, kw, stride,

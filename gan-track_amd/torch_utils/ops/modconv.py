@@ -208,7 +208,8 @@ def _scaled_input_grads(dc, x, styles, weight, need_x, need_s, need_w, stride, p
         ds = ds.to(styles.dtype) if want_ds else None
         dx = dx if need_x else None
     if need_w and not _cg.weight_gradients_disabled:
-        dw = _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32, alpha=wgain, out=acc_dw).to(weight.dtype)
+        dw = _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32, alpha=wgain, out=acc_dw,
+                            param_layout=True).to(weight.dtype)
     return dx, ds, dw
 
 

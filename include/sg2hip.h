@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SG2_ABI_VERSION 8
+#define SG2_ABI_VERSION 9
 
 enum sg2_dtype { SG2_F32 = 0, SG2_F16 = 1, SG2_BF16 = 2, SG2_F32S3 = 3 };
 
@@ -216,6 +216,12 @@ int sg2_conv3x3_up2(void* y, const void* x, const void* w, int dtype, int N, int
 int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
                      int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, const float* g_scale,
                      const float* x_scale, float alpha, void* stream);
+
+/* sg2_conv2d_wgrad with dw written as float32 [A][B][KH][KW] -- torch's [O, I, kh, kw] parameter layout, so the
+ * gradient reaches the parameter without a layout copy (ABI 9).  SG2_F32S3 operands (the f32 layers) in
+ * deterministic mode only, B % 4 == 0: its fixed-order slot sum writes the transposed layout. */
+int sg2_conv2d_wgrad_oikk(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
+                          int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, float alpha, void* stream);
 
 /* Fused first-order backward of the layer epilogue z = c*d + noise + b, y = clamp(act(z)*gain):
  *   dc = dz * d;  db[o] = sum dz;  dd[n,o] = sum_p dz*c;  dnoise[n,p] = sum_o dz
