@@ -930,7 +930,7 @@ int launch_fwd(ConvArgs& a, bool vec, hipStream_t s) {
 // ------------------------------------------------------------------------------------ wgrad
 
 struct WgradArgs {
-    int oikk;            // sg2_conv2d_wgrad_oikk: the final slot sum writes dw as [A][B][KH][KW]
+    int oikk;            // sg2_conv2d_wgrad_oikk: the final slot sum writes dw as [A][B][KH][KW] (2: [B][A][KH][KW])
     const void* g;   // [N, OH, OW, A]
     const void* x;   // [N, H, W, B]
     float* dw;       // [A][KK][B]
@@ -1441,7 +1441,7 @@ int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
     }
     int rc = launch_status("sg2_conv2d_wgrad");
     if (rc || !a.det) return rc;
-    hipError_t e = a.oikk ? det_sum_oikk(a.dw, a.det, a.splits, a.A, KK, a.B, s)
+    hipError_t e = a.oikk ? det_sum_oikk(a.dw, a.det, a.splits, a.A, KK, a.B, a.oikk == 2, s)
                           : det_sum(a.dw, 0, a.det, 0, nel, 1, a.splits, nel, arena, s);
     if (e) { set_error("sg2_conv2d_wgrad: det_sum"); return (int)e; }
     return 0;
@@ -1685,12 +1685,12 @@ extern "C" int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dty
 
 extern "C" int sg2_conv2d_wgrad_oikk(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW,
                                      int B, int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, float alpha,
-                                     void* stream) {
+                                     int swap_ab, void* stream) {
     using namespace sg2;
     SG2_CHECK(dtype == SG2_F32S3 && det_on() && B % 4 == 0,
               "sg2_conv2d_wgrad_oikk: SG2_F32S3 operands in deterministic mode, B % 4 == 0");
     return conv2d_wgrad_impl(dw, g, x, dtype, N, A, OH, OW, B, H, W, KH, KW, stride, pad_y, pad_x, nullptr, nullptr,
-                             alpha, stream, 1);
+                             alpha, stream, swap_ab ? 2 : 1);
 }
 
 int sg2::conv2d_wgrad_impl(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,

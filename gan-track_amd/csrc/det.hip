@@ -128,10 +128,11 @@ __global__ __launch_bounds__(256) void det_sum_multi_kernel(DetJobs jobs) {
 }
 
 // det_sum into the parameter layout of a convolution weight gradient: the slots hold [A][KK][B] partials (the
-// kernels' K-major layout), out is [A][B][KK] (torch's [O, I, kh, kw]).  A lane owns four consecutive b of one
-// (a, tap) -- 16-byte loads, s in order -- and writes them KK floats apart.
+// kernels' K-major layout), out is [A][B][KK] (torch's [O, I, kh, kw]), or [B][A][KK] with swap (a transposed
+// convolution's weight, whose gradient is the call with g and x exchanged).  A lane owns four consecutive b of one
+// (a, tap) -- 16-byte loads, s in order -- and writes them KK (swap: A KK) floats apart.
 __global__ __launch_bounds__(256) void det_sum_oikk_kernel(float* out, const float* ws, int64_t S, int64_t nel, int KK,
-                                                           int B) {
+                                                           int B, int A, int swap) {
     const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;   // 4-element group of the [A][KK][B] slot layout
     if (q * 4 >= nel) return;
     const float4* w = (const float4*)ws + q;
@@ -154,8 +155,9 @@ __global__ __launch_bounds__(256) void det_sum_oikk_kernel(float* out, const flo
     const int64_t at = i / B;
     const int t = (int)(at % KK);
     const int64_t a = at / KK;
-    float* o = out + (a * B + b) * KK + t;
-    o[0] += acc.x; o[KK] += acc.y; o[2 * KK] += acc.z; o[3 * KK] += acc.w;
+    float* o = out + (swap ? (int64_t)b * A + a : a * B + b) * KK + t;     // swap: [B][A][KK]
+    const int64_t st = swap ? (int64_t)A * KK : KK;
+    o[0] += acc.x; o[st] += acc.y; o[2 * st] += acc.z; o[3 * st] += acc.w;
 }
 
 }  // namespace
@@ -202,11 +204,11 @@ hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t 
     return hipGetLastError();
 }
 
-hipError_t det_sum_oikk(float* out, const float* ws, int64_t S, int A, int KK, int B, hipStream_t st) {
+hipError_t det_sum_oikk(float* out, const float* ws, int64_t S, int A, int KK, int B, int swap, hipStream_t st) {
     const int64_t nel = (int64_t)A * KK * B;
     if (nel == 0 || S <= 0) return hipSuccess;
     if (B % 4 || (uintptr_t)ws % 16) return hipErrorInvalidValue;
-    det_sum_oikk_kernel<<<(unsigned)cdiv(nel / 4, 256), 256, 0, st>>>(out, ws, S, nel, KK, B);
+    det_sum_oikk_kernel<<<(unsigned)cdiv(nel / 4, 256), 256, 0, st>>>(out, ws, S, nel, KK, B, A, swap);
     return hipGetLastError();
 }
 

@@ -77,9 +77,9 @@ struct DetSumJob {
     int64_t S, n;
 };
 hipError_t det_sum_multi(const DetSumJob* jobs, int count, DetArena& arena, hipStream_t st);
-// out[a][b][t] += sum_{s < S} ws[s][a][t][b] (t < KK, B % 4 == 0): a weight gradient's slots into torch's
-// [O, I, kh, kw] layout (sg2_conv2d_wgrad_oikk).
-hipError_t det_sum_oikk(float* out, const float* ws, int64_t S, int A, int KK, int B, hipStream_t st);
+// out[a][b][t] (swap: out[b][a][t]) += sum_{s < S} ws[s][a][t][b] (t < KK, B % 4 == 0): a weight gradient's slots
+// into torch's [O, I, kh, kw] layout (sg2_conv2d_wgrad_oikk).
+hipError_t det_sum_oikk(float* out, const float* ws, int64_t S, int A, int KK, int B, int swap, hipStream_t st);
 #define SG2_DET_GET(ptr, arena, n, what)                                                        \
     do {                                                                                       \
         (ptr) = (arena).get(n);                                                                \

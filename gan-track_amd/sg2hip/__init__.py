@@ -60,7 +60,7 @@ SIGNATURES = {
                        _vp, _vp, _vp],
     'sg2_conv3x3_up2': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp],
     'sg2_conv2d_wgrad': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _f, _vp],
-    'sg2_conv2d_wgrad_oikk': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp],
+    'sg2_conv2d_wgrad_oikk': [_vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _f, _i, _vp],
     'sg2_upfirdn2d_lim': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i,
                           _i, _f, _vp, _vp],
     'sg2_upfirdn2d_fused': [_vp, _vp, _vp, _i, _c_i64p, _c_i64p, _c_i64p, _c_i64p, _i, _i, _i, _i, _i, _i, _i, _i, _i,

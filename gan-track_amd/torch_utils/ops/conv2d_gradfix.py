@@ -227,20 +227,22 @@ def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None, alpha=1.0,
     out: a zeroed f32 buffer of A*kh*kw*B elements to accumulate into (the call skips its memset).
     param_layout: where the library can (f32 layers under the deterministic reductions, sg2_conv2d_wgrad_oikk),
     write dw contiguous in [A, B, kh, kw] -- the parameter's own layout, which autograd's gradient accumulation then
-    takes as is instead of copying a permuted view."""
+    takes as is instead of copying a permuted view; 'swap': contiguous [B, A, kh, kw], returned as its [A, B, kh, kw]
+    view (a transposed conv's weight gradient, whose caller transposes A and B back)."""
     n, a, oh, ow = g.shape
     _, b, h, w = x.shape
     ga, xa, dt, gs, xs = g, x, _hip.dtype_code(g), g_scale, x_scale
     if _p3(g, 8) and a % 8 == 0 and b % 8 == 0 and not (kh == 1 and kw == 1 and min(a, b) <= 4):
         ga, xa, dt, gs, xs = split3(_nhwc(g), g_scale), split3(_nhwc(x), x_scale), _hip.F32S3, None, None
-        if param_layout and _hip.det_active():
-            dw = out.view(a, b, kh, kw) if out is not None else \
-                torch.empty([a, b, kh, kw], dtype=torch.float32, device=g.device)
+        if param_layout and _hip.det_active() and b % 4 == 0:
+            swap = param_layout == 'swap'
+            shape = [b, a, kh, kw] if swap else [a, b, kh, kw]
+            dw = out.view(*shape) if out is not None else torch.empty(shape, dtype=torch.float32, device=g.device)
             with _hip.zeroed_accumulators(out is not None):
                 _hip.check(_hip.lib().sg2_conv2d_wgrad_oikk(
                     _hip.ptr(dw), _hip.ptr(ga), _hip.ptr(xa), dt, n, a, oh, ow, b, h, w, kh, kw, stride,
-                    pad[0], pad[1], float(alpha), _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad_oikk')
-            return dw
+                    pad[0], pad[1], float(alpha), int(swap), _hip.stream_ptr(g.device)), 'sg2_conv2d_wgrad_oikk')
+            return dw.transpose(0, 1) if swap else dw
     dw = out.view(a, kh, kw, b) if out is not None else torch.empty([a, kh, kw, b], dtype=torch.float32, device=g.device)
     with _hip.zeroed_accumulators(out is not None):
         _hip.check(_hip.lib().sg2_conv2d_wgrad(

@@ -404,11 +404,13 @@ class _LayerVJP(torch.autograd.Function):
                 g_s = gsc if g_s is None else g_s + gsc
         if need[3] and (G is not None or hscale is not None):
             acc = torch.zeros([cout * kh * kw * cin], dtype=torch.float32, device=x.device)
+            # (both calls take the same kernel path, so they agree on acc's layout; the returned view reads it)
             if G is not None:
-                _cg._wgrad_raw(dc, G, kh, kw, stride, (pad, pad), alpha=wgain, out=acc)
+                g_w = _cg._wgrad_raw(dc, G, kh, kw, stride, (pad, pad), alpha=wgain, out=acc, param_layout=True)
             if hscale is not None:
-                _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32, g_scale=hscale, alpha=wgain, out=acc)
-            g_w = acc.view(cout, kh, kw, cin).permute(0, 3, 1, 2).to(weight.dtype)
+                g_w = _cg._wgrad_raw(dc, x, kh, kw, stride, (pad, pad), x_scale=s32, g_scale=hscale, alpha=wgain,
+                                     out=acc, param_layout=True)
+            g_w = g_w.to(weight.dtype)
         g_s = g_s.to(styles.dtype) if g_s is not None else None
         return (g_dy, g_x, g_s, g_w, g_d) + (None,) * 12
 
@@ -601,7 +603,8 @@ class UpModConv(torch.autograd.Function):
                     dx, _ = _cg.conv_fused(dt_, _cg._pack_conv(weight.transpose(0, 1), dt), cin, h, w, kh, kw, 2, tpad, out_scale=s32)
                 dx = dx if need[0] else None
             if need[2] and not _cg.weight_gradients_disabled:
-                dw = _cg._wgrad_raw(x, dt_, kh, kw, 2, tpad, g_scale=s32).transpose(0, 1).to(weight.dtype)
+                dw = _cg._wgrad_raw(x, dt_, kh, kw, 2, tpad, g_scale=s32, param_layout='swap').transpose(0, 1) \
+                    .to(weight.dtype)
         else:
             wt = weight.to(dt).transpose(0, 1)                # conv_transpose2d weight [Cin, Cout, kh, kw]
             dz = _ba.bias_act_grad(dy, y, act='lrelu', alpha=alpha, gain=gain, clamp=clamp)
@@ -719,11 +722,12 @@ class _UpLayerVJP(torch.autograd.Function):
                     g_x = gxc
         if need[3] and (G is not None or hscale is not None):
             acc = torch.zeros([cin * kh * kw * cout], dtype=torch.float32, device=x.device)
+            # (the transposed conv's weight: the [cin, cout] gradient transposed, written so where the library can)
             if G is not None:
-                _cg._wgrad_raw(G, u, kh, kw, 2, tpad, out=acc)
+                g_w = _cg._wgrad_raw(G, u, kh, kw, 2, tpad, out=acc, param_layout='swap')
             if hscale is not None:
-                _cg._wgrad_raw(x, u, kh, kw, 2, tpad, g_scale=s32, x_scale=hscale, out=acc)
-            g_w = acc.view(cin, kh, kw, cout).permute(3, 0, 1, 2).to(weight.dtype)
+                g_w = _cg._wgrad_raw(x, u, kh, kw, 2, tpad, g_scale=s32, x_scale=hscale, out=acc, param_layout='swap')
+            g_w = g_w.transpose(0, 1).to(weight.dtype)
         g_s = g_s.to(styles.dtype) if g_s is not None else None
         return (g_dy, g_x, g_s, g_w, g_d) + (None,) * 12
 
