@@ -1687,8 +1687,8 @@ extern "C" int sg2_conv2d_wgrad_oikk(float* dw, const void* g, const void* x, in
                                      int B, int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, float alpha,
                                      int swap_ab, void* stream) {
     using namespace sg2;
-    SG2_CHECK(dtype == SG2_F32S3 && det_on() && B % 4 == 0,
-              "sg2_conv2d_wgrad_oikk: SG2_F32S3 operands in deterministic mode, B % 4 == 0");
+    SG2_CHECK(dtype == SG2_F32S3 && det_on() && B % 4 == 0 && KH * KW <= 9 && A <= 65535,
+              "sg2_conv2d_wgrad_oikk: SG2_F32S3 operands in deterministic mode, B % 4 == 0, KH KW <= 9");
     return conv2d_wgrad_impl(dw, g, x, dtype, N, A, OH, OW, B, H, W, KH, KW, stride, pad_y, pad_x, nullptr, nullptr,
                              alpha, stream, swap_ab ? 2 : 1);
 }

@@ -234,7 +234,7 @@ def _wgrad_raw(g, x, kh, kw, stride, pad, x_scale=None, g_scale=None, alpha=1.0,
     ga, xa, dt, gs, xs = g, x, _hip.dtype_code(g), g_scale, x_scale
     if _p3(g, 8) and a % 8 == 0 and b % 8 == 0 and not (kh == 1 and kw == 1 and min(a, b) <= 4):
         ga, xa, dt, gs, xs = split3(_nhwc(g), g_scale), split3(_nhwc(x), x_scale), _hip.F32S3, None, None
-        if param_layout and _hip.det_active() and b % 4 == 0:
+        if param_layout and _hip.det_active() and b % 4 == 0 and kh * kw <= 9:
             swap = param_layout == 'swap'
             shape = [b, a, kh, kw] if swap else [a, b, kh, kw]
             dw = out.view(*shape) if out is not None else torch.empty(shape, dtype=torch.float32, device=g.device)

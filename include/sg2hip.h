@@ -220,7 +220,8 @@ int sg2_conv2d_wgrad(float* dw, const void* g, const void* x, int dtype, int N, 
 /* sg2_conv2d_wgrad with dw written as float32 [A][B][KH][KW] -- torch's [O, I, kh, kw] parameter layout, so the
  * gradient reaches the parameter without a layout copy -- or, swap_ab != 0, as [B][A][KH][KW] (a transposed
  * convolution's weight, whose gradient is the call with g and x exchanged) (ABI 9).  SG2_F32S3 operands (the f32
- * layers) in deterministic mode only, B % 4 == 0: its fixed-order slot sum writes the transposed layout. */
+ * layers) in deterministic mode only, B % 4 == 0, KH * KW <= 9: its fixed-order slot sum writes the transposed
+ * layout. */
 int sg2_conv2d_wgrad_oikk(float* dw, const void* g, const void* x, int dtype, int N, int A, int OH, int OW, int B,
                           int H, int W, int KH, int KW, int stride, int pad_y, int pad_x, float alpha, int swap_ab,
                           void* stream);
