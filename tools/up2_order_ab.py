@@ -1,7 +1,9 @@
 """A/B of the up-2 transposed conv's workgroup order (SG2_UP2_ORDER: 0 channel-block major, 1 XCD-contiguous
 tile-major) on the up / D-dgrad shapes of the bench networks (GPU): time per launch, alternating, and the two
 outputs compared bitwise (the order changes which workgroup computes a tile, not the arithmetic).
-    python tools/up2_order_ab.py"""
+    python tools/up2_order_ab.py
+(The XCD order measured slower, profiles/r06ay/, and was removed with its switch: in today's tree both legs run
+the block-major order.)"""
 import os
 import sys
 
