@@ -276,3 +276,34 @@ def test_det_affine_grid_sample_bwd_singular():
         u = fn().clone()
     w = fn()
     assert rel_err(u, ref) < 1e-5 and rel_err(w, ref) < 1e-5, (rel_err(u, ref), rel_err(w, ref))
+
+
+@pytest.mark.parametrize('geom', [(512, 512, 3, 1, 1, 2, 8, 8), (64, 40, 3, 1, 1, 3, 10, 9), (40, 104, 3, 2, 0, 2, 17, 17),
+                                  (48, 136, 1, 1, 0, 2, 12, 12), (8, 520, 3, 1, 1, 1, 4, 4)])
+@pytest.mark.parametrize('layout', [True, 'swap'])
+def test_det_wgrad_param_layout(geom, layout):
+    """The f32 weight gradient's fixed-order slot sum written straight into the parameter layout
+    (sg2_conv2d_wgrad_oikk: [A, B, kh, kw], or [B, A, kh, kw] for 'swap'; an LDS-transposed tile of one a x 64 b per
+    workgroup): contiguous in that layout, deterministic, equal to the K-major slot sum's permuted view to the
+    rounding of its summation order, and to a float64
+    weight gradient; B not a multiple of 64, 1x1 and stride-2 forms included."""
+    from torch_utils.ops import conv2d_gradfix as cg
+    A, B, k, stride, pad, N, H, W = geom
+    g = torch.Generator().manual_seed(41)
+    x = _nhwc(torch.randn(N, B, H, W, generator=g), torch.float32)
+    oh, ow = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    gr = _nhwc(torch.randn(N, A, oh, ow, generator=g), torch.float32)
+    with sg2hip.deterministic():
+        p1 = cg._wgrad_raw(gr, x, k, k, stride, (pad, pad), alpha=0.5, param_layout=layout).clone()
+        p2 = cg._wgrad_raw(gr, x, k, k, stride, (pad, pad), alpha=0.5, param_layout=layout)
+        plain = cg._wgrad_raw(gr, x, k, k, stride, (pad, pad), alpha=0.5)
+        torch.cuda.synchronize()
+    assert p2.shape == (A, B, k, k)
+    assert (p2.transpose(0, 1) if layout == 'swap' else p2).is_contiguous()
+    assert torch.equal(p1, p2), 'parameter-layout weight gradient not deterministic'
+    ref = 0.5 * torch.nn.grad.conv2d_weight(x.double().cpu(), (A, B, k, k), gr.double().cpu(), stride=stride,
+                                            padding=pad)
+    e_plain = rel_err(p2, plain.double().cpu())
+    assert e_plain < 1e-6, f'parameter layout vs K-major slot sum {e_plain:.3g}'
+    e_ref = rel_err(p2, ref)
+    assert e_ref < 1e-5, f'parameter layout vs float64 {e_ref:.3g}'
