@@ -1420,9 +1420,11 @@ int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
     const int mt = (int)cdiv(a.A, BM), nt = (int)cdiv(a.B, BN);
     const int KK = a.KH * a.KW;
     const int chunks = (int)cdiv(a.M, BK);
-    // workgroups the pixel split aims at (every workgroup adds a BM x BN partial per tap with float atomics);
-    // SG2_CWGRAD_WGS overrides (tuning runs)
-    static const int target = [] { const char* e = getenv("SG2_CWGRAD_WGS"); return e ? std::max(1, atoi(e)) : 2048; }();
+    // workgroups the pixel split aims at (every workgroup adds a BM x BN partial per tap: float atomics, or a slot
+    // of the fixed-order sum); SG2_CWGRAD_WGS overrides (tuning runs).  1024 since the parameter-layout slot sum
+    // (fewer slots to sum): bench 777.3 / 778.7 img/s at 2048, 781.5 / 781.2 at 1024, 768-1536 level, 512 lower
+    // (profiles/r06be, r06bf)
+    static const int target = [] { const char* e = getenv("SG2_CWGRAD_WGS"); return e ? std::max(1, atoi(e)) : 1024; }();
     int splits = (int)std::max<int64_t>(1, std::min<int64_t>(chunks / 8, cdiv(target, (int64_t)mt * nt * KK)));
     a.kper = (int)cdiv(chunks, splits) * BK;
     a.splits = (int)cdiv(a.M, a.kper);
