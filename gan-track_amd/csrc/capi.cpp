@@ -1,4 +1,5 @@
 // ABI bookkeeping of libsg2hip: version and the per-thread last-error message.
+#include <cstdlib>
 #include <string>
 
 #include "sg2_common.h"
@@ -10,6 +11,10 @@ static thread_local bool g_acc_zeroed = false;
 bool accumulators_prezeroed() { return g_acc_zeroed; }
 static thread_local bool g_ws_clean = false;
 bool workspace_clean() { return g_ws_clean; }
+bool det_assign_on() {
+    static const bool on = [] { const char* e = getenv("SG2_DET_ASSIGN"); return !(e && e[0] == '0'); }();
+    return on;
+}
 // Process-wide, not per thread: autograd runs the backward passes of a deterministic scope on its own device
 // thread, whose calls must see the mode (sg2_set_deterministic is called between launches, never concurrently).
 static float* g_det_base = nullptr;

@@ -1443,8 +1443,8 @@ int launch_wgrad(WgradArgs& a, bool vec, hipStream_t s) {
     }
     int rc = launch_status("sg2_conv2d_wgrad");
     if (rc || !a.det) return rc;
-    hipError_t e = a.oikk ? det_sum_oikk(a.dw, a.det, a.splits, a.A, KK, a.B, a.oikk == 2, s)
-                          : det_sum(a.dw, 0, a.det, 0, nel, 1, a.splits, nel, arena, s);
+    hipError_t e = a.oikk ? det_sum_oikk(a.dw, a.det, a.splits, a.A, KK, a.B, a.oikk == 2, s, det_assign())
+                          : det_sum(a.dw, 0, a.det, 0, nel, 1, a.splits, nel, arena, s, det_assign());
     if (e) { set_error("sg2_conv2d_wgrad: det_sum"); return (int)e; }
     return 0;
 }
@@ -1576,7 +1576,7 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
             int rc1 = launch_status("sg2_conv2d (1x1, small Cin, dot)");
             if (rc1 || !base.e.det_dot) return rc1;
             hipError_t e = det_sum(base.e.dot_out, 0, base.e.det_dot, 0, (int64_t)N * Cout, 1, g.x, (int64_t)N * Cout,
-                                   arena, s);
+                                   arena, s, det_assign());
             if (e) { set_error("sg2_conv2d: det_sum"); return (int)e; }
             return 0;
         }
@@ -1658,7 +1658,7 @@ extern "C" int sg2_conv2d_fused(void* y, const void* x, const void* w, int dtype
         }
         if (rc == 0 && base.e.det_dot) {
             hipError_t e = det_sum(base.e.dot_out, Cout, base.e.det_dot, (int64_t)OH * OW * Cout, Cout, N,
-                                   (int64_t)OH * OW, Cout, arena, s);
+                                   (int64_t)OH * OW, Cout, arena, s, det_assign());
             if (e) { set_error("sg2_conv2d: det_sum"); return (int)e; }
         }
     });
@@ -1744,7 +1744,7 @@ int sg2::conv2d_wgrad_impl(float* dw, const void* g, const void* x, int dtype, i
 #undef WGB
         int rc1 = launch_status("sg2_conv2d_wgrad (1x1, small B)");
         if (rc1 || !a.det) return rc1;
-        e = det_sum(dw, 0, a.det, 0, (int64_t)A * B, 1, rows, (int64_t)A * B, arena, s);
+        e = det_sum(dw, 0, a.det, 0, (int64_t)A * B, 1, rows, (int64_t)A * B, arena, s, det_assign());
         if (e) { set_error("sg2_conv2d_wgrad: det_sum"); return (int)e; }
         return 0;
     }
@@ -1761,7 +1761,7 @@ int sg2::conv2d_wgrad_impl(float* dw, const void* g, const void* x, int dtype, i
 #undef WG1
         int rc1 = launch_status("sg2_conv2d_wgrad (1x1, small A)");
         if (rc1 || !a.det) return rc1;
-        e = det_sum(dw, 0, a.det, 0, (int64_t)A * B, 1, rows, (int64_t)A * B, arena, s);
+        e = det_sum(dw, 0, a.det, 0, (int64_t)A * B, 1, rows, (int64_t)A * B, arena, s, det_assign());
         if (e) { set_error("sg2_conv2d_wgrad: det_sum"); return (int)e; }
         return 0;
     }

@@ -449,7 +449,8 @@ int launch3_k(const Conv3Args& a, hipStream_t s) {
         SG2_DET_GET(b.det_dot, arena, (int64_t)grid.x * a.Cout, "sg2_conv3x3");
         kern<<<grid, 256, lds, s>>>(b);
         if (int rc = launch_status("sg2_conv3x3")) return rc;
-        hipError_t e = det_sum(a.dot_out, a.Cout, b.det_dot, (int64_t)tps * a.Cout, a.Cout, a.N, tps, a.Cout, arena, s);
+        hipError_t e = det_sum(a.dot_out, a.Cout, b.det_dot, (int64_t)tps * a.Cout, a.Cout, a.N, tps, a.Cout, arena, s,
+                               det_assign());
         if (e) { set_error("sg2_conv3x3: det_sum"); return (int)e; }
         return 0;
     }
@@ -829,7 +830,7 @@ int launch_c64p(const Conv3Args& a, hipStream_t s, int tiles, int grid) {
         if (e) { set_error("sg2_conv3x3 (c64 persistent): zero"); return (int)e; }
         kern<<<grid, 512, P_LDS, s>>>(b, tiles);
         if (int rc = launch_status("sg2_conv3x3 (c64 persistent)")) return rc;
-        e = det_sum(a.dot_out, P_C, b.det_dot, nslot, P_C, a.N, (int64_t)maxb * 8, P_C, arena, s);
+        e = det_sum(a.dot_out, P_C, b.det_dot, nslot, P_C, a.N, (int64_t)maxb * 8, P_C, arena, s, det_assign());
         if (e) { set_error("sg2_conv3x3 (c64 persistent): det_sum"); return (int)e; }
         return 0;
     }

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void det_sum_kernel(float* out, int64_t go, co
 constexpr int kVecS = 16;
 
 __global__ __launch_bounds__(256) void det_sum_vec4_kernel(float* out, int64_t go, const float* ws, int64_t gw,
-                                                           int64_t ss, int64_t S, int64_t n4) {
+                                                           int64_t ss, int64_t S, int64_t n4, int assign) {
     const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t g = blockIdx.y;
     if (i4 >= n4) return;
@@ -74,6 +74,10 @@ __global__ __launch_bounds__(256) void det_sum_vec4_kernel(float* out, int64_t g
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     float4* o = (float4*)(out + g * go) + i4;
+    if (assign) {
+        *o = acc;
+        return;
+    }
     float4 r = *o;
     r.x += acc.x; r.y += acc.y; r.z += acc.z; r.w += acc.w;
     *o = r;
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(256) void det_sum_multi_kernel(DetJobs jobs) {
 constexpr int kOikkB = 64, kOikkMaxKK = 9;
 
 __global__ __launch_bounds__(256) void det_sum_oikk_kernel(float* out, const float* ws, int64_t S, int64_t nel, int KK,
-                                                           int B, int A, int swap) {
+                                                           int B, int A, int swap, int assign) {
     __shared__ float tile[kOikkMaxKK][kOikkB + 1];
     const int a = blockIdx.y, b0 = blockIdx.x * kOikkB;
     const int nb = min(kOikkB, B - b0);
@@ -161,14 +165,14 @@ __global__ __launch_bounds__(256) void det_sum_oikk_kernel(float* out, const flo
     for (int e = threadIdx.x; e < nb * KK; e += 256) {
         const int bl = e / KK, t = e - bl * KK;
         float* o = out + (swap ? (int64_t)(b0 + bl) * A + a : (int64_t)a * B + b0 + bl) * KK + t;
-        *o += tile[t][bl];
+        *o = assign ? tile[t][bl] : *o + tile[t][bl];
     }
 }
 
 }  // namespace
 
 hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t ss, int G, int64_t S, int64_t n,
-                   DetArena& arena, hipStream_t st) {
+                   DetArena& arena, hipStream_t st, int assign) {
     if (G <= 0 || n <= 0 || S <= 0) return hipSuccess;
     if (G > 65535) return hipErrorInvalidValue;
     static const bool trace = getenv("SG2_DET_TRACE") != nullptr;   // diagnostics: one line per call (tools/)
@@ -178,7 +182,7 @@ hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t 
         (uintptr_t)ws % 16 == 0 && bx * G >= 512) {
         if (trace) fprintf(stderr, "DETSUM G=%d n=%lld S=%lld K=%lld\n", G, (long long)n, (long long)S, 1LL);
         det_sum_vec4_kernel<<<dim3((unsigned)cdiv(n / 4, 256), (unsigned)G, 1), 256, 0, st>>>(out, go, ws, gw, ss, S,
-                                                                                             n / 4);
+                                                                                             n / 4, assign);
         return hipGetLastError();
     }
     // few outputs over a long sum (a bias or dot reduction over every pixel block): first chunks of the s range in
@@ -205,15 +209,17 @@ hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t 
     }
     if (trace) fprintf(stderr, "DETSUM G=%d n=%lld S=%lld K=%lld\n", G, (long long)n, (long long)S0,
                        (long long)K);
-    det_sum_kernel<<<dim3((unsigned)bx, (unsigned)G, 1), 256, 0, st>>>(out, go, ws, gw, ss, S, n, S, 0, 0);
+    det_sum_kernel<<<dim3((unsigned)bx, (unsigned)G, 1), 256, 0, st>>>(out, go, ws, gw, ss, S, n, S, 0, assign);
     return hipGetLastError();
 }
 
-hipError_t det_sum_oikk(float* out, const float* ws, int64_t S, int A, int KK, int B, int swap, hipStream_t st) {
+hipError_t det_sum_oikk(float* out, const float* ws, int64_t S, int A, int KK, int B, int swap, hipStream_t st,
+                        int assign) {
     const int64_t nel = (int64_t)A * KK * B;
     if (nel == 0 || S <= 0) return hipSuccess;
     if (KK > kOikkMaxKK || A > 65535) return hipErrorInvalidValue;
-    det_sum_oikk_kernel<<<dim3((unsigned)cdiv(B, kOikkB), (unsigned)A), 256, 0, st>>>(out, ws, S, nel, KK, B, A, swap);
+    det_sum_oikk_kernel<<<dim3((unsigned)cdiv(B, kOikkB), (unsigned)A), 256, 0, st>>>(out, ws, S, nel, KK, B, A, swap,
+                                                                                                   assign);
     return hipGetLastError();
 }
 
@@ -246,7 +252,7 @@ hipError_t det_sum_multi(const DetSumJob* jobs, int count, DetArena& arena, hipS
         if (trace) fprintf(stderr, "DETSUM G=%d n=%lld S=%lld K=%lld\n", in.G, (long long)in.n, (long long)in.S,
                            (long long)K);
         DetJob& j = second.j[second.count++];
-        j = DetJob{in.out, ws, in.go, gw, ss, S, in.n, S, 0, 0, (int)bx, in.G, 1, nb2};
+        j = DetJob{in.out, ws, in.go, gw, ss, S, in.n, S, 0, in.assign, (int)bx, in.G, 1, nb2};
         nb2 += (int)(bx * in.G);
     }
     if (first.count) det_sum_multi_kernel<<<nb1, 256, 0, st>>>(first);

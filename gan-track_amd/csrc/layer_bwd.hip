@@ -335,7 +335,7 @@ extern "C" int sg2_vjp_axpy(void* out, const void* a, const float* sa, const voi
     else vjp_axpy_kernel<float><<<grid, 256, lds, s>>>(x);
     int rc = launch_status("sg2_vjp_axpy");
     if (rc || !x.det_dot) return rc;
-    hipError_t err = det_sum(dot, 0, x.det_dot, 0, (int64_t)N * C, 1, grid.x, (int64_t)N * C, arena, s);
+    hipError_t err = det_sum(dot, 0, x.det_dot, 0, (int64_t)N * C, 1, grid.x, (int64_t)N * C, arena, s, det_assign());
     if (err) { set_error("sg2_vjp_axpy: det_sum"); return err; }
     return 0;
 }
@@ -380,8 +380,8 @@ extern "C" int sg2_layer_bwd(void* dc, float* db, float* dd, float* dnoise, cons
     hipError_t err = hipSuccess;
     DetSumJob jobs[2];
     int nj = 0;
-    if (db) jobs[nj++] = DetSumJob{db, 0, a.det_db, 0, C, 1, (int64_t)grid.x * N, C};
-    if (dd) jobs[nj++] = DetSumJob{dd, 0, a.det_dd, 0, (int64_t)N * C, 1, grid.x, (int64_t)N * C};
+    if (db) jobs[nj++] = DetSumJob{db, 0, a.det_db, 0, C, 1, (int64_t)grid.x * N, C, det_assign()};
+    if (dd) jobs[nj++] = DetSumJob{dd, 0, a.det_dd, 0, (int64_t)N * C, 1, grid.x, (int64_t)N * C, det_assign()};
     err = det_sum_multi(jobs, nj, arena, s);
     if (err) { set_error("sg2_layer_bwd: det_sum"); return err; }
     return 0;

@@ -40,9 +40,16 @@ bool workspace_clean();
 // second replay inf / NaN, 7e-7 with this kernel).  A stand-alone memset node replays correctly
 // (tools/memset_graph_check.py); kernel nodes replay every time.
 hipError_t zero_fill(void* p, size_t bytes, hipStream_t s);
+bool det_on();
+// In deterministic mode every accumulator output that zero_acc clears is written by exactly one fixed-order slot sum
+// of the same entry call, which then assigns (det_assign) instead of adding into zeros: no fill launch (a 4.6 us
+// launch each, 45 per training step, profiles/r06bj_zero_fill_sites.txt).  A caller's pre-zeroed buffer
+// (sg2_set_zeroed_accumulators: possibly accumulating several calls) is added into as before.
+bool det_assign_on();   // SG2_DET_ASSIGN=0: the former fill + add (an A/B switch)
 inline hipError_t zero_acc(void* p, size_t bytes, hipStream_t s) {
-    return accumulators_prezeroed() ? hipSuccess : zero_fill(p, bytes, s);
+    return (accumulators_prezeroed() || (det_on() && det_assign_on())) ? hipSuccess : zero_fill(p, bytes, s);
 }
+inline int det_assign() { return (accumulators_prezeroed() || !det_assign_on()) ? 0 : 1; }
 
 // Deterministic mode (sg2_set_deterministic, process-wide).  Every float accumulation that the fast path
 // makes with atomics (split-K partial sums, weight-gradient pixel splits, per-channel dot / bias / demod
@@ -65,7 +72,7 @@ class DetArena {
 // increasing order four outputs a lane; det.hip), one launch, or two (a chunk pass into `arena`) for few outputs
 // over many slots.
 hipError_t det_sum(float* out, int64_t go, const float* ws, int64_t gw, int64_t ss, int G, int64_t S, int64_t n,
-                   DetArena& arena, hipStream_t st);
+                   DetArena& arena, hipStream_t st, int assign = 0);   // assign: out = instead of out +=
 // Up to four independent det_sum calls in (at most) two launches: the chunk passes of those that need one
 // together, then the final sums together; each job's order is det_sum's.
 struct DetSumJob {
@@ -75,11 +82,13 @@ struct DetSumJob {
     int64_t gw, ss;
     int G;
     int64_t S, n;
+    int assign;     // out = instead of out +=
 };
 hipError_t det_sum_multi(const DetSumJob* jobs, int count, DetArena& arena, hipStream_t st);
 // out[a][b][t] (swap: out[b][a][t]) += sum_{s < S} ws[s][a][t][b] (t < KK, B % 4 == 0): a weight gradient's slots
 // into torch's [O, I, kh, kw] layout (sg2_conv2d_wgrad_oikk).
-hipError_t det_sum_oikk(float* out, const float* ws, int64_t S, int A, int KK, int B, int swap, hipStream_t st);
+hipError_t det_sum_oikk(float* out, const float* ws, int64_t S, int A, int KK, int B, int swap, hipStream_t st,
+                        int assign = 0);
 #define SG2_DET_GET(ptr, arena, n, what)                                                        \
     do {                                                                                       \
         (ptr) = (arena).get(n);                                                                \

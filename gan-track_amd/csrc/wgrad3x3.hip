@@ -738,7 +738,7 @@ int wgrad3x3_launch(float* dw, const void* g, const void* x, const float* gscale
                           pad_x, alpha, s);
     if (rc || !a.det) return rc;
     const int64_t nel = (int64_t)A * KH * KW * B;
-    hipError_t e = det_sum(dw, 0, a.det, 0, nel, 1, a.det_slots, nel, arena, s);
+    hipError_t e = det_sum(dw, 0, a.det, 0, nel, 1, a.det_slots, nel, arena, s, det_assign());
     if (e) { set_error("sg2_conv2d_wgrad: det_sum"); return (int)e; }
     return 0;
 }

@@ -32,6 +32,9 @@ from . import upfirdn2d as _up
 _CL = torch.channels_last
 enabled = True         # switch for A/B tests against the composed (unfused) path
 prezero = os.environ.get('SG2_PREZERO', '1') != '0'   # one zero fill per layer backward (A/B switch)
+# deterministic mode: the library's slot sums assign the accumulators instead of adding into zeros, so the layer
+# backward allocates them unfilled (SG2_DET_ASSIGN=0: the former fill + add; the library reads the same switch)
+det_assign = os.environ.get('SG2_DET_ASSIGN', '1') != '0'
 fast_backward = True   # first-order backward through the fused kernels (A/B switch)
 fused_vjp = os.environ.get('SG2_FUSED_VJP', '1') != '0'   # create_graph input-gradient pass as one node (A/B)
 tap_enabled = os.environ.get('SG2_TORGB_TAP', '1') != '0'   # toRGB input gradient + next block's in one epilogue
@@ -430,7 +433,7 @@ def _fast_backward(need, dy, x, styles, weight, dcoefs, noise, bias, zsrc, c, st
     want_dw = need[2] and not _cg.weight_gradients_disabled
     sizes = [cout if (wide and want_db) else 0, n * cout if (wide and want_dd) else 0, n * cin if want_ds else 0,
              cout * kh * kw * cin if want_dw else 0]
-    if not prezero:
+    if not prezero or (det_assign and _cg._hip.det_active()):   # deterministic: each slot sum assigns (no fill)
         sizes = [0, 0, 0, 0]
     acc = torch.zeros([sum(sizes)], dtype=torch.float32, device=dy.device) if sum(sizes) else None
     parts, o = [], 0
