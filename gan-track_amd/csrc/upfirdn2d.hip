@@ -659,15 +659,16 @@ __device__ __forceinline__ void fir4_strip(const UpfParams& p, const vecT* base,
 
 // 4x4 filter, up = down = 1, channels-last: the FIR of every G up-layer and D down-layer pad-FIR.
 // A workgroup owns a TW x TH output tile x CG = 8 channel vectors (a whole 128-byte line of each
-// pixel, so no line is split between workgroups on different XCDs).  All loads of the
+// pixel, so no line is split between workgroups on different XCDs); CG = 4 with TW = 64 for 16-bit C = 32
+// (C5's 1024^2 layers: a 64-byte pixel, where 8-vector groups left half the lanes idle).  All loads of the
 // (TH+3) x (TW+3) input patch are issued before the first LDS write (one latency per tile, ~13
 // 16-byte loads in flight per lane).  Each lane then owns one column x one channel vector and slides
 // down the strip: every input row is read from LDS once (4 ds_read_b128) and feeds the up-to-4 output
 // rows that use it, 5.5 LDS reads per output instead of 16.  Blocks are renumbered so each XCD walks a
 // contiguous run of tiles (neighbouring tiles share halo rows in that XCD's L2).
-template <typename T, int TW, int TH>
+template <typename T, int TW, int TH, int CG = 8>
 __global__ __launch_bounds__(256, 2) void upfirdn_nhwc_f4s(UpfParams p) {
-    constexpr int V = VecN<T>::N, F = 4, CG = 8;
+    constexpr int V = VecN<T>::N, F = 4;
     constexpr int IW = TW + F - 1, IH = TH + F - 1, NIN = IW * IH * CG;
     constexpr int NL = (NIN + 255) / 256;
     static_assert(TW * CG == 256, "one lane per (column, channel vector)");
@@ -743,6 +744,20 @@ int launch(const UpfParams& p, bool vec, hipStream_t s) {
         // (narrow ragged widths, e.g. the 65- and 33-wide pad-FIR of D, waste up to half the shifted last
         // column tile: they stay on upfirdn_nhwc_f4)
         constexpr int TW = 32, TH = 8;
+        const char* e32 = getenv("SG2_FIR_C32");      // A/B: 0 = the 8-vector groups (read per launch: tests)
+        const bool c32_off = e32 && e32[0] == '0';
+        if (!c32_off && p.C / VecN<T>::N == 4 && (p.OW % 64 == 0 || p.OW >= 224)) {   // 16-bit C = 32
+            constexpr int TW4 = 64, CG4 = 4;
+            const int64_t blocks4 = (int64_t)p.N * cdiv(p.OH, TH) * cdiv(p.OW, TW4);
+            if (blocks4 < INT32_MAX) {
+                const size_t lds = (size_t)(TH + 3) * (TW4 + 3) * CG4 * 16;
+                auto k = upfirdn_nhwc_f4s<T, TW4, TH, CG4>;
+                static bool set4 = false;
+                if (!set4) { (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); set4 = true; }
+                k<<<(unsigned)blocks4, 256, lds, s>>>(p);
+                return launch_status("sg2_upfirdn2d");
+            }
+        }
         const int64_t blocks = (int64_t)p.N * cdiv(p.OH, TH) * cdiv(p.OW, TW) * cdiv(p.C / VecN<T>::N, 8);
         if (blocks < INT32_MAX) {
             const size_t lds = (size_t)(TH + 3) * (TW + 3) * 8 * 16;

@@ -134,6 +134,35 @@ def test_upfirdn2d_vec_path(dtype):
         assert rel_err(y.float(), r) < tol, kw
 
 
+@pytest.mark.parametrize('dtype', [torch.float16, torch.bfloat16])
+def test_upfirdn2d_f4s_c32(dtype, monkeypatch):
+    """The 4x4 FIR strip kernel's C = 32 form (16-bit: a 64-byte pixel, 64-column tiles of 4 channel vectors; C5's
+    1024^2 layers) vs the oracle, plain and with the fused layer epilogue, and bitwise against the 8-vector-group
+    form (SG2_FIR_C32=0: the same taps in the same order)."""
+    from torch_utils.ops import upfirdn2d
+    torch.manual_seed(9)
+    tol = {torch.float16: 2e-3, torch.bfloat16: 1e-2}[dtype]
+    f = upfirdn2d.setup_filter([1, 3, 3, 1])
+    for (n, h, w, pad) in [(2, 24, 128, [2, 1, 2, 1]), (1, 40, 256, [2, 2, 2, 2]), (3, 9, 227, [1, 2, 2, 1])]:
+        x = torch.randn(n, 32, h, w).to(dtype).float()
+        xd = x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+        monkeypatch.delenv('SG2_FIR_C32', raising=False)
+        y = upfirdn2d.upfirdn2d(xd, f.to(DEV), padding=pad, gain=4)
+        r = O.upfirdn2d(x, f, padding=pad, gain=4)
+        assert y.shape == r.shape
+        assert rel_err(y.float(), r) < tol, (n, h, w, pad)
+        f2 = f.to(DEV)                                 # (setup_filter makes the 4-tap filter 2-D)
+        s = (torch.rand(n, 32) + 0.5).to(DEV)
+        b = (torch.randn(32) * 0.1).to(DEV)
+        ye, _ = upfirdn2d.fir_fused(xd, f2, pad, gain=4.0, out_scale=s, bias=b, act=1, alpha=0.2,
+                                    act_gain=2 ** 0.5, clamp=256.0)
+        monkeypatch.setenv('SG2_FIR_C32', '0')
+        assert torch.equal(y, upfirdn2d.upfirdn2d(xd, f.to(DEV), padding=pad, gain=4)), (n, h, w, pad)
+        ye2, _ = upfirdn2d.fir_fused(xd, f2, pad, gain=4.0, out_scale=s, bias=b, act=1, alpha=0.2,
+                                     act_gain=2 ** 0.5, clamp=256.0)
+        assert torch.equal(ye, ye2), (n, h, w, pad)
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float16, torch.bfloat16])
 def test_upfirdn2d_up2_blocks(dtype, monkeypatch):
     """2x up-FIR on channels-last feature maps (upfirdn_nhwc_up2, a 2 x 2 output cell per lane; the adjoint of
